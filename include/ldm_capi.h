@@ -1,0 +1,200 @@
+/*
+ * ldm_capi.h — C ABI of the MI355X-native latent-diffusion hot path (libldm_amd.so).
+ *
+ * The reference (PrioteasaAndrei/music-style-transfer-ldm) has no native boundary: its hot path is
+ * nn.Module.__call__ -> ATen.  This header is the thin C ABI the drop-in Python
+ * modules (music-style-transfer-ldm_amd/models/ (*.py)) call through ctypes.  Each entry point names the
+ * reference code it replaces.
+ *
+ * Conventions
+ *   - Plain pointers + sizes; every tensor is a contiguous fp32 NCHW device buffer unless stated.
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream); every
+ *     launch goes on it, nothing is synchronised, nothing is allocated: workspaces come from the
+ *     caller (graph-capture safe, §8(b) "Ownership").
+ *   - Return 0 on success, otherwise a nonzero code; ldm_last_error() gives the message
+ *     (thread-local).  The Python layer raises RuntimeError with it.
+ */
+#ifndef LDM_CAPI_H
+#define LDM_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDM_CAPI_VERSION 1
+
+/* ---- errors / introspection --------------------------------------------------------------- */
+const char* ldm_last_error(void);
+int ldm_capi_version(void);
+/* Number of HIP devices visible to the runtime this library is bound to (no kernel launch). */
+int ldm_device_count(int* count);
+
+/* ---- 2-D convolution / transposed convolution -----------------------------------------------
+ * Replaces nn.Conv2d / nn.ConvTranspose2d (+ following BatchNorm2d(eval) / ReLU / Tanh / time-emb
+ * add / skip add) at model.py:16-25 (encoder), :37-46 (decoder), :61-79 (style encoder),
+ * :178-194 + :205-229 (UNet).  Implicit GEMM on f32 MFMA (v_mfma_f32_32x32x2_f32 /
+ * v_mfma_f32_16x16x4_f32), transposed convs as sub-pixel phases, fused epilogue. */
+typedef struct ldm_conv_desc {
+    int32_t B, Cin, Hin, Win;
+    int32_t Cout, Hout, Wout;
+    int32_t kh, kw, stride, pad, out_pad;
+    int32_t transposed; /* 0: Conv2d weight [Cout,Cin,kh,kw]; 1: ConvTranspose2d weight [Cin,Cout,kh,kw] */
+} ldm_conv_desc;
+
+enum {
+    LDM_ACT_NONE = 0,
+    LDM_ACT_RELU = 1,
+    LDM_ACT_TANH = 2,
+    LDM_ACT_TANH_HALF = 3, /* (tanh(x)+1)/2: decoder output rescale, model.py:371,:405,:498 */
+    LDM_ACT_GELU = 4       /* exact erf GELU (nn.GELU(), model.py:173)                     */
+};
+
+typedef struct ldm_epilogue {
+    const float* bias;      /* [Cout] or NULL                                                */
+    const float* bn_weight; /* eval-mode BatchNorm2d after bias (NULL = none): gamma [Cout]    */
+    const float* bn_bias;   /*   beta [Cout]                                                   */
+    const float* bn_mean;   /*   running_mean [Cout]                                           */
+    const float* bn_var;    /*   running_var [Cout]                                            */
+    float bn_eps;
+    int32_t act;            /* LDM_ACT_*                                                       */
+    const float* bcast_add; /* [B,Cout] added after act (UNet time embedding, model.py:206)   */
+    const float* skip_add;  /* [B,Cout,Hout,Wout] added after act (UNet skips, model.py:221) */
+} ldm_epilogue;
+
+typedef struct ldm_conv_plan {
+    int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32         */
+    int32_t tm, tn, wk;    /* MFMA tiles per wave along M / N, waves splitting K per block      */
+    int64_t packed_floats; /* size of the packed-weight buffer ldm_conv_pack_weight fills (0 = none) */
+} ldm_conv_plan;
+
+int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan);
+/* Force a specific plan (autotuning / tests).  Fills packed_floats; validates. */
+int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, ldm_conv_plan* plan);
+/* Re-lay the torch weight into the MFMA fragment order of `plan` (tap-major K, zero padded). */
+int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* w,
+                         float* packed, void* stream);
+/* y = epilogue(conv(x, w)).  `w` is the packed buffer for MFMA plans, the torch weight for direct. */
+int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
+                     const ldm_epilogue* ep, float* y, void* stream);
+
+/* ---- BatchNorm2d, train mode (model.py:18,21,24,39,42 under .train(); model.py:307,344-347) ----
+ * Batch statistics over (B,H,W) per channel, normalise in place, optional activation, and the
+ * running-stat update (momentum, unbiased variance) exactly as nn.BatchNorm2d.  save_mean /
+ * save_invstd [C] are written for the backward pass (may be NULL). */
+int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
+                        float* running_mean, float* running_var, float momentum, float eps, int32_t act,
+                        float* save_mean, float* save_invstd, void* stream);
+
+/* ---- eval-mode BatchNorm2d (+activation) as a standalone op, out-of-place (y may equal x) ------ */
+int ldm_batchnorm_eval(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
+                       const float* bias, const float* running_mean, const float* running_var, float eps, int32_t act,
+                       void* stream);
+
+/* ---- elementwise activation, out-of-place (y may equal x): ReLU / Tanh / (tanh+1)/2 / GELU ------ */
+int ldm_activation(const float* x, float* y, int64_t n, int32_t act, void* stream);
+
+/* ---- SinusoidalPositionEmbeddings.forward (model.py:239-246) alone: out [B,dim] ---------------- */
+int ldm_sinusoid_embed(const void* t, int32_t t_is_float, int32_t B, int32_t dim, const float* freqs, float* out,
+                       void* stream);
+
+/* ---- time MLP: SinusoidalPositionEmbeddings -> Linear -> GELU -> Linear (model.py:170-175,
+ * :239-246).  t: [B] int64 (t_is_float=0) or float32 (t_is_float=1); freqs [dim/2] = the
+ * reference's exp(arange(half)*-(ln 1e4/(half-1))) table; w1,w2 [dim,dim] torch Linear layout. */
+int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B, int32_t dim, const float* freqs,
+                         const float* w1, const float* b1, const float* w2, const float* b2, float* out,
+                         void* stream);
+
+/* ---- cross-attention core (nn.MultiheadAttention inside CrossAttention, model.py:126-160) -------
+ * q [B,E,L] (the Q in-projection output in NCHW token order), kv [B,2E,S] (K channels then V
+ * channels), out [B,E,L] = softmax((q*scale)^T k) v per head, written channel-major so the
+ * out-projection reads it as NCHW (the reference's two permutes, model.py:144-158, vanish). */
+int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
+                       int32_t L, int32_t S, float scale, void* stream);
+
+/* ---- DDPM forward noising q_sample (ForwardDiffusion.forward, model.py:102-115) ----------------
+ * z_t = sqrt(ab[t_b]) * x0 + sqrt(1-ab[t_b]) * eps.  coef_table [T,2] = {sqrt(ab), sqrt(1-ab)} per
+ * timestep (device), t [B] int64 (device).  t outside [0,T) yields NaN for that sample (the
+ * reference raises IndexError, model.py:107; the Python layer checks host-known t up front). */
+int ldm_q_sample(const float* x0, const float* eps, const float* coef_table, int32_t T, const int64_t* t, float* zt,
+                 int32_t B, int64_t per_sample, void* stream);
+/* predict_start_from_noise (model.py:117-124): x0 = (z_t - sqrt(1-ab) * eps) / sqrt(ab), table as above. */
+int ldm_predict_start(const float* zt, const float* eps, const float* coef_table, int32_t T, const int64_t* t,
+                      float* x0, int32_t B, int64_t per_sample, void* stream);
+/* Backward of the two gathers above: kind 0 (q_sample): grad_a = sqrt(ab)*g -> d x0, grad_b = sqrt(1-ab)*g
+ * -> d eps; kind 1 (predict_start): grad_a = g/sqrt(ab) -> d z_t, grad_b = -sqrt(1-ab)*g/sqrt(ab) -> d eps.
+ * Either output may be NULL. */
+int ldm_sched_backward(int32_t kind, const float* grad, const float* coef_table, int32_t T, const int64_t* t,
+                       float* grad_a, float* grad_b, int32_t B, int64_t per_sample, void* stream);
+/* One reverse step of style_conditioned_ddim_sample / content_style_ddim_sample (model.py:439-463):
+ * coef[4] = {sqrt(ab_t), sqrt(1-ab_t), sqrt(ab_next), sqrt(1-ab_next)} (device, uniform over the
+ * batch), eta as in the reference (deterministic term).  x is updated in place; x0_log / eps_log
+ * (may be NULL) receive pred_x0 / noise_pred clones.  Bitwise equal to the reference's fp32 op
+ * sequence for identical inputs (no FMA contraction). */
+int ldm_ddim_step(float* x, const float* eps, const float* coef, float eta, float* x0_log, float* eps_log,
+                  int64_t n, void* stream);
+
+/* ---- loss reductions (loss.py): kind 0 = mean((a-b)^2) (diffusion_loss :48-49, nn.MSELoss :35),
+ * kind 1 = mean(0.5*(a^2-1-log(a^2+1e-8))) (kl_regularization_loss :31-32, b unused).
+ * Deterministic: fixed partition, fp64 partials.  workspace >= 512 doubles; out is a device scalar. */
+int ldm_loss_forward(int32_t kind, const float* a, const float* b, int64_t n, void* workspace, float* out,
+                     void* stream);
+/* grad_a / grad_b (may be NULL) = d(loss)/d(a|b) * grad_out[0] (device scalar). */
+int ldm_loss_backward(int32_t kind, const float* a, const float* b, int64_t n, const float* grad_out, float* grad_a,
+                      float* grad_b, void* stream);
+
+/* ---- whole UNet forward (UNet.forward, model.py:196-231) and the DDIM sampling loop ------------- */
+typedef struct ldm_unet_weights {
+    /* conv layers in order enc1, enc2, enc3, enc4, bottleneck, dec4, dec3, dec2, dec1:
+     * packed (or raw, for direct plans) weights and biases */
+    const float* conv_w[9];
+    const float* conv_b[9];
+    ldm_conv_plan conv_plan[9];
+    /* cross_attention2 (E=256) then cross_attention1 (E=512): packed Q-proj / KV-proj / out-proj */
+    const float* ca_wq[2];
+    const float* ca_bq[2];
+    ldm_conv_plan ca_plan_q[2];
+    const float* ca_wkv[2];
+    const float* ca_bkv[2];
+    ldm_conv_plan ca_plan_kv[2];
+    const float* ca_wo[2];
+    const float* ca_bo[2];
+    ldm_conv_plan ca_plan_o[2];
+    /* time MLP */
+    const float* t_freqs;
+    const float* t_w1;
+    const float* t_b1;
+    const float* t_w2;
+    const float* t_b2;
+} ldm_unet_weights;
+
+typedef struct ldm_unet_shape {
+    int32_t B, C, H, W;   /* latent [B,C,H,W]; style s5 [B,256,H/4,W/4], s6 [B,512,H/8,W/8] */
+    int32_t nf;           /* num_filters (64)                                                   */
+} ldm_unet_shape;
+
+/* Workspace floats needed by ldm_unet_forward for this shape. */
+int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s);
+/* Fill the 9+6 conv plans of `w` for this shape (weights must then be packed by the caller). */
+int ldm_unet_make_plans(const ldm_unet_shape* s, ldm_unet_weights* w);
+/* Conv descriptors of the 9 convs + 6 projection GEMMs (index order as in ldm_unet_weights). */
+int ldm_unet_layer_desc(const ldm_unet_shape* s, int32_t layer, ldm_conv_desc* d);
+int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights* w, const float* z, const void* t,
+                     int32_t t_is_float, const float* s5, const float* s6, float* out, float* workspace,
+                     void* stream);
+
+/* Reverse loop (style_conditioned_ddim_sample model.py:409-465 / content_style_ddim_sample :503-559):
+ * x [B,C,H,W] updated in place over nsteps = len(times)-1 steps.  t_table [nsteps,B] int64 holds
+ * times[i] repeated over the batch, coef_table [nsteps,4] the per-step coefficients.  x0_logs /
+ * eps_logs (may be NULL) are [nsteps,B,C,H,W].  Only launches: the caller may capture the whole loop
+ * into one hipGraph (the Python layer does, with torch.cuda.CUDAGraph on the same stream). */
+int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
+                    const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
+                    float* x0_logs, float* eps_logs, float* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDM_CAPI_H */

@@ -1,0 +1,482 @@
+// Small fused kernels of the hot path: time MLP, cross-attention core, DDPM/DDIM scheduler updates,
+// train-mode BatchNorm, activations.  All fp32; elementwise op order mirrors the reference's
+// separate fp32 ATen ops exactly (no FMA contraction), so the scheduler updates are bitwise the
+// reference's for identical inputs.
+#include <algorithm>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace ldm {
+
+// ------------------------------------------------------------------------------------------------
+// time MLP (model.py:170-175, :239-246): one block per batch element, one thread per feature
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void time_mlp_kernel(const void* t, int t_is_float, int dim, const float* __restrict__ freqs,
+                                                       const float* __restrict__ w1, const float* __restrict__ b1,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* emb = sm;
+    float* hid = sm + dim;
+    const int b = blockIdx.x, i = threadIdx.x;
+    // time[:, None] * freqs[None, :] with int64 time promoted to fp32 (model.py:244)
+    const float tv = t_is_float ? ((const float*)t)[b] : (float)((const int64_t*)t)[b];
+    const int half = dim / 2;
+    if (i < dim) {
+        const float arg = tv * freqs[i < half ? i : i - half];
+        emb[i] = i < half ? sinf(arg) : cosf(arg);
+    }
+    __syncthreads();
+    if (i < dim) {
+        const float* wr = w1 + (size_t)i * dim;
+        float acc = 0.f;
+        for (int k = 0; k < dim; ++k) acc = fmaf(wr[k], emb[k], acc);
+        const float x = acc + b1[i];
+        // nn.GELU() (exact): x * 0.5 * (1 + erf(x / sqrt(2)))
+        hid[i] = x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+    }
+    __syncthreads();
+    if (i < dim) {
+        const float* wr = w2 + (size_t)i * dim;
+        float acc = 0.f;
+        for (int k = 0; k < dim; ++k) acc = fmaf(wr[k], hid[k], acc);
+        out[(size_t)b * dim + i] = acc + b2[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// cross-attention core: one block per (b, head, 16-query tile).  q [B,E,L], kv [B,2E,S] channel-major.
+// out[b][h*d+c][l] = sum_s softmax_s((q*scale)[.,l] . k[.,s]) v[c][s]
+// (torch.nn.functional.multi_head_attention_forward, need_weights=True path: q_scaled = q*sqrt(1/d),
+//  bmm, softmax, bmm; dropout 0 in nn.MultiheadAttention(E, 4) as built at model.py:132)
+// ------------------------------------------------------------------------------------------------
+constexpr int kAttnLT = 16;
+
+__global__ __launch_bounds__(256) void attention_core_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                             float* __restrict__ out, int E, int heads, int L, int S,
+                                                             float scale) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int d = E / heads;
+    const int ltiles = (L + kAttnLT - 1) / kAttnLT;
+    const int lt = blockIdx.x % ltiles;
+    const int h = (blockIdx.x / ltiles) % heads;
+    const int b = blockIdx.x / (ltiles * heads);
+    const int l0 = lt * kAttnLT;
+    const int nl = min(kAttnLT, L - l0);
+    float* Qs = sm;                    // [d][LT]
+    float* Ks = Qs + d * kAttnLT;      // [d][S]
+    float* Vs = Ks + d * S;            // [d][S]
+    float* Ps = Vs + d * S;            // [LT][S]
+    const float* qb = q + ((size_t)b * E + (size_t)h * d) * L;
+    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * d) * S;
+    const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * d) * S;
+    for (int e = threadIdx.x; e < d * kAttnLT; e += blockDim.x) {
+        const int c = e / kAttnLT, l = e - c * kAttnLT;
+        Qs[e] = l < nl ? qb[(size_t)c * L + l0 + l] * scale : 0.f;
+    }
+    for (int e = threadIdx.x; e < d * S; e += blockDim.x) {
+        Ks[e] = kb[e];
+        Vs[e] = vb[e];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kAttnLT * S; e += blockDim.x) {
+        const int l = e / S, s = e - l * S;
+        float acc = 0.f;
+        for (int c = 0; c < d; ++c) acc = fmaf(Qs[c * kAttnLT + l], Ks[c * S + s], acc);
+        Ps[e] = acc;
+    }
+    __syncthreads();
+    // softmax over s: one wave per query row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int l = wave; l < nl; l += nw) {
+        float* row = Ps + l * S;
+        float mx = -INFINITY;
+        for (int s = lane; s < S; s += 64) mx = fmaxf(mx, row[s]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        float sum = 0.f;
+        for (int s = lane; s < S; s += 64) {
+            const float ex = expf(row[s] - mx);
+            row[s] = ex;
+            sum += ex;
+        }
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        for (int s = lane; s < S; s += 64) row[s] = row[s] / sum;
+    }
+    __syncthreads();
+    float* ob = out + ((size_t)b * E + (size_t)h * d) * L;
+    for (int e = threadIdx.x; e < d * kAttnLT; e += blockDim.x) {
+        const int c = e / kAttnLT, l = e - c * kAttnLT;
+        if (l >= nl) continue;
+        float acc = 0.f;
+        const float* pr = Ps + l * S;
+        const float* vr = Vs + c * S;
+        for (int s = 0; s < S; ++s) acc = fmaf(pr[s], vr[s], acc);
+        ob[(size_t)c * L + l0 + l] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// scheduler updates
+// ------------------------------------------------------------------------------------------------
+// coef_table [T,2] = {sqrt(ab), sqrt(1-ab)} per timestep (host-computed with the reference's fp32
+// torch.sqrt); t [B] int64 on device.  An out-of-range t (the reference raises IndexError,
+// model.py:107) poisons the sample with NaN instead of reading out of bounds.
+__device__ __forceinline__ bool load_coef(const float* table, int T, const int64_t* t, int b, float& sa, float& s1) {
+    const int64_t tb = t[b];
+    if (tb < 0 || tb >= T) {
+        sa = s1 = __builtin_nanf("");
+        return false;
+    }
+    sa = table[2 * tb];
+    s1 = table[2 * tb + 1];
+    return true;
+}
+
+__global__ __launch_bounds__(256) void q_sample_kernel(const float* __restrict__ x0, const float* __restrict__ eps,
+                                                       const float* __restrict__ table, int T,
+                                                       const int64_t* __restrict__ t, float* __restrict__ zt,
+                                                       int64_t per_sample, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float sa, s1;
+    load_coef(table, T, t, (int)(i / per_sample), sa, s1);
+    // torch.sqrt(alpha_bar_t) * x_0 + torch.sqrt(1 - alpha_bar_t) * eps   (model.py:113)
+    const float u = sa * x0[i];
+    const float v = s1 * eps[i];
+    zt[i] = u + v;
+}
+
+__global__ __launch_bounds__(256) void predict_start_kernel(const float* __restrict__ zt, const float* __restrict__ eps,
+                                                            const float* __restrict__ table, int T,
+                                                            const int64_t* __restrict__ t, float* __restrict__ x0,
+                                                            int64_t per_sample, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float sa, s1;
+    load_coef(table, T, t, (int)(i / per_sample), sa, s1);
+    // (z_t - torch.sqrt(1 - alpha_bar_t) * noise_pred) / torch.sqrt(alpha_bar_t)   (model.py:124)
+    const float v = s1 * eps[i];
+    x0[i] = (zt[i] - v) / sa;
+}
+
+// backward of q_sample (kind 0: ga = sa*g, gb = s1*g) and predict_start (kind 1: ga = g/sa, gb = -(s1*g)/sa)
+__global__ __launch_bounds__(256) void sched_backward_kernel(int kind, const float* __restrict__ g,
+                                                             const float* __restrict__ table, int T,
+                                                             const int64_t* __restrict__ t, float* __restrict__ ga,
+                                                             float* __restrict__ gb, int64_t per_sample, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float sa, s1;
+    load_coef(table, T, t, (int)(i / per_sample), sa, s1);
+    const float gv = g[i];
+    if (kind == 0) {
+        if (ga) ga[i] = sa * gv;
+        if (gb) gb[i] = s1 * gv;
+    } else {
+        if (ga) ga[i] = gv / sa;
+        if (gb) gb[i] = -(s1 * gv) / sa;
+    }
+}
+
+__global__ __launch_bounds__(256) void ddim_step_kernel(float* __restrict__ x, const float* __restrict__ eps,
+                                                        const float* __restrict__ coef, float eta,
+                                                        float* __restrict__ x0_log, float* __restrict__ eps_log,
+                                                        int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float sat = coef[0], s1t = coef[1], san = coef[2], s1n = coef[3];
+    const float e = eps[i];
+    const float xv = x[i];
+    // model.py:446-458, one fp32 rounding per reference op
+    const float dxt = s1t * e;                 // sqrt(1-ab_t) * noise_pred (also inside predict_start)
+    const float x0 = (xv - dxt) / sat;         // predict_start_from_noise
+    const float dxn = s1n * e;                 // direction_xt_next
+    const float nc = eta * (dxn - dxt);        // noise_contribution
+    const float t1 = san * x0;
+    x[i] = (t1 + dxn) + nc;
+    if (x0_log) x0_log[i] = x0;
+    if (eps_log) eps_log[i] = e;
+}
+
+// ------------------------------------------------------------------------------------------------
+// train-mode BatchNorm2d: one block per channel; fp64 statistics like aten's CPU kernel
+// (batch_norm_cpu_collect_stats: accscalar_t = double), then x*alpha+beta and activation.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double block_sum_double(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < nw; ++w) s += red[w];
+    return s;
+}
+
+__global__ __launch_bounds__(1024) void batchnorm_train_kernel(float* __restrict__ x, int B, int C, int HW,
+                                                                const float* __restrict__ weight,
+                                                                const float* __restrict__ bias,
+                                                                float* __restrict__ rmean, float* __restrict__ rvar,
+                                                                float momentum, float eps, int act,
+                                                                float* __restrict__ save_mean,
+                                                                float* __restrict__ save_invstd) {
+    __shared__ double red[16];
+    const int c = blockIdx.x;
+    const int64_t n = (int64_t)B * HW;
+    double s = 0.0;
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
+        s += (double)x[((size_t)b * C + c) * HW + p];
+    }
+    const double mean = block_sum_double(s, red) / (double)n;
+    double q = 0.0;
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
+        const double dv = (double)x[((size_t)b * C + c) * HW + p] - mean;
+        q += dv * dv;
+    }
+    const double var_sum = block_sum_double(q, red);
+    const float mean_f = (float)mean;
+    const float invstd = (float)(1.0 / sqrt(var_sum / (double)n + (double)eps));
+    const float alpha = invstd * (weight ? weight[c] : 1.0f);
+    const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
+        float* px = x + ((size_t)b * C + c) * HW + p;
+        const float v = *px * alpha + beta;
+        *px = apply_act(v, act);
+    }
+    if (threadIdx.x == 0) {
+        if (rmean) rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+        if (rvar) {
+            const double unbiased = n > 1 ? var_sum / (double)(n - 1) : var_sum;
+            rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
+        }
+        if (save_mean) save_mean[c] = mean_f;
+        if (save_invstd) save_invstd[c] = invstd;
+    }
+}
+
+__global__ __launch_bounds__(256) void activation_kernel(const float* x, float* y, int64_t n, int act) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = apply_act(x[i], act);
+}
+
+__global__ __launch_bounds__(256) void batchnorm_eval_kernel(const float* x, float* y, int C, int HW, int64_t n,
+                                                             const float* __restrict__ w, const float* __restrict__ b,
+                                                             const float* __restrict__ rm, const float* __restrict__ rv,
+                                                             float eps, int act) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = (int)((i / HW) % C);
+    const float invstd = 1.0f / sqrtf(rv[c] + eps);
+    const float alpha = invstd * (w ? w[c] : 1.0f);
+    const float beta = (b ? b[c] : 0.0f) - rm[c] * alpha;
+    y[i] = apply_act(x[i] * alpha + beta, act);
+}
+
+__global__ __launch_bounds__(256) void sinusoid_kernel(const void* t, int t_is_float, int B, int dim,
+                                                       const float* __restrict__ freqs, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * dim) return;
+    const int b = i / dim, k = i - b * dim, half = dim / 2;
+    const float tv = t_is_float ? ((const float*)t)[b] : (float)((const int64_t*)t)[b];
+    const float arg = tv * freqs[k < half ? k : k - half];
+    out[i] = k < half ? sinf(arg) : cosf(arg);
+}
+
+// ------------------------------------------------------------------------------------------------
+// loss reductions (deterministic: fixed block partition, fp64 partials, one final block)
+//   kind 0: mean((a-b)^2)                                  F.mse_loss / nn.MSELoss (loss.py:35,49)
+//   kind 1: mean(0.5*(a^2 - 1 - log(a^2 + 1e-8)))          kl_regularization_loss (loss.py:31-32)
+// ------------------------------------------------------------------------------------------------
+constexpr int kLossBlocks = 512;
+
+__device__ __forceinline__ float loss_term(int kind, float a, float b) {
+    if (kind == 0) {
+        const float d = a - b;
+        return d * d;
+    }
+    const float a2 = a * a;
+    return 0.5f * ((a2 - 1.0f) - logf(a2 + 1e-8f));
+}
+
+__global__ __launch_bounds__(256) void loss_partial_kernel(int kind, const float* __restrict__ a,
+                                                           const float* __restrict__ b, int64_t n,
+                                                           double* __restrict__ partial) {
+    __shared__ double red[16];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        s += (double)loss_term(kind, a[i], b ? b[i] : 0.f);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+        partial[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(64) void loss_final_kernel(const double* __restrict__ partial, int np, int64_t n,
+                                                        float* __restrict__ out) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < np; i += 64) s += partial[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (threadIdx.x == 0) out[0] = (float)(s / (double)n);
+}
+
+// d/da of the mean loss times upstream scalar gradient g (device scalar)
+__global__ __launch_bounds__(256) void loss_backward_kernel(int kind, const float* __restrict__ a,
+                                                            const float* __restrict__ b, int64_t n,
+                                                            const float* __restrict__ g, float* __restrict__ ga,
+                                                            float* __restrict__ gb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float scale = g[0] / (float)n;
+    if (kind == 0) {
+        const float d = 2.0f * (a[i] - (b ? b[i] : 0.f)) * scale;
+        if (ga) ga[i] = d;
+        if (gb) gb[i] = -d;
+    } else {
+        // d/da 0.5*(a^2 - 1 - log(a^2+eps)) = a - a/(a^2+eps)
+        const float av = a[i];
+        const float a2 = av * av;
+        if (ga) ga[i] = (av - av / (a2 + 1e-8f)) * scale;
+    }
+}
+
+static unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B, int32_t dim, const float* freqs,
+                                    const float* w1, const float* b1, const float* w2, const float* b2, float* out,
+                                    void* stream) {
+    LDM_REQUIRE(t && freqs && w1 && b1 && w2 && b2 && out, "time_mlp: null argument");
+    LDM_REQUIRE(B > 0 && dim > 1 && dim % 2 == 0 && dim <= 256, "time_mlp: unsupported dim");
+    const int threads = (dim + 63) / 64 * 64;
+    hipLaunchKernelGGL(time_mlp_kernel, dim3(B), dim3(threads), 2 * dim * sizeof(float), (hipStream_t)stream, t,
+                       t_is_float, dim, freqs, w1, b1, w2, b2, out);
+    LDM_CHECK_LAUNCH("time_mlp_kernel");
+    return 0;
+}
+
+extern "C" int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
+                                  int32_t L, int32_t S, float scale, void* stream) {
+    LDM_REQUIRE(q && kv && out, "attention: null argument");
+    LDM_REQUIRE(B > 0 && heads > 0 && E % heads == 0 && L > 0 && S > 0, "attention: bad shape");
+    const int d = E / heads;
+    const size_t lds = ((size_t)d * kAttnLT + 2 * (size_t)d * S + (size_t)kAttnLT * S) * sizeof(float);
+    LDM_REQUIRE(lds <= 64 * 1024, "attention: head tile exceeds LDS budget");
+    const int ltiles = (L + kAttnLT - 1) / kAttnLT;
+    hipLaunchKernelGGL(attention_core_kernel, dim3(B * heads * ltiles), dim3(256), lds, (hipStream_t)stream, q, kv, out,
+                       E, heads, L, S, scale);
+    LDM_CHECK_LAUNCH("attention_core_kernel");
+    return 0;
+}
+
+extern "C" int ldm_q_sample(const float* x0, const float* eps, const float* coef_table, int32_t T, const int64_t* t,
+                            float* zt, int32_t B, int64_t per_sample, void* stream) {
+    LDM_REQUIRE(x0 && eps && coef_table && t && zt && B > 0 && per_sample > 0 && T > 0, "q_sample: bad argument");
+    const int64_t n = (int64_t)B * per_sample;
+    hipLaunchKernelGGL(q_sample_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x0, eps,
+                       coef_table, T, t, zt, per_sample, n);
+    LDM_CHECK_LAUNCH("q_sample_kernel");
+    return 0;
+}
+
+extern "C" int ldm_predict_start(const float* zt, const float* eps, const float* coef_table, int32_t T,
+                                 const int64_t* t, float* x0, int32_t B, int64_t per_sample, void* stream) {
+    LDM_REQUIRE(x0 && eps && coef_table && t && zt && B > 0 && per_sample > 0 && T > 0, "predict_start: bad argument");
+    const int64_t n = (int64_t)B * per_sample;
+    hipLaunchKernelGGL(predict_start_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, zt, eps,
+                       coef_table, T, t, x0, per_sample, n);
+    LDM_CHECK_LAUNCH("predict_start_kernel");
+    return 0;
+}
+
+extern "C" int ldm_sched_backward(int32_t kind, const float* grad, const float* coef_table, int32_t T, const int64_t* t,
+                                  float* grad_a, float* grad_b, int32_t B, int64_t per_sample, void* stream) {
+    LDM_REQUIRE(grad && coef_table && t && B > 0 && per_sample > 0 && T > 0 && (kind == 0 || kind == 1),
+                "sched_backward: bad argument");
+    const int64_t n = (int64_t)B * per_sample;
+    hipLaunchKernelGGL(sched_backward_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind, grad,
+                       coef_table, T, t, grad_a, grad_b, per_sample, n);
+    LDM_CHECK_LAUNCH("sched_backward_kernel");
+    return 0;
+}
+
+extern "C" int ldm_ddim_step(float* x, const float* eps, const float* coef, float eta, float* x0_log, float* eps_log,
+                             int64_t n, void* stream) {
+    LDM_REQUIRE(x && eps && coef && n > 0, "ddim_step: bad argument");
+    hipLaunchKernelGGL(ddim_step_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, eps, coef, eta,
+                       x0_log, eps_log, n);
+    LDM_CHECK_LAUNCH("ddim_step_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
+                                   float* running_mean, float* running_var, float momentum, float eps, int32_t act,
+                                   float* save_mean, float* save_invstd, void* stream) {
+    LDM_REQUIRE(x && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
+    hipLaunchKernelGGL(batchnorm_train_kernel, dim3(C), dim3(1024), 0, (hipStream_t)stream, x, B, C, HW, weight, bias,
+                       running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
+    LDM_CHECK_LAUNCH("batchnorm_train_kernel");
+    return 0;
+}
+
+extern "C" int ldm_activation(const float* x, float* y, int64_t n, int32_t act, void* stream) {
+    LDM_REQUIRE(x && y && n >= 0, "activation: bad argument");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(activation_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, y, n, act);
+    LDM_CHECK_LAUNCH("activation_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_eval(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
+                                  const float* bias, const float* running_mean, const float* running_var, float eps,
+                                  int32_t act, void* stream) {
+    LDM_REQUIRE(x && y && running_mean && running_var && B > 0 && C > 0 && HW > 0, "batchnorm_eval: bad argument");
+    const int64_t n = (int64_t)B * C * HW;
+    hipLaunchKernelGGL(batchnorm_eval_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, y, C, HW,
+                       n, weight, bias, running_mean, running_var, eps, act);
+    LDM_CHECK_LAUNCH("batchnorm_eval_kernel");
+    return 0;
+}
+
+extern "C" int ldm_sinusoid_embed(const void* t, int32_t t_is_float, int32_t B, int32_t dim, const float* freqs,
+                                  float* out, void* stream) {
+    LDM_REQUIRE(t && freqs && out && B > 0 && dim > 1 && dim % 2 == 0, "sinusoid: bad argument");
+    hipLaunchKernelGGL(sinusoid_kernel, dim3(blocks_for((int64_t)B * dim, 256)), dim3(256), 0, (hipStream_t)stream, t,
+                       t_is_float, B, dim, freqs, out);
+    LDM_CHECK_LAUNCH("sinusoid_kernel");
+    return 0;
+}
+
+extern "C" int ldm_loss_forward(int32_t kind, const float* a, const float* b, int64_t n, void* workspace, float* out,
+                                void* stream) {
+    LDM_REQUIRE(a && workspace && out && n > 0 && (kind == 0 || kind == 1), "loss_forward: bad argument");
+    LDM_REQUIRE(kind != 0 || b, "loss_forward: mse needs two inputs");
+    const int np = (int)std::min<int64_t>(kLossBlocks, (n + 255) / 256);
+    hipLaunchKernelGGL(loss_partial_kernel, dim3(np), dim3(256), 0, (hipStream_t)stream, kind, a, b, n,
+                       (double*)workspace);
+    LDM_CHECK_LAUNCH("loss_partial_kernel");
+    hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const double*)workspace, np, n, out);
+    LDM_CHECK_LAUNCH("loss_final_kernel");
+    return 0;
+}
+
+extern "C" int ldm_loss_backward(int32_t kind, const float* a, const float* b, int64_t n, const float* grad_out,
+                                 float* grad_a, float* grad_b, void* stream) {
+    LDM_REQUIRE(a && grad_out && n > 0 && (kind == 0 || kind == 1), "loss_backward: bad argument");
+    hipLaunchKernelGGL(loss_backward_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind, a, b, n,
+                       grad_out, grad_a, grad_b);
+    LDM_CHECK_LAUNCH("loss_backward_kernel");
+    return 0;
+}

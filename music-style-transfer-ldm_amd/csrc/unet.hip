@@ -1,0 +1,223 @@
+// Whole-UNet forward (UNet.forward, model.py:196-231) and the DDIM reverse loop
+// (style_conditioned_ddim_sample model.py:409-465 / content_style_ddim_sample :503-559) as one C call:
+// ~16 launches per denoising step, no host synchronisation, no allocation — the Python layer
+// captures the full loop into a single hipGraph.
+#include <cmath>
+
+#include "common.h"
+
+namespace ldm {
+
+// Layer index -> geometry.  0..8: enc1 enc2 enc3 enc4 bottleneck dec4 dec3 dec2 dec1 (model.py:178-194)
+// 9..14: [CA2 q, CA2 kv, CA2 out, CA1 q, CA1 kv, CA1 out] 1x1 projections of the packed
+// nn.MultiheadAttention in_proj / out_proj (model.py:132, :184-185).
+static int layer_desc(const ldm_unet_shape& s, int layer, ldm_conv_desc& d) {
+    LDM_REQUIRE(s.B > 0 && s.C > 0 && s.nf > 0, "unet: bad shape");
+    LDM_REQUIRE(s.H % 8 == 0 && s.W % 8 == 0 && s.H >= 8 && s.W >= 8,
+                "unet: latent H and W must be multiples of 8 (skip connections, model.py:221-227)");
+    LDM_REQUIRE(s.nf * 4 == 256, "unet: CrossAttention dims are fixed at 512/256 (model.py:184-185) -> num_filters 64");
+    d = ldm_conv_desc{};
+    d.B = s.B;
+    const int nf = s.nf;
+    const int H = s.H, W = s.W;
+    auto conv = [&](int cin, int hin, int win, int cout, int stride) {
+        d.Cin = cin;
+        d.Hin = hin;
+        d.Win = win;
+        d.Cout = cout;
+        d.kh = d.kw = 3;
+        d.stride = stride;
+        d.pad = 1;
+        d.out_pad = 0;
+        d.transposed = 0;
+        d.Hout = (hin + 2 - 3) / stride + 1;
+        d.Wout = (win + 2 - 3) / stride + 1;
+    };
+    auto convT = [&](int cin, int hin, int win, int cout) {
+        d.Cin = cin;
+        d.Hin = hin;
+        d.Win = win;
+        d.Cout = cout;
+        d.kh = d.kw = 3;
+        d.stride = 2;
+        d.pad = 1;
+        d.out_pad = 1;
+        d.transposed = 1;
+        d.Hout = 2 * hin;
+        d.Wout = 2 * win;
+    };
+    auto proj = [&](int cin, int cout, int hw) {
+        d.Cin = cin;
+        d.Hin = 1;
+        d.Win = hw;
+        d.Cout = cout;
+        d.kh = d.kw = 1;
+        d.stride = 1;
+        d.pad = 0;
+        d.out_pad = 0;
+        d.transposed = 0;
+        d.Hout = 1;
+        d.Wout = hw;
+    };
+    const int L2 = (H / 4) * (W / 4), L1 = (H / 8) * (W / 8);
+    switch (layer) {
+        case 0: conv(s.C, H, W, nf, 1); break;
+        case 1: conv(nf, H, W, 2 * nf, 2); break;
+        case 2: conv(2 * nf, H / 2, W / 2, 4 * nf, 2); break;
+        case 3: conv(4 * nf, H / 4, W / 4, 8 * nf, 2); break;
+        case 4: conv(8 * nf, H / 8, W / 8, 8 * nf, 1); break;
+        case 5: convT(8 * nf, H / 8, W / 8, 4 * nf); break;
+        case 6: convT(4 * nf, H / 4, W / 4, 2 * nf); break;
+        case 7: convT(2 * nf, H / 2, W / 2, nf); break;
+        case 8: conv(nf, H, W, s.C, 1); break;
+        case 9: proj(256, 256, L2); break;
+        case 10: proj(256, 512, L2); break;
+        case 11: proj(256, 256, L2); break;
+        case 12: proj(512, 512, L1); break;
+        case 13: proj(512, 1024, L1); break;
+        case 14: proj(512, 512, L1); break;
+        default: return fail(2, "unet: layer index out of range");
+    }
+    return 0;
+}
+
+struct UNetWs {
+    float *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
+    int64_t total;
+};
+
+static UNetWs carve(const ldm_unet_shape& s, float* base) {
+    const int64_t B = s.B, nf = s.nf, HW = (int64_t)s.H * s.W;
+    const int64_t HW2 = HW / 4, L2 = HW / 16, L1 = HW / 64;
+    UNetWs w{};
+    int64_t off = 0;
+    auto take = [&](int64_t n) {
+        float* p = base ? base + off : nullptr;
+        off += (n + 63) / 64 * 64;   // 256-byte aligned sub-buffers
+        return p;
+    };
+    w.temb = take(B * 128);
+    w.z1 = take(B * nf * HW);
+    w.z2 = take(B * 2 * nf * HW2);
+    w.z3 = take(B * 4 * nf * L2);
+    w.q2 = take(B * 256 * L2);
+    w.kv2 = take(B * 512 * L2);
+    w.a2 = take(B * 256 * L2);
+    w.c2 = take(B * 256 * L2);
+    w.z4 = take(B * 8 * nf * L1);
+    w.q1 = take(B * 512 * L1);
+    w.kv1 = take(B * 1024 * L1);
+    w.a1 = take(B * 512 * L1);
+    w.c1 = take(B * 512 * L1);
+    w.zb = take(B * 8 * nf * L1);
+    w.d4 = take(B * 4 * nf * L2);
+    w.d3 = take(B * 2 * nf * HW2);
+    w.d2 = take(B * nf * HW);
+    w.eps = take(B * (int64_t)s.C * HW);
+    w.total = off;
+    return w;
+}
+
+static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& plan, const float* x, const float* w,
+                     const float* bias, int act, const float* bcast, const float* skip, float* y, hipStream_t st) {
+    ldm_conv_desc d;
+    int rc = layer_desc(s, layer, d);
+    if (rc) return rc;
+    ldm_epilogue ep{};
+    ep.bias = bias;
+    ep.act = act;
+    ep.bcast_add = bcast;
+    ep.skip_add = skip;
+    return ldm_conv_forward(&d, &plan, x, w, &ep, y, st);
+}
+
+#define LDM_TRY(expr)            \
+    do {                         \
+        int _rc = (expr);        \
+        if (_rc) return _rc;     \
+    } while (0)
+
+static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* z, const void* t,
+                        int t_is_float, const float* s5, const float* s6, float* out, const UNetWs& ws,
+                        hipStream_t st) {
+    const int HW = s.H * s.W;
+    const int L2 = HW / 16, L1 = HW / 64;
+    // t_embedding = time_mlp(t)[:, :, None, None]                               (model.py:203)
+    LDM_TRY(ldm_time_mlp_forward(t, t_is_float, s.B, 128, w.t_freqs, w.t_w1, w.t_b1, w.t_w2, w.t_b2, ws.temb, st));
+    // z1 = relu(enc1(z)); z2 = relu(enc2(z1)) + t_emb; z3 = relu(enc3(z2))      (model.py:205-209)
+    LDM_TRY(conv_call(s, 0, w.conv_plan[0], z, w.conv_w[0], w.conv_b[0], LDM_ACT_RELU, nullptr, nullptr, ws.z1, st));
+    LDM_TRY(conv_call(s, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, ws.temb, nullptr, ws.z2, st));
+    LDM_TRY(conv_call(s, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
+    // z3 = cross_attention2(z3, s5)                                              (model.py:211)
+    LDM_TRY(conv_call(s, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
+    LDM_TRY(conv_call(s, 10, w.ca_plan_kv[0], s5, w.ca_wkv[0], w.ca_bkv[0], 0, nullptr, nullptr, ws.kv2, st));
+    LDM_TRY(ldm_attention_core(ws.q2, ws.kv2, ws.a2, s.B, 256, 4, L2, L2, (float)std::sqrt(1.0 / 64.0), st));
+    LDM_TRY(conv_call(s, 11, w.ca_plan_o[0], ws.a2, w.ca_wo[0], w.ca_bo[0], 0, nullptr, nullptr, ws.c2, st));
+    // z4 = relu(enc4(z3)); z4 = cross_attention1(z4, s6)                         (model.py:212-214)
+    LDM_TRY(conv_call(s, 3, w.conv_plan[3], ws.c2, w.conv_w[3], w.conv_b[3], LDM_ACT_RELU, nullptr, nullptr, ws.z4, st));
+    LDM_TRY(conv_call(s, 12, w.ca_plan_q[1], ws.z4, w.ca_wq[1], w.ca_bq[1], 0, nullptr, nullptr, ws.q1, st));
+    LDM_TRY(conv_call(s, 13, w.ca_plan_kv[1], s6, w.ca_wkv[1], w.ca_bkv[1], 0, nullptr, nullptr, ws.kv1, st));
+    LDM_TRY(ldm_attention_core(ws.q1, ws.kv1, ws.a1, s.B, 512, 4, L1, L1, (float)std::sqrt(1.0 / 128.0), st));
+    LDM_TRY(conv_call(s, 14, w.ca_plan_o[1], ws.a1, w.ca_wo[1], w.ca_bo[1], 0, nullptr, nullptr, ws.c1, st));
+    // bottleneck + decoder with skips (ReLU before the add)                     (model.py:217-229)
+    LDM_TRY(conv_call(s, 4, w.conv_plan[4], ws.c1, w.conv_w[4], w.conv_b[4], LDM_ACT_RELU, nullptr, nullptr, ws.zb, st));
+    LDM_TRY(conv_call(s, 5, w.conv_plan[5], ws.zb, w.conv_w[5], w.conv_b[5], LDM_ACT_RELU, nullptr, ws.z3, ws.d4, st));
+    LDM_TRY(conv_call(s, 6, w.conv_plan[6], ws.d4, w.conv_w[6], w.conv_b[6], LDM_ACT_RELU, nullptr, ws.z2, ws.d3, st));
+    LDM_TRY(conv_call(s, 7, w.conv_plan[7], ws.d3, w.conv_w[7], w.conv_b[7], LDM_ACT_RELU, nullptr, ws.z1, ws.d2, st));
+    LDM_TRY(conv_call(s, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, out, st));
+    return 0;
+}
+
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" int ldm_unet_layer_desc(const ldm_unet_shape* s, int32_t layer, ldm_conv_desc* d) {
+    LDM_REQUIRE(s && d, "unet_layer_desc: null argument");
+    return layer_desc(*s, layer, *d);
+}
+
+extern "C" int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s) {
+    if (!s) return -1;
+    return carve(*s, nullptr).total;
+}
+
+extern "C" int ldm_unet_make_plans(const ldm_unet_shape* s, ldm_unet_weights* w) {
+    LDM_REQUIRE(s && w, "unet_make_plans: null argument");
+    for (int l = 0; l < 15; ++l) {
+        ldm_conv_desc d;
+        LDM_TRY(layer_desc(*s, l, d));
+        ldm_conv_plan* p = l < 9 ? &w->conv_plan[l]
+                                 : ((l - 9) % 3 == 0 ? &w->ca_plan_q[(l - 9) / 3]
+                                                     : ((l - 9) % 3 == 1 ? &w->ca_plan_kv[(l - 9) / 3]
+                                                                         : &w->ca_plan_o[(l - 9) / 3]));
+        LDM_TRY(ldm_conv_make_plan(&d, p));
+    }
+    return 0;
+}
+
+extern "C" int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights* w, const float* z, const void* t,
+                                int32_t t_is_float, const float* s5, const float* s6, float* out, float* workspace,
+                                void* stream) {
+    LDM_REQUIRE(s && w && z && t && s5 && s6 && out && workspace, "unet_forward: null argument");
+    UNetWs ws = carve(*s, workspace);
+    return unet_forward(*s, *w, z, t, t_is_float, s5, s6, out, ws, (hipStream_t)stream);
+}
+
+extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
+                               const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps,
+                               float eta, float* x0_logs, float* eps_logs, float* workspace, void* stream) {
+    LDM_REQUIRE(s && w && x && s5 && s6 && t_table && coef_table && workspace, "ddim_sample: null argument");
+    LDM_REQUIRE(nsteps >= 0, "ddim_sample: negative step count");
+    UNetWs ws = carve(*s, workspace);
+    const int64_t n = (int64_t)s->B * s->C * s->H * s->W;
+    hipStream_t st = (hipStream_t)stream;
+    for (int i = 0; i < nsteps; ++i) {
+        // noise_pred = unet(x, t, style_embedding)                                (model.py:439)
+        LDM_TRY(unet_forward(*s, *w, x, t_table + (size_t)i * s->B, 0, s5, s6, ws.eps, ws, st));
+        // x0 / direction / eta update and the two log clones                      (model.py:442-463)
+        LDM_TRY(ldm_ddim_step(x, ws.eps, coef_table + 4 * (size_t)i, eta, x0_logs ? x0_logs + (size_t)i * n : nullptr,
+                              eps_logs ? eps_logs + (size_t)i * n : nullptr, n, st));
+    }
+    return 0;
+}

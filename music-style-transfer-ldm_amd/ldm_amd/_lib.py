@@ -1,0 +1,128 @@
+"""ctypes binding of libldm_amd.so (include/ldm_capi.h).
+
+torch is imported first on purpose: its wheel ships libamdhip64.so with SONAME libamdhip64.so.7, and
+loading it before libldm_amd.so makes the dynamic linker bind our library to the SAME HIP runtime
+instance, so torch's streams, allocations and graph capture are valid in our launches.
+
+There is no CPU fallback anywhere: if the library is missing or no HIP device is present, every
+entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("LDM_AMD_LIB", os.path.join(PKG_ROOT, "lib", "libldm_amd.so"))
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+c_fp = ctypes.c_void_p  # device float* as raw address
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in
+                ("B", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kh", "kw", "stride", "pad", "out_pad", "transposed")]
+
+    def key(self):
+        return tuple(getattr(self, f[0]) for f in self._fields_)
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("bias", c_fp), ("bn_weight", c_fp), ("bn_bias", c_fp), ("bn_mean", c_fp), ("bn_var", c_fp),
+                ("bn_eps", c_float), ("act", c_int32), ("bcast_add", c_fp), ("skip_add", c_fp)]
+
+
+class ConvPlan(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("tm", c_int32), ("tn", c_int32), ("wk", c_int32), ("packed_floats", c_int64)]
+
+    def key(self):
+        return (self.kind, self.tm, self.tn, self.wk)
+
+
+class UNetShape(ctypes.Structure):
+    _fields_ = [("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32), ("nf", c_int32)]
+
+
+class UNetWeights(ctypes.Structure):
+    _fields_ = [("conv_w", c_fp * 9), ("conv_b", c_fp * 9), ("conv_plan", ConvPlan * 9),
+                ("ca_wq", c_fp * 2), ("ca_bq", c_fp * 2), ("ca_plan_q", ConvPlan * 2),
+                ("ca_wkv", c_fp * 2), ("ca_bkv", c_fp * 2), ("ca_plan_kv", ConvPlan * 2),
+                ("ca_wo", c_fp * 2), ("ca_bo", c_fp * 2), ("ca_plan_o", ConvPlan * 2),
+                ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp)]
+
+
+ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
+
+# name -> (restype, argtypes).  Kept in one table so tests can check it against include/ldm_capi.h.
+SIGNATURES = {
+    "ldm_last_error": (ctypes.c_char_p, []),
+    "ldm_capi_version": (c_int32, []),
+    "ldm_device_count": (c_int32, [ctypes.POINTER(c_int32)]),
+    "ldm_conv_make_plan": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan)]),
+    "ldm_conv_make_plan_forced": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, c_int32, c_int32, c_int32,
+                                            ctypes.POINTER(ConvPlan)]),
+    "ldm_conv_pack_weight": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp, c_vp]),
+    "ldm_conv_forward": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp,
+                                   ctypes.POINTER(Epilogue), c_fp, c_vp]),
+    "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
+                                      c_int32, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_eval": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_int32,
+                                     c_vp]),
+    "ldm_activation": (c_int32, [c_fp, c_fp, c_int64, c_int32, c_vp]),
+    "ldm_sinusoid_embed": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_vp]),
+    "ldm_time_mlp_forward": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_attention_core": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_vp]),
+    "ldm_q_sample": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
+    "ldm_predict_start": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
+    "ldm_sched_backward": (c_int32, [c_int32, c_fp, c_fp, c_int32, c_vp, c_fp, c_fp, c_int32, c_int64, c_vp]),
+    "ldm_ddim_step":(c_int32, [c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_int64, c_vp]),
+    "ldm_loss_forward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_vp, c_fp, c_vp]),
+    "ldm_loss_backward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_unet_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape)]),
+    "ldm_unet_make_plans": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights)]),
+    "ldm_unet_layer_desc": (c_int32, [ctypes.POINTER(UNetShape), c_int32, ctypes.POINTER(ConvDesc)]),
+    "ldm_unet_forward": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_vp, c_int32,
+                                   c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_ddim_sample": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_fp, c_fp, c_vp,
+                                  c_fp, c_int32, c_float, c_fp, c_fp, c_fp, c_vp]),
+}
+
+_LIB = None
+
+
+class LDMError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load (once) and return the CDLL with every prototype declared. Raises if absent."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise LDMError(f"libldm_amd.so not found at {p}: build it with `make -C music-style-transfer-ldm_amd/csrc` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().ldm_last_error().decode(errors="replace")
+        raise LDMError(f"{what} failed (code {rc}): {msg}")
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+    return rc

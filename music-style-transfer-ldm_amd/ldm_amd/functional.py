@@ -1,0 +1,200 @@
+"""Autograd-aware functional layer over ops.py.
+
+Every function here computes on the HIP path.  When autograd needs a graph (grad mode on and an input
+requires grad) the call is wrapped in a torch.autograd.Function whose backward runs the matching HIP
+backward kernels (ldm_amd.backward); a missing backward raises instead of silently detaching.
+"""
+import torch
+
+from . import ops
+
+_BACKWARD = {}   # name -> callable(ctx, *grad_outputs) registered by ldm_amd.backward
+
+
+def register_backward(name):
+    def deco(fn):
+        _BACKWARD[name] = fn
+        return fn
+    return deco
+
+
+def _needs_grad(*ts):
+    if not torch.is_grad_enabled():
+        return False
+    return any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+
+
+class _HipOp(torch.autograd.Function):
+    """Generic wrapper: forward = fwd(ctx_dict, *tensors); backward dispatched by name."""
+
+    @staticmethod
+    def forward(ctx, name, fwd, nin, *args):
+        tensors = args[:nin]
+        store = {}
+        out = fwd(store, *tensors)
+        ctx.name = name
+        ctx.store = store
+        ctx.nin = nin
+        saved = store.pop("saved", ())
+        ctx.save_for_backward(*saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, *grads):
+        fn = _BACKWARD.get(ctx.name)
+        if fn is None:
+            raise NotImplementedError(f"music-style-transfer-ldm_amd: backward of '{ctx.name}' has no HIP kernel yet")
+        gin = fn(ctx, *grads)
+        return (None, None, None) + tuple(gin)
+
+
+def hip_apply(name, fwd, *tensors):
+    """Run fwd(store, *tensors) on the HIP path; build an autograd node only if needed."""
+    if _needs_grad(*tensors):
+        return _HipOp.apply(name, fwd, len(tensors), *tensors)
+    return fwd({}, *tensors)
+
+
+# ------------------------------------------------------------------------------------------------
+def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0, act="none", bcast=None,
+         skip=None, bn_eval=None, wkey=None):
+    """act(BN_eval(conv(x,w)+b)) + bcast + skip, differentiable in x, weight, bias, bcast, skip.
+
+    wkey = (owner_parameter, tag) caches the packed weight of a parameter slice against the parameter."""
+    cfg = dict(stride=stride, padding=padding, transposed=transposed, output_padding=output_padding, act=act)
+
+    def fwd(store, x_, w_, b_, bc_, sk_):
+        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, **cfg)
+        store["cfg"] = cfg
+        store["bn"] = bn_eval
+        store["saved"] = (x_, w_, y)
+        store["has"] = (b_ is not None, bc_ is not None, sk_ is not None)
+        return y
+
+    return hip_apply("conv", fwd, x, weight, bias, bcast, skip)
+
+
+def linear(x, weight, bias, act="none"):
+    """y = act(x W^T + b) for x [..., in]: a 1x1 conv over N = prod(leading dims) 'pixels'."""
+    lead = x.shape[:-1]
+    n = 1
+    for s in lead:
+        n *= s
+    x4 = x.reshape(n, x.shape[-1], 1, 1)
+    y = conv(x4, weight.view(weight.shape[0], weight.shape[1], 1, 1), bias, stride=1, padding=0, act=act)
+    return y.reshape(*lead, weight.shape[0])
+
+
+def activation(x, act):
+    def fwd(store, x_):
+        y = ops.activation(x_, act)
+        store["act"] = act
+        store["saved"] = (x_, y)
+        return y
+
+    return hip_apply("activation", fwd, x)
+
+
+def batchnorm(x, bn_module, act="none"):
+    """nn.BatchNorm2d semantics (train: batch stats + running update; eval: running stats) + act."""
+    m = bn_module
+    use_batch = m.training or not m.track_running_stats
+    if not use_batch:
+        def fwd_eval(store, x_, w_, b_):
+            y = ops.batchnorm_eval(x_, w_, b_, m.running_mean, m.running_var, m.eps, act)
+            store["saved"] = (x_, w_, y)
+            store["bn"] = (m.running_mean, m.running_var, m.eps, act)
+            return y
+        return hip_apply("batchnorm_eval", fwd_eval, x, m.weight, m.bias)
+
+    momentum = m.momentum
+    if m.training and m.track_running_stats:
+        m.num_batches_tracked.add_(1)
+        if momentum is None:
+            momentum = 1.0 / float(m.num_batches_tracked.item())
+    rm = m.running_mean if (m.training and m.track_running_stats) else None
+    rv = m.running_var if (m.training and m.track_running_stats) else None
+
+    def fwd_train(store, x_, w_, b_):
+        y = ops.f32c(x_).clone()
+        sm, si = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps, act,
+                                      save=True)
+        store["saved"] = (x_, w_, b_, sm, si, y)
+        store["act"] = act
+        return y
+
+    return hip_apply("batchnorm_train", fwd_train, x, m.weight, m.bias)
+
+
+def time_mlp(t, w1, b1, w2, b2):
+    def fwd(store, w1_, b1_, w2_, b2_):
+        return ops.time_mlp(t, w1_, b1_, w2_, b2_)
+
+    return hip_apply("time_mlp", fwd, w1, b1, w2, b2)
+
+
+def q_sample(x0, eps, coef_table, t):
+    def fwd(store, x0_, eps_):
+        store["sched"] = (coef_table, t)
+        return ops.q_sample(x0_, eps_, coef_table, t)
+
+    return hip_apply("q_sample", fwd, x0, eps)
+
+
+def predict_start(zt, eps, coef_table, t):
+    def fwd(store, zt_, eps_):
+        store["sched"] = (coef_table, t)
+        return ops.predict_start(zt_, eps_, coef_table, t)
+
+    return hip_apply("predict_start", fwd, zt, eps)
+
+
+def _sched_bw(kind):
+    def bw(ctx, g):
+        tab, t = ctx.store["sched"]
+        return ops.sched_backward(kind, g, tab, t, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+    return bw
+
+
+register_backward("q_sample")(_sched_bw(0))
+register_backward("predict_start")(_sched_bw(1))
+
+
+def mse_loss(a, b):
+    def fwd(store, a_, b_):
+        store["saved"] = (a_, b_)
+        return ops.loss_forward(0, a_, b_)
+
+    return hip_apply("mse_loss", fwd, a, b)
+
+
+def kl_loss(z):
+    def fwd(store, z_):
+        store["saved"] = (z_,)
+        return ops.loss_forward(1, z_)
+
+    return hip_apply("kl_loss", fwd, z)
+
+
+@register_backward("mse_loss")
+def _mse_backward(ctx, g):
+    a, b = ctx.saved_tensors
+    ga, gb = ops.loss_backward(0, a, b, g, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+    return ga, gb
+
+
+@register_backward("kl_loss")
+def _kl_backward(ctx, g):
+    (z,) = ctx.saved_tensors
+    gz, _ = ops.loss_backward(1, z, None, g, True, False)
+    return (gz,)
+
+
+def attention_core(q, kv, heads):
+    def fwd(store, q_, kv_):
+        out = ops.attention_core(q_, kv_, heads)
+        store["saved"] = (q_, kv_, out)
+        store["heads"] = heads
+        return out
+
+    return hip_apply("attention_core", fwd, q, kv)

@@ -1,0 +1,352 @@
+"""Tensor-level entry points over the C ABI (torch tensors in, torch tensors out).
+
+torch is only the owner of device memory and streams here; every arithmetic operation of the hot
+path runs in libldm_amd.so.  Inputs must be contiguous float32 tensors on a HIP device: there is no
+CPU fallback (a CPU tensor raises).
+"""
+import ctypes
+import math
+import weakref
+
+import torch
+
+from . import _lib as L
+
+byref = ctypes.byref
+
+
+# ------------------------------------------------------------------------------------------------
+# helpers
+# ------------------------------------------------------------------------------------------------
+def stream_handle():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def require_device(*ts, dtype=torch.float32, what="music-style-transfer-ldm_amd"):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f"{what}: tensor on {t.device}; the HIP kernels need a GPU tensor "
+                               "(there is no CPU fallback)")
+        if dtype is not None and t.dtype != dtype:
+            raise RuntimeError(f"{what}: expected {dtype}, got {t.dtype}")
+
+
+def f32c(t):
+    """contiguous float32 view/copy on the same device (a dtype cast is a device copy, not compute)."""
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+# plans and packed weights
+# ------------------------------------------------------------------------------------------------
+class IdCache:
+    """Per-object cache keyed by identity (tensors cannot key a WeakKeyDictionary: their __eq__ is
+    elementwise).  Entries die with their key object."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, obj, default=None):
+        hit = self._d.get(id(obj))
+        if hit is None or hit[0]() is not obj:
+            return default
+        return hit[1]
+
+    def __setitem__(self, obj, value):
+        k = id(obj)
+        self._d[k] = (weakref.ref(obj, lambda _r, k=k, d=self._d: d.pop(k, None)), value)
+
+    def clear(self):
+        self._d.clear()
+
+
+_PLAN_CACHE = {}
+_PLAN_OVERRIDE = {}      # desc.key() -> (kind, tm, tn, wk), filled by the autotuner / tests
+_PACK_CACHE = IdCache()
+
+
+def make_desc(B, Cin, Hin, Win, Cout, kh, kw, stride, pad, out_pad=0, transposed=False):
+    if transposed:
+        Hout = (Hin - 1) * stride - 2 * pad + kh + out_pad
+        Wout = (Win - 1) * stride - 2 * pad + kw + out_pad
+    else:
+        Hout = (Hin + 2 * pad - kh) // stride + 1
+        Wout = (Win + 2 * pad - kw) // stride + 1
+    return L.ConvDesc(B, Cin, Hin, Win, Cout, Hout, Wout, kh, kw, stride, pad, out_pad, int(bool(transposed)))
+
+
+def get_plan(desc, force=None):
+    key = desc.key()
+    force = force or _PLAN_OVERRIDE.get(key)
+    if force is not None:
+        plan = L.ConvPlan()
+        L.call("ldm_conv_make_plan_forced", byref(desc), *force, byref(plan))
+        return plan
+    plan = _PLAN_CACHE.get(key)
+    if plan is None:
+        plan = L.ConvPlan()
+        L.call("ldm_conv_make_plan", byref(desc), byref(plan))
+        _PLAN_CACHE[key] = plan
+    return plan
+
+
+def set_plan_override(desc, kind, tm=1, tn=1, wk=1):
+    _PLAN_OVERRIDE[desc.key()] = (kind, tm, tn, wk)
+
+
+def clear_plan_overrides():
+    _PLAN_OVERRIDE.clear()
+
+
+def packed_weight(weight, desc, plan, owner=None, tag=None):
+    """Weight re-laid into the plan's MFMA fragment order; cached per (owner tensor, _version, layout).
+
+    `owner`/`tag` let a slice of a parameter (the q / kv rows of in_proj_weight) be cached against the
+    parameter itself, whose _version moves on every in-place update."""
+    if plan.kind == 0:
+        return weight
+    owner = weight if owner is None else owner
+    key = (owner._version, tag, desc.Cin, desc.Cout, desc.kh, desc.kw, desc.stride, desc.pad, desc.out_pad,
+           desc.transposed, plan.kind, plan.tm)
+    per = _PACK_CACHE.get(owner)
+    if per is None:
+        per = {}
+        _PACK_CACHE[owner] = per
+    buf = per.get(key)
+    if buf is None:
+        # drop stale versions of this weight
+        for k in [k for k in per if k[0] != owner._version]:
+            del per[k]
+        w = f32c(weight.detach())
+        buf = torch.empty(int(plan.packed_floats), device=weight.device, dtype=torch.float32)
+        L.call("ldm_conv_pack_weight", byref(desc), byref(plan), w.data_ptr(), buf.data_ptr(), stream_handle())
+        per[key] = buf
+    return buf
+
+
+# ------------------------------------------------------------------------------------------------
+# convolution with fused epilogue
+# ------------------------------------------------------------------------------------------------
+def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False, output_padding=0, bn=None,
+                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None):
+    """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps)."""
+    require_device(x, weight, bias, bcast, skip)
+    x = f32c(x)
+    B, Cin, H, W = x.shape
+    if transposed:
+        cin_w, Cout, kh, kw = weight.shape
+    else:
+        Cout, cin_w, kh, kw = weight.shape
+    if cin_w != Cin:
+        raise RuntimeError(f"conv: input has {Cin} channels, weight expects {cin_w}")
+    desc = make_desc(B, Cin, H, W, Cout, kh, kw, stride, padding, output_padding, transposed)
+    if desc.Hout <= 0 or desc.Wout <= 0:
+        raise RuntimeError("conv: non-positive output size")
+    plan = plan or get_plan(desc)
+    wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
+    y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
+    ep = L.Epilogue()
+    ep.bias = _p(bias)
+    keep = []
+    if bn is not None:
+        g, b_, m, v, eps = bn
+        require_device(g, b_, m, v)
+        ep.bn_weight, ep.bn_bias, ep.bn_mean, ep.bn_var = _p(g), _p(b_), _p(m), _p(v)
+        ep.bn_eps = float(eps)
+    ep.act = L.ACT[act]
+    if bcast is not None:
+        bcast = f32c(bcast)
+        keep.append(bcast)
+        ep.bcast_add = bcast.data_ptr()
+    if skip is not None:
+        skip = f32c(skip)
+        keep.append(skip)
+        ep.skip_add = skip.data_ptr()
+    L.call("ldm_conv_forward", byref(desc), byref(plan), x.data_ptr(), _p(wbuf), byref(ep), y.data_ptr(),
+           stream_handle())
+    return y
+
+
+def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False):
+    """In-place train-mode BatchNorm2d (+activation); updates running stats like nn.BatchNorm2d."""
+    require_device(x, weight, bias, running_mean, running_var)
+    assert x.is_contiguous() and x.dtype == torch.float32
+    B, C, H, W = x.shape
+    sm = si = None
+    if save:
+        sm = torch.empty(C, device=x.device, dtype=torch.float32)
+        si = torch.empty(C, device=x.device, dtype=torch.float32)
+    L.call("ldm_batchnorm_train", x.data_ptr(), B, C, H * W, _p(weight), _p(bias), _p(running_mean),
+           _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si), stream_handle())
+    return (sm, si) if save else None
+
+
+def activation(x, act, inplace=False):
+    require_device(x)
+    x = f32c(x)
+    y = x if inplace else torch.empty_like(x)
+    L.call("ldm_activation", x.data_ptr(), y.data_ptr(), x.numel(), L.ACT[act], stream_handle())
+    return y
+
+
+def batchnorm_eval(x, weight, bias, running_mean, running_var, eps, act="none"):
+    require_device(x, weight, bias, running_mean, running_var)
+    x = f32c(x)
+    y = torch.empty_like(x)
+    B, C = x.shape[0], x.shape[1]
+    HW = x.numel() // max(1, B * C)
+    L.call("ldm_batchnorm_eval", x.data_ptr(), y.data_ptr(), B, C, HW, _p(weight), _p(bias), _p(running_mean),
+           _p(running_var), float(eps), L.ACT[act], stream_handle())
+    return y
+
+
+_LOSS_WS = {}
+
+
+def loss_forward(kind, a, b=None):
+    """kind 0: mean((a-b)^2); kind 1: mean(0.5*(a^2-1-log(a^2+1e-8))).  Returns a 0-dim device tensor."""
+    require_device(a, b)
+    a = f32c(a)
+    if b is not None:
+        b = f32c(b)
+        if b.shape != a.shape:
+            raise RuntimeError(f"loss: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    ws = _LOSS_WS.get(str(a.device))
+    if ws is None:
+        ws = torch.empty(512, device=a.device, dtype=torch.float64)
+        _LOSS_WS[str(a.device)] = ws
+    out = torch.empty((), device=a.device, dtype=torch.float32)
+    L.call("ldm_loss_forward", kind, a.data_ptr(), _p(b), a.numel(), ws.data_ptr(), out.data_ptr(), stream_handle())
+    return out
+
+
+def loss_backward(kind, a, b, grad_out, need_a=True, need_b=False):
+    a = f32c(a)
+    b = None if b is None else f32c(b)
+    g = f32c(grad_out.reshape(()).to(a.device))
+    ga = torch.empty_like(a) if need_a else None
+    gb = torch.empty_like(a) if (need_b and b is not None) else None
+    L.call("ldm_loss_backward", kind, a.data_ptr(), _p(b), a.numel(), g.data_ptr(), _p(ga), _p(gb), stream_handle())
+    return ga, gb
+
+
+def _t_arg(t, device):
+    if not t.is_cuda:
+        t = t.to(device)
+    t_is_float = 0 if t.dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8) else 1
+    t = t.to(torch.int64 if t_is_float == 0 else torch.float32).reshape(-1).contiguous()
+    return t, t_is_float
+
+
+def sinusoid_embed(t, dim, device):
+    t, is_f = _t_arg(t, device)
+    out = torch.empty((t.shape[0], dim), device=device, dtype=torch.float32)
+    L.call("ldm_sinusoid_embed", t.data_ptr(), is_f, t.shape[0], dim, sinusoid_freqs(dim, device).data_ptr(),
+           out.data_ptr(), stream_handle())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# time MLP, attention, scheduler
+# ------------------------------------------------------------------------------------------------
+_FREQ_CACHE = {}
+
+
+def sinusoid_freqs(dim, device):
+    """exp(arange(half) * -(ln(1e4)/(half-1))) computed exactly as model.py:241-243 (host constant)."""
+    key = (dim, str(device))
+    f = _FREQ_CACHE.get(key)
+    if f is None:
+        half = dim // 2
+        e = math.log(10000) / (half - 1)
+        f = torch.exp(torch.arange(half) * -e).to(torch.float32).to(device)
+        _FREQ_CACHE[key] = f
+    return f
+
+
+def time_mlp(t, w1, b1, w2, b2):
+    require_device(w1, b1, w2, b2)
+    dim = w1.shape[0]
+    t, t_is_float = _t_arg(t, w1.device)
+    out = torch.empty((t.shape[0], dim), device=w1.device, dtype=torch.float32)
+    L.call("ldm_time_mlp_forward", t.data_ptr(), t_is_float, t.shape[0], dim, sinusoid_freqs(dim, w1.device).data_ptr(),
+           w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), out.data_ptr(), stream_handle())
+    return out
+
+
+def attention_core(q, kv, heads):
+    """q [B,E,L], kv [B,2E,S] -> [B,E,L] (softmax((q*sqrt(1/d))^T k) v per head)."""
+    require_device(q, kv)
+    B, E, Lq = q.shape
+    S = kv.shape[2]
+    out = torch.empty_like(q)
+    scale = float(math.sqrt(1.0 / float(E // heads)))
+    L.call("ldm_attention_core", q.data_ptr(), kv.data_ptr(), out.data_ptr(), B, E, heads, Lq, S, scale,
+           stream_handle())
+    return out
+
+
+_COEF_CACHE = IdCache()
+
+
+def alpha_bar_coef_table(alpha_bar, device):
+    """[T,2] float32 {sqrt(ab), sqrt(1-ab)} on `device`: the exact fp32 values torch.sqrt gives for the
+    reference's expressions (model.py:113, :124, :449-452).  Host constant, cached per buffer version."""
+    per = _COEF_CACHE.get(alpha_bar)
+    key = (alpha_bar._version, str(device))
+    if per is None or per[0] != key:
+        ab = alpha_bar.detach().to("cpu", torch.float32)
+        tab = torch.stack([torch.sqrt(ab), torch.sqrt(1 - ab)], dim=1).contiguous().to(device)
+        per = (key, tab)
+        _COEF_CACHE[alpha_bar] = per
+    return per[1]
+
+
+def q_sample(x0, eps, coef_table, t):
+    require_device(x0, eps, coef_table)
+    t = t.to(x0.device, torch.int64).contiguous()
+    x0 = f32c(x0)
+    eps = f32c(eps)
+    zt = torch.empty_like(x0)
+    B = x0.shape[0]
+    L.call("ldm_q_sample", x0.data_ptr(), eps.data_ptr(), coef_table.data_ptr(), coef_table.shape[0], t.data_ptr(),
+           zt.data_ptr(), B, x0.numel() // B, stream_handle())
+    return zt
+
+
+def predict_start(zt, eps, coef_table, t):
+    require_device(zt, eps, coef_table)
+    t = t.to(zt.device, torch.int64).contiguous()
+    zt = f32c(zt)
+    eps = f32c(eps)
+    x0 = torch.empty_like(zt)
+    B = zt.shape[0]
+    L.call("ldm_predict_start", zt.data_ptr(), eps.data_ptr(), coef_table.data_ptr(), coef_table.shape[0],
+           t.data_ptr(), x0.data_ptr(), B, zt.numel() // B, stream_handle())
+    return x0
+
+
+def sched_backward(kind, g, coef_table, t, need_a=True, need_b=True):
+    g = f32c(g)
+    t = t.to(g.device, torch.int64).contiguous()
+    ga = torch.empty_like(g) if need_a else None
+    gb = torch.empty_like(g) if need_b else None
+    B = g.shape[0]
+    L.call("ldm_sched_backward", kind, g.data_ptr(), coef_table.data_ptr(), coef_table.shape[0], t.data_ptr(),
+           _p(ga), _p(gb), B, g.numel() // B, stream_handle())
+    return ga, gb
+
+
+def ddim_step_(x, eps, coef4, eta, x0_log=None, eps_log=None):
+    require_device(x, eps, coef4, x0_log, eps_log)
+    L.call("ldm_ddim_step", x.data_ptr(), eps.data_ptr(), coef4.data_ptr(), float(eta), _p(x0_log), _p(eps_log),
+           x.numel(), stream_handle())
+    return x

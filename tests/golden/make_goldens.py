@@ -1,0 +1,198 @@
+"""Generate golden vectors by running the REFERENCE implementation on CPU (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
+stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
+``model.VGGishFeatureLoss`` swapped for an empty module (its constructor is a remote
+torch.hub fetch, model.py:260 -> loss.py:56).  Every weight and input comes from
+tests/golden/recipe.py, so only inputs/outputs are stored: tests/golden/ref_goldens.npz.
+The reference never travels to the GPU box; only this .npz does.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import recipe  # noqa: E402
+
+REF = "/root/reference/models"
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("pytorch_lightning", types.ModuleType("pytorch_lightning"))
+    lp = types.ModuleType("lpips")
+    lp.LPIPS = None
+    sys.modules.setdefault("lpips", lp)
+    sys.path.insert(0, REF)
+    import model as ref_model  # noqa: E402
+    import loss as ref_loss  # noqa: E402
+
+    class _NoVGGish(torch.nn.Module):
+        def forward(self, a, b):
+            return torch.zeros((), dtype=a.dtype)
+
+    ref_model.VGGishFeatureLoss = _NoVGGish
+    return ref_model, ref_loss
+
+
+def np32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def main():
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+
+    # ---- (1) schedule tables, index lists, sinusoid ------------------------------------------
+    fd = M.ForwardDiffusion(200)
+    G["sched_beta"] = np32(fd.beta_t)
+    G["sched_alpha"] = np32(fd.alpha_t)
+    G["sched_alpha_bar"] = np32(fd.alpha_bar_t)
+    for T in (10, 50, 100, 250, 1000):
+        f = M.ForwardDiffusion(T)
+        G[f"sched_alpha_bar_T{T}"] = np32(f.alpha_bar_t)
+    for start, n in ((199, 50), (199, 100), (199, 200), (49, 50), (99, 100), (199, 250), (199, 2), (9, 10)):
+        G[f"times_{start}_{n}"] = torch.linspace(start, 0, n).long().numpy()
+    sp = M.SinusoidalPositionEmbeddings(128)
+    tt = torch.tensor([0, 1, 57, 199], dtype=torch.long)
+    G["sinus_t"] = tt.numpy()
+    G["sinus_emb"] = np32(sp(tt))
+
+    with torch.no_grad():
+        # ---- (2) UNet forward -------------------------------------------------------------
+        unet = M.UNet(32, 32, 64)
+        recipe.fill_module(unet, seed=100)
+        for tag, (B, H, W, seed) in {"s": (2, 16, 16, 1), "c": (1, 16, 64, 2)}.items():
+            z = torch.from_numpy(recipe.normal((B, 32, H, W), seed))
+            s5 = torch.from_numpy(recipe.uniform01((B, 256, H // 4, W // 4), seed + 10))
+            s6 = torch.from_numpy(recipe.uniform01((B, 512, H // 8, W // 8), seed + 20))
+            t = torch.from_numpy(recipe.timesteps(B, seed + 30))
+            out = unet(z, t, {"s5": s5, "s6": s6})
+            G[f"unet_{tag}_t"] = t.numpy()
+            G[f"unet_{tag}_out"] = np32(out)
+            G[f"unet_{tag}_temb"] = np32(unet.time_mlp(t))
+
+        # ---- (3) CrossAttention standalone ------------------------------------------------
+        for E, (h, w) in ((256, (4, 16)), (512, (2, 8))):
+            ca = M.CrossAttention(E, 4)
+            recipe.fill_module(ca, seed=200 + E)
+            q = torch.from_numpy(recipe.normal((2, E, h, w), 300 + E))
+            kv = torch.from_numpy(recipe.uniform01((2, E, h, w), 400 + E))
+            G[f"ca{E}_out"] = np32(ca(q, kv))
+
+        # ---- (4) VAE encoder / decoder (eval and train BN), style encoder ----------------
+        enc = M.SpectrogramEncoder(32)
+        dec = M.SpectrogramDecoder(32)
+        sty = M.StyleEncoder(1, 64)
+        recipe.fill_module(enc, seed=500)
+        recipe.fill_module(dec, seed=501)
+        recipe.fill_module(sty, seed=502)
+        x_s = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 600))
+        x_c = torch.from_numpy(recipe.uniform01((1, 1, 128, 512), 601))
+        enc.eval()
+        dec.eval()
+        G["enc_eval_s_out"] = np32(enc(x_s))
+        G["enc_eval_c_out"] = np32(enc(x_c))
+        zl = torch.from_numpy(recipe.normal((2, 32, 16, 16), 602))
+        G["dec_eval_s_out"] = np32(dec(zl))
+        enc.train()
+        dec.train()
+        G["enc_train_s_out"] = np32(enc(x_s))
+        G["enc_train_s_rm0"] = np32(enc.encoder[1].running_mean)
+        G["enc_train_s_rv0"] = np32(enc.encoder[1].running_var)
+        G["dec_train_s_out"] = np32(dec(zl))
+        G["dec_train_s_rm1"] = np32(dec.decoder[4].running_mean)
+        G["dec_train_s_rv1"] = np32(dec.decoder[4].running_var)
+        so = sty(x_s)
+        G["style_s_s1_slice"] = np32(so["s1"][:, :8])
+        for k in ("s5", "s6"):
+            G[f"style_s_{k}"] = np32(so[k])
+        so = sty(x_c)
+        for k in ("s5", "s6"):
+            G[f"style_c_{k}"] = np32(so[k])
+
+        # ---- (5) DDIM loops (B=1: the reference crashes for B>1 at model.py:461) -------------
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.eval()
+        style = torch.from_numpy(recipe.uniform01((1, 1, 128, 128), 701))
+        emb = ldm.style_encoder(style)
+        zT = torch.from_numpy(recipe.normal((1, 32, 16, 16), 702))
+        for eta in (0.0, 1.0):
+            x, logs = ldm.style_conditioned_ddim_sample(zT, emb, timesteps=50, eta=eta)
+            e = int(eta)
+            G[f"ddim50_eta{e}_x"] = np32(x)
+            G[f"ddim50_eta{e}_x0_first"] = np32(logs["pred_x0"][0])
+            G[f"ddim50_eta{e}_eps_last"] = np32(logs["noise_pred"][-1])
+            G[f"ddim50_eta{e}_times"] = np.array(logs["timesteps"], dtype=np.int64)
+        x, logs = ldm.content_style_ddim_sample(zT, emb, timesteps=10, eta=1.0)
+        G["cs10_eta1_x"] = np32(x)
+        G["cs10_eta1_times"] = np.array(logs["timesteps"], dtype=np.int64)
+        # canonical 128x512 latent, a short DDIM (5 steps) to bound fixture cost
+        style_c = torch.from_numpy(recipe.uniform01((1, 1, 128, 512), 703))
+        emb_c = ldm.style_encoder(style_c)
+        zT_c = torch.from_numpy(recipe.normal((1, 32, 16, 64), 704))
+        x, _ = ldm.style_conditioned_ddim_sample(zT_c, emb_c, timesteps=5, eta=0.0)
+        G["ddim5_c_x"] = np32(x)
+        # decoded sample through the full wrapper path (CPU generator z_T, model.py:394)
+        torch.manual_seed(1234)
+        dec_out = ldm.style_ddim_sample_wrapper((1, 32, 16, 16), style, timesteps=8, eta=0.0)
+        G["wrap8_decoded"] = np32(dec_out)
+
+        # ---- (6) LDM.forward with recorded noise ------------------------------------------
+        content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 710))
+        style2 = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 711))
+        t2 = torch.from_numpy(recipe.timesteps(2, 712))
+        torch.manual_seed(11)
+        out = ldm(content, style2, t2)
+        G["fwd_eval_t"] = t2.numpy()
+        for k in ("z_t", "noise", "noise_pred", "z_0", "reconstructed"):
+            G[f"fwd_eval_{k}"] = np32(out[k])
+        G["loss_diffusion"] = np32(L.diffusion_loss(out["noise_pred"], out["noise"]))
+        G["loss_kl"] = np32(L.kl_regularization_loss(out["z_0"]))
+        G["loss_mse"] = np32(torch.nn.MSELoss()(out["reconstructed"], content))
+
+    # ---- (7) restated train step (train_step, train.py:163-208, fp32, no LPIPS / VGGish) --------
+    ldm.train()
+    for p in ldm.encoder.parameters():
+        p.requires_grad_(False)
+    trainable = [p for p in ldm.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(trainable, lr=5e-4)
+    opt.zero_grad()
+    torch.manual_seed(12)
+    out = ldm(content, style2, t2)
+    dl = L.diffusion_loss(out["noise_pred"], out["noise"])
+    mse = torch.nn.MSELoss()(out["reconstructed"], content)
+    kl = L.kl_regularization_loss(out["z_0"])
+    total = mse + 0.01 * kl + dl
+    total.backward()
+    G["train_noise"] = np32(out["noise"])
+    G["train_total"] = np32(total)
+    G["train_recon"] = np32(out["reconstructed"])
+    named = dict(ldm.named_parameters())
+    for k in ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
+              "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
+              "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
+              "style_encoder.enc1.weight"):
+        g = named[k].grad
+        G["grad_" + k] = np32(g[:256] if g.dim() == 2 and g.shape[0] > 256 else g)
+    opt.step()
+    for k in ("unet.dec1.weight", "decoder.decoder.6.weight", "style_encoder.enc6.bias"):
+        G["adam1_" + k] = np32(named[k])
+    G["train_enc_rm0"] = np32(ldm.encoder.encoder[1].running_mean)
+    G["train_dec_rv1"] = np32(ldm.decoder.decoder[4].running_var)
+
+    path = os.path.join(HERE, "ref_goldens.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
+if __name__ == "__main__":
+    main()
