@@ -60,6 +60,27 @@ def layer_bytes(d):
     return 4.0 * (w + d.B * d.Cin * d.Hin * d.Win + d.B * d.Cout * d.Hout * d.Wout)
 
 
+def _graph_time_us(fn, reps):
+    """Average device time per call of fn() in a dependent chain: reps calls captured in one hipGraph,
+    replayed, bracketed by HIP events on the replay stream (host launch cost excluded)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    g.replay()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
 def time_layers(engine, shape, dev, reps=50):
     """Average launch duration of each UNet GEMM-shaped kernel, HIP events on the launching stream."""
     import ctypes
@@ -83,18 +104,10 @@ def time_layers(engine, shape, dev, reps=50):
         ep.bias = bptr[i]
         ep.act = 1 if i < 8 else 0
         plan = plans[i]
-        args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr(),
-                st.cuda_stream)
+        args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr())
         lib = L.load()
-        for _ in range(5):
-            L.check(lib.ldm_conv_forward(*args), name)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            lib.ldm_conv_forward(*args)
-        e1.record(st)
-        e1.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
+        L.check(lib.ldm_conv_forward(*args, st.cuda_stream), name)
+        us = _graph_time_us(lambda: lib.ldm_conv_forward(*args, torch.cuda.current_stream().cuda_stream), reps)
         fl, by = layer_flops(d), layer_bytes(d)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
                      "flops": fl, "bytes": by, "plan": [plan.kind, plan.tm, plan.tn, plan.wk]}
@@ -102,15 +115,12 @@ def time_layers(engine, shape, dev, reps=50):
     for name, E, Lt in (("attn2", 256, shape.H * shape.W // 16), ("attn1", 512, shape.H * shape.W // 64)):
         q = torch.randn(shape.B, E, Lt, device=dev)
         kv = torch.randn(shape.B, 2 * E, Lt, device=dev)
-        for _ in range(5):
-            ops.attention_core(q, kv, 4)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            ops.attention_core(q, kv, 4)
-        e1.record(st)
-        e1.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
+        o = torch.empty_like(q)
+        scale = float((1.0 / (E // 4)) ** 0.5)
+        lib = L.load()
+        us = _graph_time_us(lambda: lib.ldm_attention_core(q.data_ptr(), kv.data_ptr(), o.data_ptr(), shape.B, E, 4,
+                                                           Lt, Lt, scale, torch.cuda.current_stream().cuda_stream),
+                            reps)
         fl = 4.0 * shape.B * E * Lt * Lt
         by = 4.0 * shape.B * 4 * E * Lt
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),

@@ -188,8 +188,11 @@ int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights* w, const f
 /* Reverse loop (style_conditioned_ddim_sample model.py:409-465 / content_style_ddim_sample :503-559):
  * x [B,C,H,W] updated in place over nsteps = len(times)-1 steps.  t_table [nsteps,B] int64 holds
  * times[i] repeated over the batch, coef_table [nsteps,4] the per-step coefficients.  x0_logs /
- * eps_logs (may be NULL) are [nsteps,B,C,H,W].  Only launches: the caller may capture the whole loop
- * into one hipGraph (the Python layer does, with torch.cuda.CUDAGraph on the same stream). */
+ * eps_logs (may be NULL) are [nsteps,B,C,H,W].  workspace: ldm_ddim_workspace_floats(s, nsteps) floats.
+ * The time MLP for all steps is one launch before the loop; each step's update is fused into dec1's
+ * epilogue.  Only launches: the caller may capture the whole loop into one hipGraph (the Python layer
+ * does, with torch.cuda.CUDAGraph on the same stream). */
+int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps);
 int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
                     float* x0_logs, float* eps_logs, float* workspace, void* stream);

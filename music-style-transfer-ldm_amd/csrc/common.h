@@ -35,6 +35,27 @@ int fail(int code, const std::string& msg);
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// Division of a non-negative int < 2^31 by a runtime constant with one mul_hi + shift (Granlund-
+// Montgomery, round-up multiplier): the GPU's integer division is a ~30-instruction VALU sequence.
+struct FastDiv {
+    int32_t d;
+    uint32_t mul, shr;
+    static FastDiv make(int32_t dv) {
+        FastDiv f{dv, 0u, 0u};
+        if (dv > 1) {
+            uint32_t l = 0;
+            while ((1u << l) < (uint32_t)dv) ++l;   // ceil(log2 d)
+            const uint32_t p = 31 + l;
+            f.mul = (uint32_t)(((1ull << p) + (uint32_t)dv - 1) / (uint32_t)dv);
+            f.shr = p - 32;
+        }
+        return f;
+    }
+    __device__ __forceinline__ int div(int n) const {
+        return d == 1 ? n : (int)(__umulhi((uint32_t)n, mul) >> shr);
+    }
+};
+
 constexpr int kMaxPhase = 4;
 constexpr int kMaxTap = 9;
 
@@ -46,8 +67,10 @@ struct PhaseTable {
     int32_t osy;      // output step per q (conv: 1, convT: 2)
     int32_t ry[kMaxPhase], rx[kMaxPhase];
     int32_t ntap[kMaxPhase];
-    int8_t dy[kMaxPhase][kMaxTap], dx[kMaxPhase][kMaxTap];
-    int8_t kk[kMaxPhase][kMaxTap];   // kernel-window index kh*KW+kw of the tap
+    // int32 (not int8): the kernels index these with a wave-uniform tap, which must compile to a
+    // scalar s_load_dword from the kernarg segment; byte fields force per-lane global loads.
+    int32_t dy[kMaxPhase][kMaxTap], dx[kMaxPhase][kMaxTap];
+    int32_t kk[kMaxPhase][kMaxTap];   // kernel-window index kh*KW+kw of the tap
     int64_t wofs[kMaxPhase];         // packed-weight offset (floats) of each phase
     int32_t kchunks[kMaxPhase];      // K chunks of each phase
 };
@@ -65,9 +88,35 @@ struct EpiArgs {
     int32_t act;
     const float* bcast;
     const float* skip;
+    // fused DDIM reverse update (model.py:442-458) on the conv output eps = noise_pred:
+    // x <- sqrt(ab_n)*x0 + sqrt(1-ab_n)*eps + eta*(...) in place, with pred_x0 / noise_pred logs.
+    const float* ddim_coef;   // [4] {sqrt(ab_t), sqrt(1-ab_t), sqrt(ab_n), sqrt(1-ab_n)} or NULL
+    float ddim_eta;
+    float* ddim_x;
+    float* ddim_x0_log;
+    float* ddim_eps_log;
 };
 
+// conv.hip: implicit-GEMM conv with the full internal epilogue (incl. the fused DDIM update); y may be
+// NULL when ep.ddim_coef is set.
+int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
+                    float* y, hipStream_t st);
+
+// One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
+// with fp contract off).  Returns x_next; x0 out.
+__device__ __forceinline__ float ddim_update(float xv, float e, const float* coef, float eta, float& x0) {
+#pragma clang fp contract(off)
+    const float sat = coef[0], s1t = coef[1], san = coef[2], s1n = coef[3];
+    const float dxt = s1t * e;            // sqrt(1-ab_t) * noise_pred (also inside predict_start)
+    x0 = (xv - dxt) / sat;                // predict_start_from_noise
+    const float dxn = s1n * e;            // direction_xt_next
+    const float nc = eta * (dxn - dxt);   // noise_contribution
+    const float t1 = san * x0;
+    return (t1 + dxn) + nc;
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
+#pragma clang fp contract(off)
     if (act == LDM_ACT_RELU) return v < 0.f ? 0.f : v;   // F.relu; NaN propagates like torch
     if (act == LDM_ACT_TANH) return tanhf(v);
     if (act == LDM_ACT_TANH_HALF) {

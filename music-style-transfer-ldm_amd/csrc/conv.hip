@@ -17,9 +17,14 @@
 // read consecutive output pixels (coalesced).  Waves of a block split K; their partial tiles are
 // summed in LDS in a fixed order (deterministic) and the fused epilogue runs once per output.
 //
+// The K loop is software-pipelined in registers: chunks are loaded in groups of kGroup, and the
+// loads of group g+1 are issued before the MFMAs of group g, so at ~1-2 waves per SIMD (these GEMMs
+// are small) the L2/HBM latency hides under matrix work instead of serialising every chunk.
+//
 // Matrix instructions (exact fp32, bitwise an fmaf chain — cdna_hip_programming.md §3):
 //   kind 1: v_mfma_f32_32x32x2_f32  lane l: A[l&31][k=l>>5], B[k=l>>5][l&31]; D row=(r&3)+8(r>>2)+4(l>>5), col=l&31
 //   kind 2: v_mfma_f32_16x16x4_f32  lane l: A[l&15][k=l>>4], B[k=l>>4][l&15]; D row=4(l>>4)+r,            col=l&15
+// Within a K-chunk, lane group lg = lane/TILE holds k = NLG*j + lg for MFMA step j = 0..3 (NLG = 64/TILE).
 #include <algorithm>
 #include <cstdio>
 
@@ -37,6 +42,7 @@ struct ConvArgs {
     int32_t KK;     // kh*kw
     int32_t Mpad;   // rows of the packed weight
     int32_t transposed;
+    FastDiv fd_hw, fd_w;   // n -> (b, q) and q -> (qy, qx) of the phase grid
     PhaseTable pt;
     EpiArgs ep;
 };
@@ -62,9 +68,9 @@ int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
         int n = 0;
         for (int a = 0; a < d.kh; ++a)
             for (int b = 0; b < d.kw; ++b) {
-                pt.dy[0][n] = (int8_t)(a - d.pad);
-                pt.dx[0][n] = (int8_t)(b - d.pad);
-                pt.kk[0][n] = (int8_t)(a * d.kw + b);
+                pt.dy[0][n] = (int32_t)(a - d.pad);
+                pt.dx[0][n] = (int32_t)(b - d.pad);
+                pt.kk[0][n] = (int32_t)(a * d.kw + b);
                 ++n;
             }
         pt.ntap[0] = n;
@@ -94,9 +100,9 @@ int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
                     const int vx = rx + d.pad - b;
                     if (vx & 1) continue;
                     LDM_REQUIRE(n < kMaxTap, "conv_transpose: too many taps");
-                    pt.dy[p][n] = (int8_t)(vy >> 1);
-                    pt.dx[p][n] = (int8_t)(vx >> 1);
-                    pt.kk[p][n] = (int8_t)(a * d.kw + b);
+                    pt.dy[p][n] = (int32_t)(vy >> 1);
+                    pt.dx[p][n] = (int32_t)(vx >> 1);
+                    pt.kk[p][n] = (int32_t)(a * d.kw + b);
                     ++n;
                 }
             }
@@ -133,9 +139,25 @@ static int layout_for_plan(const ldm_conv_desc& d, const ldm_conv_plan& p, Phase
 // ------------------------------------------------------------------------------------------------
 // epilogue (op order of the reference: conv+bias -> BN(eval) -> act -> +bcast -> +skip)
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, int oy, int ox, float v) {
+// Epilogue operands of one output element, loaded ahead of time (before the K loop) so their memory
+// latency overlaps the GEMM instead of trailing it.
+struct EpiPre {
+    float bias, bcast, skip, x;
+};
+
+__device__ __forceinline__ EpiPre epi_prefetch(const ConvArgs& a, int m, int b, size_t oidx) {
     const EpiArgs& e = a.ep;
-    if (e.bias) v = v + e.bias[m];
+    EpiPre p;
+    p.bias = e.bias ? e.bias[m] : 0.f;
+    p.bcast = e.bcast ? e.bcast[(size_t)b * a.Cout + m] : 0.f;
+    p.skip = e.skip ? e.skip[oidx] : 0.f;
+    p.x = e.ddim_coef ? e.ddim_x[oidx] : 0.f;
+    return p;
+}
+
+__device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx, float v, const EpiPre& p) {
+    const EpiArgs& e = a.ep;
+    if (e.bias) v = v + p.bias;
     if (e.bn_w) {
         // aten batch_norm_cpu_collect_linear_and_constant_terms: alpha = invstd*w, beta = b - mean*alpha
         const float invstd = 1.0f / sqrtf(e.bn_v[m] + e.bn_eps);
@@ -144,215 +166,257 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, 
         v = v * alpha + beta;
     }
     v = apply_act(v, e.act);
-    const size_t oidx = (((size_t)b * a.Cout + m) * a.Hout + oy) * a.Wout + ox;
-    if (e.bcast) v = v + e.bcast[(size_t)b * a.Cout + m];
-    if (e.skip) v = v + e.skip[oidx];
+    if (e.bcast) v = v + p.bcast;
+    if (e.skip) v = v + p.skip;
+    if (e.ddim_coef) {
+        float x0;
+        e.ddim_x[oidx] = ddim_update(p.x, v, e.ddim_coef, e.ddim_eta, x0);
+        if (e.ddim_x0_log) e.ddim_x0_log[oidx] = x0;
+        if (e.ddim_eps_log) e.ddim_eps_log[oidx] = v;
+        if (a.y) a.y[oidx] = v;
+        return;
+    }
     a.y[oidx] = v;
 }
 
-// Split-K partial tiles (one per wave) live in LDS; sum in wave order, then epilogue.
-template <int BM, int BN, int WK>
-__device__ __forceinline__ void reduce_and_store(const ConvArgs& a, const float* smem, int m0, int n0, int ph) {
+__device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, int oy, int ox, float v) {
+    const size_t oidx = (((size_t)b * a.Cout + m) * a.Hout + oy) * a.Wout + ox;
+    epi_finish(a, m, oidx, v, epi_prefetch(a, m, b, oidx));
+}
+
+// ------------------------------------------------------------------------------------------------
+// MFMA traits
+// ------------------------------------------------------------------------------------------------
+template <int KIND>
+struct Mfma;
+
+template <>
+struct Mfma<1> {
+    static constexpr int TILE = 32, NLG = 2, NACC = 16;
+    typedef floatx16 acc_t;
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int r, int lg) { return (r & 3) + 8 * (r >> 2) + 4 * lg; }
+};
+
+template <>
+struct Mfma<2> {
+    static constexpr int TILE = 16, NLG = 4, NACC = 4;
+    typedef floatx4 acc_t;
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int r, int lg) { return 4 * lg + r; }
+};
+
+constexpr int kGroup = 4;   // K-chunks per prefetch group
+
+template <int TM, int TN>
+struct Frag {
+    floatx4 a[TM];
+    float b[TN][4];
+};
+
+// ------------------------------------------------------------------------------------------------
+// kinds 1/2: block = WK waves over one (TILE*TM x TILE*TN) output tile of one phase; each wave owns
+// every WK-th K-chunk, register-pipelined in groups of kGroup chunks.
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int TM, int TN, int WK>
+__global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
+    using MF = Mfma<KIND>;
+    constexpr int TILE = MF::TILE, NLG = MF::NLG, CK = 4 * NLG;
+    constexpr int BM = TILE * TM, BN = TILE * TN;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63;
+    // wave index made provably uniform: chunk / tap indices then live in SGPRs and the tap-table
+    // lookups below are scalar kernarg loads (lgkmcnt), not per-lane global loads that would force a
+    // vmcnt(0) drain of the prefetched operands on every chunk.
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ph = blockIdx.z;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int HqWq = a.pt.Hq * a.pt.Wq;
     const int Nq = a.B * HqWq;
-    for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
-        const int mloc = e / BN, nloc = e - mloc * BN;
-        const int m = m0 + mloc, n = n0 + nloc;
-        if (m >= a.Cout || n >= Nq) continue;
-        float v = smem[e];
+    const int HWin = a.Hin * a.Win;
+    const int col = lane % TILE, lg = lane / TILE;
+
+    // Operands come through bounds-checked buffer loads: one SGPR descriptor per tensor, a per-lane
+    // 32-bit byte offset fixed for a whole tap, and a scalar soffset that walks the K chunks — so the
+    // K loop spends no VALU on addressing, and an input pixel outside the window (padding) is simply an
+    // out-of-range offset that the hardware returns as 0.
+    constexpr int kOOB = 0x7ffffff0;
+    // per output column: top-left input pixel (iy0, ix0) of its window and the byte offset of
+    // (b, channel lg, iy0, ix0); a tap then only adds the uniform (dy, dx).  Invalid columns get
+    // iy0 = -0x4000000 so every tap falls outside the window.
+    int iy0[TN], ix0[TN], base4[TN];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
-        const int b = n / HqWq;
-        const int r = n - b * HqWq;
-        const int qy = r / a.pt.Wq;
+    for (int ni = 0; ni < TN; ++ni) {
+        const int n = n0 + TILE * ni + col;
+        const bool nv = n < Nq;
+        const int nn = nv ? n : 0;
+        const int b = a.fd_hw.div(nn);
+        const int r = nn - b * HqWq;
+        const int qy = a.fd_w.div(r);
         const int qx = r - qy * a.pt.Wq;
-        epilogue_store(a, m, b, qy * a.pt.osy + a.pt.ry[ph], qx * a.pt.osy + a.pt.rx[ph], v);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// kind 1: v_mfma_f32_32x32x2_f32.  Block = WK waves, tile (32TM x 32TN); each wave owns every WK-th
-// 8-deep K chunk of the whole tile.
-// ------------------------------------------------------------------------------------------------
-template <int TM, int TN, int WK>
-__global__ __launch_bounds__(64 * WK) void conv_mfma32_kernel(ConvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int BM = 32 * TM, BN = 32 * TN;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int ph = blockIdx.z;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-    const int HqWq = a.pt.Hq * a.pt.Wq;
-    const int Nq = a.B * HqWq;
-    const int HWin = a.Hin * a.Win;
-    const int col = lane & 31, h = lane >> 5;
-
-    int qy[TN], qx[TN];
-    const float* xb[TN];
-    bool nv[TN];
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-        const int n = n0 + 32 * ni + col;
-        nv[ni] = n < Nq;
-        const int nn = nv[ni] ? n : 0;
-        const int b = nn / HqWq;
-        const int r = nn - b * HqWq;
-        qy[ni] = r / a.pt.Wq;
-        qx[ni] = r - qy[ni] * a.pt.Wq;
-        xb[ni] = a.x + ((size_t)b * a.Cin + h) * HWin;
+        iy0[ni] = nv ? qy * a.pt.sy : -0x4000000;
+        ix0[ni] = qx * a.pt.sy;
+        base4[ni] = ((b * a.Cin + lg) * HWin + iy0[ni] * a.Win + ix0[ni]) * 4;
     }
 
-    floatx16 acc[TM][TN];
+    typename MF::acc_t acc[TM][TN];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+            for (int r = 0; r < MF::NACC; ++r) acc[mi][ni][r] = 0.f;
 
-    const int cin8 = a.Cin >> 3;
+    const int cpt = a.Cin / CK;   // chunks per tap
     const int nchunk = a.pt.kchunks[ph];
-    const size_t wstride = (size_t)a.Mpad * 8;
-    const float* wp = a.w + a.pt.wofs[ph] + (size_t)(m0 + col) * 8 + h * 4;
+    const int wstride_b = a.Mpad * CK * 4;                 // bytes per packed chunk
+    const int nmine = nchunk > wave ? (nchunk - wave + WK - 1) / WK : 0;
+    const int ngrp = (nmine + kGroup - 1) / kGroup;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.B * a.Cin * HWin * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.w + a.pt.wofs[ph]), (short)0, nchunk * wstride_b, 0x00020000);
+    const int a_voff = ((m0 + col) * CK + lg * 4) * 4;
+    const int cstep_b = CK * HWin * 4;                     // bytes per channel chunk in x
 
-    int t_cur = -1;
-    int off[TN];
-    bool ok[TN];
-    for (int c = wave; c < nchunk; c += WK) {
-        const int t = c / cin8;
-        const int ci0 = (c - t * cin8) << 3;
-        if (t != t_cur) {
-            t_cur = t;
-            const int dy = a.pt.dy[ph][t], dx = a.pt.dx[ph][t];
+    // Epilogue operands of the outputs this thread will finish (element e = tid + k*64*WK of the tile),
+    // issued now so they land while the K loop runs.
+    constexpr int EPT = (BM * BN + 64 * WK - 1) / (64 * WK);
+    constexpr bool kPre = EPT <= 8;
+    EpiPre pre[kPre ? EPT : 1];
+    int po[kPre ? EPT : 1], pm[kPre ? EPT : 1];
+    if constexpr (kPre) {
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) {
-                const int iy = qy[ni] * a.pt.sy + dy, ix = qx[ni] * a.pt.sy + dx;
-                ok[ni] = nv[ni] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-                off[ni] = ok[ni] ? iy * a.Win + ix : 0;
-            }
+        for (int k = 0; k < EPT; ++k) {
+            const int e = (int)threadIdx.x + k * 64 * WK;
+            const int mloc = e / BN, nloc = e - mloc * BN;
+            const int m = m0 + mloc, n = n0 + nloc;
+            const bool valid = e < BM * BN && m < a.Cout && n < Nq;
+            const int mm = valid ? m : 0, nn = valid ? n : 0;
+            const int b = a.fd_hw.div(nn);
+            const int r = nn - b * HqWq;
+            const int qyy = a.fd_w.div(r);
+            const int qxx = r - qyy * a.pt.Wq;
+            const int oy = qyy * a.pt.osy + a.pt.ry[ph], ox = qxx * a.pt.osy + a.pt.rx[ph];
+            const size_t oidx = (((size_t)b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
+            pre[k] = epi_prefetch(a, mm, b, oidx);
+            po[k] = valid ? (int)oidx : -1;
+            pm[k] = mm;
         }
-        floatx4 av[TM];
-#pragma unroll
-        for (int mi = 0; mi < TM; ++mi) av[mi] = *(const floatx4*)(wp + c * wstride + mi * 32 * 8);
-        float bv[TN][4];
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni) {
-            const float* p = xb[ni] + (size_t)ci0 * HWin + off[ni];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[ni][j] = ok[ni] ? p[(size_t)(2 * j) * HWin] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-                for (int ni = 0; ni < TN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni], 0, 0, 0);
     }
 
+    // K cursor (wave-uniform): chunk c = wave + WK*i  <->  (tap t, channel chunk cc), advanced without
+    // division; per-lane tap offsets are recomputed only when the tap changes.
+    int t_ld = wave / cpt, cc_ld = wave - (wave / cpt) * cpt, c_ld = wave;
+    int tcur = -1;
+    int voff[TN];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) voff[ni] = kOOB;
+
+    // Loads are unconditional (past this wave's range the cursor stays on its last chunk and the
+    // compute is skipped): every path has the same loads in flight, so the vmcnt bookkeeping stays
+    // exact and the next group's loads really overlap this group's MFMAs.
+    auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) {
+            const int i = grp * kGroup + q;
+            if (t_ld != tcur) {
+                tcur = t_ld;
+                const int dy = a.pt.dy[ph][t_ld], dx = a.pt.dx[ph][t_ld];
+                const int dxy4 = (dy * a.Win + dx) * 4;   // uniform
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const bool ok = (unsigned)(iy0[ni] + dy) < (unsigned)a.Hin && (unsigned)(ix0[ni] + dx) < (unsigned)a.Win;
+                    voff[ni] = ok ? base4[ni] + dxy4 : kOOB;
+                }
+            }
+            const int soff_a = c_ld * wstride_b;
+            const int soff_b = cc_ld * cstep_b;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+                f[q].a[mi] = __builtin_bit_cast(
+                    floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    f[q].b[ni][j] = __builtin_bit_cast(
+                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], soff_b + NLG * j * HWin * 4, 0));
+            if (i + 1 < nmine) {   // advance the cursor to this wave's next chunk
+                c_ld += WK;
+                cc_ld += WK;
+                while (cc_ld >= cpt) {
+                    cc_ld -= cpt;
+                    ++t_ld;
+                }
+            }
+        }
+    };
+    auto compute = [&](const Frag<TM, TN>(&f)[kGroup], int grp) {
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) {
+            if (grp * kGroup + q < nmine) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni)
+                            acc[mi][ni] = MF::mma(f[q].a[mi][j], f[q].b[ni][j], acc[mi][ni]);
+            }
+        }
+    };
+
+    Frag<TM, TN> f0[kGroup], f1[kGroup];
+    if (ngrp > 0) {
+        load(f0, 0);
+        for (int g = 0; g < ngrp; g += 2) {
+            load(f1, g + 1);    // may be past the end: clamped + masked
+            compute(f0, g);
+            if (g + 2 < ngrp) load(f0, g + 2);
+            compute(f1, g + 1);
+        }
+    }
+
+    // split-K partial tiles -> LDS, fixed-order sum, fused epilogue
     float* sw = smem + wave * BM * BN;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int mloc = 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h;
-                sw[mloc * BN + 32 * ni + col] = acc[mi][ni][r];
-            }
+            for (int r = 0; r < MF::NACC; ++r)
+                sw[(TILE * mi + MF::row(r, lg)) * BN + TILE * ni + col] = acc[mi][ni][r];
     __syncthreads();
-    reduce_and_store<BM, BN, WK>(a, smem, m0, n0, ph);
-}
-
-// ------------------------------------------------------------------------------------------------
-// kind 2: v_mfma_f32_16x16x4_f32 (4x the tiles of kind 1 for the same M x N: used where M*N is small)
-// ------------------------------------------------------------------------------------------------
-template <int TM, int TN, int WK>
-__global__ __launch_bounds__(64 * WK) void conv_mfma16_kernel(ConvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int BM = 16 * TM, BN = 16 * TN;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int ph = blockIdx.z;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-    const int HqWq = a.pt.Hq * a.pt.Wq;
-    const int Nq = a.B * HqWq;
-    const int HWin = a.Hin * a.Win;
-    const int col = lane & 15, g = lane >> 4;
-
-    int qy[TN], qx[TN];
-    const float* xb[TN];
-    bool nv[TN];
+    if constexpr (kPre) {
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-        const int n = n0 + 16 * ni + col;
-        nv[ni] = n < Nq;
-        const int nn = nv[ni] ? n : 0;
-        const int b = nn / HqWq;
-        const int r = nn - b * HqWq;
-        qy[ni] = r / a.pt.Wq;
-        qx[ni] = r - qy[ni] * a.pt.Wq;
-        xb[ni] = a.x + ((size_t)b * a.Cin + g) * HWin;
-    }
-
-    floatx4 acc[TM][TN];
+        for (int k = 0; k < EPT; ++k) {
+            const int e = (int)threadIdx.x + k * 64 * WK;
+            if (po[k] < 0) continue;
+            float v = smem[e];
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
-
-    const int cin16 = a.Cin >> 4;
-    const int nchunk = a.pt.kchunks[ph];
-    const size_t wstride = (size_t)a.Mpad * 16;
-    const float* wp = a.w + a.pt.wofs[ph] + (size_t)(m0 + col) * 16 + g * 4;
-
-    int t_cur = -1;
-    int off[TN];
-    bool ok[TN];
-    for (int c = wave; c < nchunk; c += WK) {
-        const int t = c / cin16;
-        const int ci0 = (c - t * cin16) << 4;
-        if (t != t_cur) {
-            t_cur = t;
-            const int dy = a.pt.dy[ph][t], dx = a.pt.dx[ph][t];
-#pragma unroll
-            for (int ni = 0; ni < TN; ++ni) {
-                const int iy = qy[ni] * a.pt.sy + dy, ix = qx[ni] * a.pt.sy + dx;
-                ok[ni] = nv[ni] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-                off[ni] = ok[ni] ? iy * a.Win + ix : 0;
-            }
+            for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+            epi_finish(a, pm[k], (size_t)po[k], v, pre[k]);
         }
-        floatx4 av[TM];
+    } else {
+        for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
+            const int mloc = e / BN, nloc = e - mloc * BN;
+            const int m = m0 + mloc, n = n0 + nloc;
+            if (m >= a.Cout || n >= Nq) continue;
+            float v = smem[e];
 #pragma unroll
-        for (int mi = 0; mi < TM; ++mi) av[mi] = *(const floatx4*)(wp + c * wstride + mi * 16 * 16);
-        float bv[TN][4];
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni) {
-            const float* p = xb[ni] + (size_t)ci0 * HWin + off[ni];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[ni][j] = ok[ni] ? p[(size_t)(4 * j) * HWin] : 0.f;
+            for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+            const int b = n / HqWq;
+            const int r = n - b * HqWq;
+            const int qyy = r / a.pt.Wq;
+            const int qxx = r - qyy * a.pt.Wq;
+            epilogue_store(a, m, b, qyy * a.pt.osy + a.pt.ry[ph], qxx * a.pt.osy + a.pt.rx[ph], v);
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-                for (int ni = 0; ni < TN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mi][j], bv[ni][j], acc[mi][ni], 0, 0, 0);
     }
-
-    float* sw = smem + wave * BM * BN;
-#pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mloc = 16 * mi + 4 * g + r;
-                sw[mloc * BN + 16 * ni + col] = acc[mi][ni][r];
-            }
-    __syncthreads();
-    reduce_and_store<BM, BN, WK>(a, smem, m0, n0, ph);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -396,14 +460,14 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight packing into fragment order
+// weight packing into fragment order: packed[phase][chunk][Mpad][NLG][4], k = chunk*CK + NLG*j + lg
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w, float* __restrict__ out, ConvArgs a,
                                                         int kind, int64_t total) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const int ck = kind == 1 ? 8 : 16;
-    // find phase
+    const int nlg = kind == 1 ? 2 : 4;
+    const int ck = 4 * nlg;
     int ph = 0;
     for (int p = 1; p < a.pt.nphase; ++p)
         if (idx >= a.pt.wofs[p]) ph = p;
@@ -412,15 +476,8 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict_
     const int64_t rowid = local / ck;
     const int m = (int)(rowid % a.Mpad);
     const int c = (int)(rowid / a.Mpad);
-    int kin;
-    if (kind == 1) {
-        const int hh = slot >> 2, j = slot & 3;   // slot = h*4 + j, k = 2j + h
-        kin = 2 * j + hh;
-    } else {
-        const int g = slot >> 2, j = slot & 3;    // slot = g*4 + j, k = 4j + g
-        kin = 4 * j + g;
-    }
-    const int k = c * ck + kin;
+    const int lg = slot >> 2, j = slot & 3;
+    const int k = c * ck + nlg * j + lg;
     const int t = k / a.Cin, ci = k - t * a.Cin;
     float v = 0.f;
     if (m < a.Cout && t < a.pt.ntap[ph]) {
@@ -447,6 +504,8 @@ static int make_args(const ldm_conv_desc& d, const ldm_conv_plan& p, ConvArgs& a
     a.Wout = d.Wout;
     a.KK = d.kh * d.kw;
     a.transposed = d.transposed;
+    a.fd_hw = FastDiv::make(a.pt.Hq * a.pt.Wq);
+    a.fd_w = FastDiv::make(a.pt.Wq);
     return 0;
 }
 
@@ -495,16 +554,16 @@ extern "C" int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan) {
     // direct VALU path: no 8-aligned channel chunks, or tiny output channel count
     if (d->Cin % 8 != 0 || M < 16) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, plan);
     // Heuristic (refined by the Python-side autotuner): fill >= ~2048 waves (2 per SIMD).
-    auto waves_for = [&](int kind, int tm, int tn) {
+    auto tiles_for = [&](int kind, int tm, int tn) {
         const int bm = tile_m(kind) * tm, bn = tile_m(kind) * tn;
         return (int64_t)((M + bm - 1) / bm) * ((Nq + bn - 1) / bn) * pt.nphase;
     };
     int kind = (M >= 32 && Nq >= 32) ? 1 : 2;
     if (kind == 2 && d->Cin % 16 != 0) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, plan);
-    int64_t tiles = waves_for(kind, 1, 1);
+    int64_t tiles = tiles_for(kind, 1, 1);
     if (kind == 1 && tiles * 8 < 1024 && d->Cin % 16 == 0) {
         kind = 2;
-        tiles = waves_for(kind, 1, 1);
+        tiles = tiles_for(kind, 1, 1);
     }
     const int64_t chunks = (int64_t)maxtap * (d->Cin / chunk_k(kind));
     int wk = 1;
@@ -529,71 +588,73 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     return 0;
 }
 
-#define LDM_MFMA_DISPATCH(KERNEL, TILE)                                                                   \
-    do {                                                                                                  \
-        const int BMx = TILE * p.tm, BNx = TILE * p.tn;                                                   \
-        const size_t lds = (size_t)p.wk * BMx * BNx * sizeof(float);                                      \
-        dim3 grid((unsigned)((Nq + BNx - 1) / BNx), (unsigned)((d->Cout + BMx - 1) / BMx), a.pt.nphase);  \
-        dim3 block(64 * p.wk);                                                                            \
-        const int code = (p.tm - 1) * 2 + (p.tn - 1);                                                     \
-        switch (p.wk * 10 + code) {                                                                       \
-            case 10: hipLaunchKernelGGL((KERNEL<1, 1, 1>), grid, block, lds, st, a); break;               \
-            case 11: hipLaunchKernelGGL((KERNEL<1, 2, 1>), grid, block, lds, st, a); break;               \
-            case 12: hipLaunchKernelGGL((KERNEL<2, 1, 1>), grid, block, lds, st, a); break;               \
-            case 13: hipLaunchKernelGGL((KERNEL<2, 2, 1>), grid, block, lds, st, a); break;               \
-            case 20: hipLaunchKernelGGL((KERNEL<1, 1, 2>), grid, block, lds, st, a); break;               \
-            case 21: hipLaunchKernelGGL((KERNEL<1, 2, 2>), grid, block, lds, st, a); break;               \
-            case 22: hipLaunchKernelGGL((KERNEL<2, 1, 2>), grid, block, lds, st, a); break;               \
-            case 23: hipLaunchKernelGGL((KERNEL<2, 2, 2>), grid, block, lds, st, a); break;               \
-            case 40: hipLaunchKernelGGL((KERNEL<1, 1, 4>), grid, block, lds, st, a); break;               \
-            case 41: hipLaunchKernelGGL((KERNEL<1, 2, 4>), grid, block, lds, st, a); break;               \
-            case 42: hipLaunchKernelGGL((KERNEL<2, 1, 4>), grid, block, lds, st, a); break;               \
-            case 43: hipLaunchKernelGGL((KERNEL<2, 2, 4>), grid, block, lds, st, a); break;               \
-            case 80: hipLaunchKernelGGL((KERNEL<1, 1, 8>), grid, block, lds, st, a); break;               \
-            case 81: hipLaunchKernelGGL((KERNEL<1, 2, 8>), grid, block, lds, st, a); break;               \
-            case 82: hipLaunchKernelGGL((KERNEL<2, 1, 8>), grid, block, lds, st, a); break;               \
-            case 83: hipLaunchKernelGGL((KERNEL<2, 2, 8>), grid, block, lds, st, a); break;               \
-            default: return fail(3, "conv: no kernel instance for plan");                                 \
-        }                                                                                                 \
-    } while (0)
+template <int KIND>
+static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
+    const int TILE = Mfma<KIND>::TILE;
+    const int BMx = TILE * p.tm, BNx = TILE * p.tn;
+    const size_t lds = (size_t)p.wk * BMx * BNx * sizeof(float);
+    dim3 grid((unsigned)((Nq + BNx - 1) / BNx), (unsigned)((a.Cout + BMx - 1) / BMx), a.pt.nphase);
+    dim3 block(64 * p.wk);
+    const int code = (p.tm - 1) * 2 + (p.tn - 1);
+#define LDM_CASE(WK, C, TM, TN) \
+    case WK * 10 + C: hipLaunchKernelGGL((conv_mfma_kernel<KIND, TM, TN, WK>), grid, block, lds, st, a); break;
+    switch (p.wk * 10 + code) {
+        LDM_CASE(1, 0, 1, 1) LDM_CASE(1, 1, 1, 2) LDM_CASE(1, 2, 2, 1) LDM_CASE(1, 3, 2, 2)
+        LDM_CASE(2, 0, 1, 1) LDM_CASE(2, 1, 1, 2) LDM_CASE(2, 2, 2, 1) LDM_CASE(2, 3, 2, 2)
+        LDM_CASE(4, 0, 1, 1) LDM_CASE(4, 1, 1, 2) LDM_CASE(4, 2, 2, 1) LDM_CASE(4, 3, 2, 2)
+        LDM_CASE(8, 0, 1, 1) LDM_CASE(8, 1, 1, 2) LDM_CASE(8, 2, 2, 1) LDM_CASE(8, 3, 2, 2)
+        default: return fail(3, "conv: no kernel instance for plan");
+    }
+#undef LDM_CASE
+    LDM_CHECK_LAUNCH("conv_mfma_kernel");
+    return 0;
+}
 
-extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
-                                const ldm_epilogue* ep, float* y, void* stream) {
-    LDM_REQUIRE(d && plan && x && w && y, "conv forward: null argument");
+namespace ldm {
+
+int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
+                    float* y, hipStream_t st) {
+    LDM_REQUIRE(x && w && (y || ep.ddim_coef), "conv forward: null argument");
+    LDM_REQUIRE(!ep.ddim_coef || ep.ddim_x, "conv forward: fused DDIM update needs x");
     ConvArgs a;
-    int rc = make_args(*d, *plan, a);
+    int rc = make_args(d, p, a);
     if (rc) return rc;
     a.x = x;
     a.w = w;
     a.y = y;
-    if (ep) {
-        a.ep.bias = ep->bias;
-        a.ep.bn_w = ep->bn_weight;
-        a.ep.bn_b = ep->bn_bias;
-        a.ep.bn_m = ep->bn_mean;
-        a.ep.bn_v = ep->bn_var;
-        a.ep.bn_eps = ep->bn_eps;
-        a.ep.act = ep->act;
-        a.ep.bcast = ep->bcast_add;
-        a.ep.skip = ep->skip_add;
-        LDM_REQUIRE(!a.ep.bn_w || (a.ep.bn_b && a.ep.bn_m && a.ep.bn_v), "conv: incomplete BatchNorm parameters");
-    }
-    hipStream_t st = (hipStream_t)stream;
-    const ldm_conv_plan& p = *plan;
-    const int64_t Nq = (int64_t)d->B * a.pt.Hq * a.pt.Wq;
+    a.ep = ep;
+    LDM_REQUIRE(!a.ep.bn_w || (a.ep.bn_b && a.ep.bn_m && a.ep.bn_v), "conv: incomplete BatchNorm parameters");
+    const int64_t Nq = (int64_t)d.B * a.pt.Hq * a.pt.Wq;
     if (p.kind == 0) {
-        const int64_t total = (int64_t)d->B * d->Cout * d->Hout * d->Wout;
+        const int64_t total = (int64_t)d.B * d.Cout * d.Hout * d.Wout;
         hipLaunchKernelGGL(conv_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
         LDM_CHECK_LAUNCH("conv_direct_kernel");
         return 0;
     }
-    LDM_REQUIRE(plan_ok(*d, p.kind, p.tm, p.tn, p.wk), "conv forward: invalid plan");
-    if (p.kind == 1) {
-        LDM_MFMA_DISPATCH(conv_mfma32_kernel, 32);
-        LDM_CHECK_LAUNCH("conv_mfma32_kernel");
-    } else {
-        LDM_MFMA_DISPATCH(conv_mfma16_kernel, 16);
-        LDM_CHECK_LAUNCH("conv_mfma16_kernel");
+    LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk), "conv forward: invalid plan");
+    // buffer descriptors use 32-bit byte offsets; padding lanes use offset 0x7ffffff0 (out of range)
+    LDM_REQUIRE((int64_t)d.B * d.Cin * d.Hin * d.Win * 4 < 0x7ff00000LL &&
+                    p.packed_floats * 4 < 0x7ff00000LL,
+                "conv forward: tensor too large for 32-bit buffer offsets (split the batch)");
+    return p.kind == 1 ? launch_mfma<1>(a, p, Nq, st) : launch_mfma<2>(a, p, Nq, st);
+}
+
+}  // namespace ldm
+
+extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
+                                const ldm_epilogue* ep, float* y, void* stream) {
+    LDM_REQUIRE(d && plan && x && w && y, "conv forward: null argument");
+    EpiArgs e{};
+    if (ep) {
+        e.bias = ep->bias;
+        e.bn_w = ep->bn_weight;
+        e.bn_b = ep->bn_bias;
+        e.bn_m = ep->bn_mean;
+        e.bn_v = ep->bn_var;
+        e.bn_eps = ep->bn_eps;
+        e.act = ep->act;
+        e.bcast = ep->bcast_add;
+        e.skip = ep->skip_add;
     }
-    return 0;
+    return conv_forward_ex(*d, *plan, x, w, e, y, (hipStream_t)stream);
 }

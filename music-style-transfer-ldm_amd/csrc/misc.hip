@@ -118,6 +118,172 @@ __global__ __launch_bounds__(256) void attention_core_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------------------------------------------
+// cross-attention core on f32 MFMA: one block (4 waves) per (b, head).
+//   S = (q*scale)^T k   : A[m=l][k=c] = q[c][l], B[k=c][n=s] = k[c][s] — both read straight from the
+//                         channel-major projections (lanes walk l / s: coalesced), tiles round-robin
+//                         over waves, written to LDS
+//   P = softmax_s(S)    : one wave per query row, padded columns -> 0
+//   O = V P^T           : A[m=c][k=s] = V[c][s] (staged in LDS), B[k=s][n=l] = P[l][s] (LDS),
+//                         stored channel-major out[b][h*d+c][l] (coalesced along l)
+// KIND 1 = v_mfma_f32_32x32x2_f32 (L, S > 16), KIND 2 = v_mfma_f32_16x16x4_f32 (small maps).
+// ------------------------------------------------------------------------------------------------
+template <int KIND>
+struct AMfma;
+template <>
+struct AMfma<1> {
+    static constexpr int TILE = 32, NLG = 2, NACC = 16;
+    typedef floatx16 acc_t;
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int r, int lg) { return (r & 3) + 8 * (r >> 2) + 4 * lg; }
+};
+template <>
+struct AMfma<2> {
+    static constexpr int TILE = 16, NLG = 4, NACC = 4;
+    typedef floatx4 acc_t;
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int r, int lg) { return 4 * lg + r; }
+};
+
+// Compile-time padded sizes LP x SP and head dim D (instances in ldm_attention_core); the actual L, S
+// (<= LP, SP) are runtime and masked.  All index math folds to shifts.
+// Each block owns LT query rows of one (b, head): grid = B * heads * (LP / LT).
+template <int KIND, int LP, int SP, int D, int LT>
+__global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                             float* __restrict__ out, int E, int heads, int L, int S,
+                                                             float scale) {
+    using MF = AMfma<KIND>;
+    constexpr int TILE = MF::TILE, NLG = MF::NLG;
+    static_assert(LT % TILE == 0 && LP % LT == 0, "query split");
+    constexpr int KBQ = D / NLG < 16 ? D / NLG : 16;     // k-steps per register batch (QK^T)
+    constexpr int KBP = SP / NLG < 16 ? SP / NLG : 16;    // (PV)
+    static_assert(LP % TILE == 0 && SP % TILE == 0 && D % TILE == 0 && D % (KBQ * NLG) == 0 &&
+                      SP % (KBP * NLG) == 0 && SP <= 64 * 64,
+                  "attention instance shape");
+    constexpr int LDP = SP + 1;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ps = sm;               // [LT][SP+1]  (rows l0 .. l0+LT-1)
+    float* Vs = sm + LT * LDP;    // [D][SP+1]
+    constexpr int NSPLIT = LP / LT;
+    const int l0 = (blockIdx.x % NSPLIT) * LT;
+    const int bh = blockIdx.x / NSPLIT;
+    const int h = bh % heads, b = bh / heads;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane % TILE, lg = lane / TILE;
+    const float* qb = q + ((size_t)b * E + (size_t)h * D) * L;
+    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
+    const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
+
+    // stage V [D][S] -> LDS [D][SP+1]: every load of this thread issues before any LDS store
+    {
+        constexpr int NV = (D * SP + 255) / 256;
+        float v[NV];
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = u * 256 + (int)threadIdx.x;
+            const int c = e / SP, s = e % SP;
+            v[u] = vb[(e < D * SP && s < S) ? c * S + s : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = u * 256 + (int)threadIdx.x;
+            const int c = e / SP, s = e % SP;
+            if (e < D * SP) Vs[c * LDP + s] = s < S ? v[u] : 0.f;
+        }
+    }
+    // S = (q*scale)^T k for this block's LT rows: tiles round-robin over the 4 waves
+    constexpr int NTL = LT / TILE, NTS = SP / TILE;
+    for (int tile = wave; tile < NTL * NTS; tile += 4) {
+        const int lt = tile / NTS, st = tile % NTS;
+        const int l = l0 + lt * TILE + col, s = st * TILE + col;
+        const bool lok = l < L, sok = s < S;
+        typename MF::acc_t acc;
+#pragma unroll
+        for (int r = 0; r < MF::NACC; ++r) acc[r] = 0.f;
+        const float* qp = qb + lg * L + (lok ? l : 0);
+        const float* kp = kb + lg * S + (sok ? s : 0);
+#pragma unroll
+        for (int k0 = 0; k0 < D; k0 += KBQ * NLG) {
+            float av[KBQ], bv[KBQ];
+#pragma unroll
+            for (int j = 0; j < KBQ; ++j) {   // the whole batch in flight before its MFMAs
+                av[j] = qp[(k0 + NLG * j) * L];
+                bv[j] = kp[(k0 + NLG * j) * S];
+            }
+#pragma unroll
+            for (int j = 0; j < KBQ; ++j)
+                acc = MF::mma(lok ? av[j] * scale : 0.f, sok ? bv[j] : 0.f, acc);   // q_scaled = q * sqrt(1/d)
+        }
+#pragma unroll
+        for (int r = 0; r < MF::NACC; ++r) Ps[(lt * TILE + MF::row(r, lg)) * LDP + st * TILE + col] = acc[r];
+    }
+    __syncthreads();
+    // softmax over s: RPW = 64/SP rows per wave pass, one lane per column, segmented shuffles
+    {
+        constexpr int RPW = SP >= 64 ? 1 : 64 / SP;
+        constexpr int SEG = SP >= 64 ? 64 : SP;
+        const int sub = lane / SEG, s0 = lane % SEG;
+        for (int r0 = wave * RPW; r0 < LT; r0 += 4 * RPW) {
+            const int r = r0 + sub;             // local row; global query row l0 + r
+            float* row = Ps + r * LDP;
+            float x[SP / SEG];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < SP / SEG; ++u) {
+                const int s = s0 + u * SEG;
+                x[u] = row[s];
+                if (s < S) mx = fmaxf(mx, x[u]);
+            }
+#pragma unroll
+            for (int o = SEG / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            float sum = 0.f;
+#pragma unroll
+            for (int u = 0; u < SP / SEG; ++u) {
+                const int s = s0 + u * SEG;
+                x[u] = s < S ? expf(x[u] - mx) : 0.f;
+                sum += x[u];
+            }
+#pragma unroll
+            for (int o = SEG / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+#pragma unroll
+            for (int u = 0; u < SP / SEG; ++u) row[s0 + u * SEG] = l0 + r < L ? x[u] / sum : 0.f;
+        }
+    }
+    __syncthreads();
+    // O[c][l] = sum_s V[c][s] P[l][s]
+    constexpr int NTC = D / TILE;
+    float* ob = out + ((size_t)b * E + (size_t)h * D) * L;
+    for (int tile = wave; tile < NTC * NTL; tile += 4) {
+        const int ct = tile / NTL, lt = tile % NTL;
+        typename MF::acc_t acc;
+#pragma unroll
+        for (int r = 0; r < MF::NACC; ++r) acc[r] = 0.f;
+        const float* va = Vs + (ct * TILE + col) * LDP + lg;
+        const float* pb = Ps + (lt * TILE + col) * LDP + lg;
+#pragma unroll
+        for (int k0 = 0; k0 < SP; k0 += KBP * NLG) {
+            float av[KBP], bv[KBP];
+#pragma unroll
+            for (int j = 0; j < KBP; ++j) {
+                av[j] = va[k0 + NLG * j];
+                bv[j] = pb[k0 + NLG * j];
+            }
+#pragma unroll
+            for (int j = 0; j < KBP; ++j) acc = MF::mma(av[j], bv[j], acc);
+        }
+        const int l = l0 + lt * TILE + col;
+        if (l < L) {
+#pragma unroll
+            for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * L + l] = acc[r];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // scheduler updates
 // ------------------------------------------------------------------------------------------------
 // coef_table [T,2] = {sqrt(ab), sqrt(1-ab)} per timestep (host-computed with the reference's fp32
@@ -186,16 +352,9 @@ __global__ __launch_bounds__(256) void ddim_step_kernel(float* __restrict__ x, c
                                                         int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float sat = coef[0], s1t = coef[1], san = coef[2], s1n = coef[3];
     const float e = eps[i];
-    const float xv = x[i];
-    // model.py:446-458, one fp32 rounding per reference op
-    const float dxt = s1t * e;                 // sqrt(1-ab_t) * noise_pred (also inside predict_start)
-    const float x0 = (xv - dxt) / sat;         // predict_start_from_noise
-    const float dxn = s1n * e;                 // direction_xt_next
-    const float nc = eta * (dxn - dxt);        // noise_contribution
-    const float t1 = san * x0;
-    x[i] = (t1 + dxn) + nc;
+    float x0;
+    x[i] = ddim_update(x[i], e, coef, eta, x0);   // model.py:446-458
     if (x0_log) x0_log[i] = x0;
     if (eps_log) eps_log[i] = e;
 }
@@ -372,6 +531,27 @@ extern "C" int ldm_attention_core(const float* q, const float* kv, float* out, i
     LDM_REQUIRE(q && kv && out, "attention: null argument");
     LDM_REQUIRE(B > 0 && heads > 0 && E % heads == 0 && L > 0 && S > 0, "attention: bad shape");
     const int d = E / heads;
+    {
+        // compile-time instances covering the UNet's maps (128x512 mel: L=64 / 16; 128x128: 16 / 4)
+        hipStream_t st = (hipStream_t)stream;
+        const dim3 blk(256);
+#define LDM_ATT(KIND, LP, SP, D, LT)                                                                      \
+    if (d == D && L <= LP && S <= SP) {                                                                   \
+        const size_t lds = ((size_t)LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);              \
+        hipLaunchKernelGGL((attention_mfma_kernel<KIND, LP, SP, D, LT>), dim3(B * heads * (LP / LT)), blk, lds, st, \
+                           q, kv, out, E, heads, L, S, scale);                                            \
+        LDM_CHECK_LAUNCH("attention_mfma_kernel");                                                        \
+        return 0;                                                                                         \
+    }
+        LDM_ATT(2, 16, 16, 64, 16)
+        LDM_ATT(2, 16, 16, 128, 16)
+        LDM_ATT(2, 32, 32, 64, 16)
+        LDM_ATT(2, 32, 32, 128, 16)
+        LDM_ATT(2, 64, 64, 64, 16)
+        LDM_ATT(2, 64, 64, 128, 16)
+#undef LDM_ATT
+    }
+    // generic VALU fallback (head dims not a multiple of the MFMA tile)
     const size_t lds = ((size_t)d * kAttnLT + 2 * (size_t)d * S + (size_t)kAttnLT * S) * sizeof(float);
     LDM_REQUIRE(lds <= 64 * 1024, "attention: head tile exceeds LDS budget");
     const int ltiles = (L + kAttnLT - 1) / kAttnLT;

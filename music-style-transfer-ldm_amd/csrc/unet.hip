@@ -118,17 +118,34 @@ static UNetWs carve(const ldm_unet_shape& s, float* base) {
     return w;
 }
 
+// Optional fusion of the reverse-loop update into dec1's epilogue (see EpiArgs::ddim_*).
+struct DdimFuse {
+    const float* coef;
+    float eta;
+    float* x;
+    float* x0_log;
+    float* eps_log;
+};
+
 static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& plan, const float* x, const float* w,
-                     const float* bias, int act, const float* bcast, const float* skip, float* y, hipStream_t st) {
+                     const float* bias, int act, const float* bcast, const float* skip, float* y, hipStream_t st,
+                     const DdimFuse* fuse = nullptr) {
     ldm_conv_desc d;
     int rc = layer_desc(s, layer, d);
     if (rc) return rc;
-    ldm_epilogue ep{};
+    EpiArgs ep{};
     ep.bias = bias;
     ep.act = act;
-    ep.bcast_add = bcast;
-    ep.skip_add = skip;
-    return ldm_conv_forward(&d, &plan, x, w, &ep, y, st);
+    ep.bcast = bcast;
+    ep.skip = skip;
+    if (fuse) {
+        ep.ddim_coef = fuse->coef;
+        ep.ddim_eta = fuse->eta;
+        ep.ddim_x = fuse->x;
+        ep.ddim_x0_log = fuse->x0_log;
+        ep.ddim_eps_log = fuse->eps_log;
+    }
+    return conv_forward_ex(d, plan, x, w, ep, y, st);
 }
 
 #define LDM_TRY(expr)            \
@@ -139,14 +156,18 @@ static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& pl
 
 static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* z, const void* t,
                         int t_is_float, const float* s5, const float* s6, float* out, const UNetWs& ws,
-                        hipStream_t st) {
+                        hipStream_t st, const float* temb_pre = nullptr, const DdimFuse* fuse = nullptr) {
     const int HW = s.H * s.W;
     const int L2 = HW / 16, L1 = HW / 64;
     // t_embedding = time_mlp(t)[:, :, None, None]                               (model.py:203)
-    LDM_TRY(ldm_time_mlp_forward(t, t_is_float, s.B, 128, w.t_freqs, w.t_w1, w.t_b1, w.t_w2, w.t_b2, ws.temb, st));
+    const float* temb = temb_pre;
+    if (!temb) {
+        LDM_TRY(ldm_time_mlp_forward(t, t_is_float, s.B, 128, w.t_freqs, w.t_w1, w.t_b1, w.t_w2, w.t_b2, ws.temb, st));
+        temb = ws.temb;
+    }
     // z1 = relu(enc1(z)); z2 = relu(enc2(z1)) + t_emb; z3 = relu(enc3(z2))      (model.py:205-209)
     LDM_TRY(conv_call(s, 0, w.conv_plan[0], z, w.conv_w[0], w.conv_b[0], LDM_ACT_RELU, nullptr, nullptr, ws.z1, st));
-    LDM_TRY(conv_call(s, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, ws.temb, nullptr, ws.z2, st));
+    LDM_TRY(conv_call(s, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, temb, nullptr, ws.z2, st));
     LDM_TRY(conv_call(s, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
     // z3 = cross_attention2(z3, s5)                                              (model.py:211)
     LDM_TRY(conv_call(s, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
@@ -164,7 +185,8 @@ static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, cons
     LDM_TRY(conv_call(s, 5, w.conv_plan[5], ws.zb, w.conv_w[5], w.conv_b[5], LDM_ACT_RELU, nullptr, ws.z3, ws.d4, st));
     LDM_TRY(conv_call(s, 6, w.conv_plan[6], ws.d4, w.conv_w[6], w.conv_b[6], LDM_ACT_RELU, nullptr, ws.z2, ws.d3, st));
     LDM_TRY(conv_call(s, 7, w.conv_plan[7], ws.d3, w.conv_w[7], w.conv_b[7], LDM_ACT_RELU, nullptr, ws.z1, ws.d2, st));
-    LDM_TRY(conv_call(s, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, out, st));
+    LDM_TRY(conv_call(s, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, out, st,
+                      fuse));
     return 0;
 }
 
@@ -209,15 +231,28 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
                                float eta, float* x0_logs, float* eps_logs, float* workspace, void* stream) {
     LDM_REQUIRE(s && w && x && s5 && s6 && t_table && coef_table && workspace, "ddim_sample: null argument");
     LDM_REQUIRE(nsteps >= 0, "ddim_sample: negative step count");
+    if (nsteps == 0) return 0;
     UNetWs ws = carve(*s, workspace);
+    float* temb_all = workspace + ws.total;   // [nsteps*B, 128] (ldm_ddim_workspace_floats)
     const int64_t n = (int64_t)s->B * s->C * s->H * s->W;
     hipStream_t st = (hipStream_t)stream;
+    // The time MLP depends only on t: all nsteps*B embeddings in one launch before the loop (the same
+    // evaluations the reference makes one step at a time, model.py:203).
+    LDM_TRY(ldm_time_mlp_forward(t_table, 0, nsteps * s->B, 128, w->t_freqs, w->t_w1, w->t_b1, w->t_w2, w->t_b2,
+                                 temb_all, st));
     for (int i = 0; i < nsteps; ++i) {
         // noise_pred = unet(x, t, style_embedding)                                (model.py:439)
-        LDM_TRY(unet_forward(*s, *w, x, t_table + (size_t)i * s->B, 0, s5, s6, ws.eps, ws, st));
-        // x0 / direction / eta update and the two log clones                      (model.py:442-463)
-        LDM_TRY(ldm_ddim_step(x, ws.eps, coef_table + 4 * (size_t)i, eta, x0_logs ? x0_logs + (size_t)i * n : nullptr,
-                              eps_logs ? eps_logs + (size_t)i * n : nullptr, n, st));
+        // and, fused into dec1's epilogue, the x0 / direction / eta update and the two log clones
+        // (model.py:442-463) — bitwise the same fp32 op sequence as ldm_ddim_step.
+        DdimFuse fuse{coef_table + 4 * (size_t)i, eta, x, x0_logs ? x0_logs + (size_t)i * n : nullptr,
+                      eps_logs ? eps_logs + (size_t)i * n : nullptr};
+        LDM_TRY(unet_forward(*s, *w, x, t_table + (size_t)i * s->B, 0, s5, s6, nullptr, ws, st,
+                             temb_all + (size_t)i * s->B * 128, &fuse));
     }
     return 0;
+}
+
+extern "C" int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps) {
+    if (!s || nsteps < 0) return -1;
+    return carve(*s, nullptr).total + (int64_t)nsteps * s->B * 128;
 }

@@ -82,6 +82,7 @@ SIGNATURES = {
     "ldm_loss_forward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_vp, c_fp, c_vp]),
     "ldm_loss_backward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_vp]),
     "ldm_unet_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape)]),
+    "ldm_ddim_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape), c_int32]),
     "ldm_unet_make_plans": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights)]),
     "ldm_unet_layer_desc": (c_int32, [ctypes.POINTER(UNetShape), c_int32, ctypes.POINTER(ConvDesc)]),
     "ldm_unet_forward": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_vp, c_int32,

@@ -110,13 +110,13 @@ class UNetEngine:
         self._bound[skey] = (vkey, w)
         return w
 
-    def workspace(self, shape, device):
+    def workspace(self, shape, device, nsteps=0):
+        n = L.load().ldm_ddim_workspace_floats(byref(shape), int(nsteps))
+        if n <= 0:
+            raise RuntimeError("ldm_ddim_workspace_floats failed")
         key = (shape.B, shape.C, shape.H, shape.W, shape.nf, str(device))
         ws = self._ws.get(key)
-        if ws is None:
-            n = L.load().ldm_unet_workspace_floats(byref(shape))
-            if n <= 0:
-                raise RuntimeError("ldm_unet_workspace_floats failed")
+        if ws is None or ws.numel() < n:
             ws = torch.empty(int(n), device=device, dtype=torch.float32)
             self._ws[key] = ws
         return ws
@@ -147,8 +147,8 @@ class UNetEngine:
         B, C, H, W = x.shape
         shape = self.shape(B, C, H, W)
         w = self.weights(shape)
-        ws = self.workspace(shape, x.device)
         n = t_table.shape[0]
+        ws = self.workspace(shape, x.device, n)
         L.call("ldm_ddim_sample", byref(shape), byref(w), x.data_ptr(), s5.data_ptr(), s6.data_ptr(),
                t_table.data_ptr(), coef_table.data_ptr(), n, float(eta), ops._p(x0_logs), ops._p(eps_logs),
                ws.data_ptr(), ops.stream_handle())
