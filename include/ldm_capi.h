@@ -62,6 +62,8 @@ typedef struct ldm_epilogue {
     int32_t act;            /* LDM_ACT_*                                                       */
     const float* bcast_add; /* [B,Cout] added after act (UNet time embedding, model.py:206)   */
     const float* skip_add;  /* [B,Cout,Hout,Wout] added after act (UNet skips, model.py:221) */
+    float* act_out;         /* [B,Cout,Hout,Wout] or NULL: also store act(.) before the adds  */
+                            /* (training: the activation's backward needs it)                */
 } ldm_epilogue;
 
 typedef struct ldm_conv_plan {
@@ -196,6 +198,53 @@ int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps);
 int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
                     float* x0_logs, float* eps_logs, float* workspace, void* stream);
+
+/* ---- train step backward (LDMTrainer.train_step, train.py:163-208: scaler.scale(loss).backward()) ---
+ * Data gradients of a conv are the forward kernel on the dual descriptor (conv <-> transposed conv);
+ * these are the remaining pieces.  All reductions are fixed-order (bitwise reproducible). */
+/* dW of nn.Conv2d / nn.ConvTranspose2d for descriptor d (the FORWARD descriptor): x = layer input,
+ * dy = gradient at the layer's pre-epilogue output.  dw in the torch weight layout; accumulate != 0 adds.
+ * workspace: ldm_conv_wgrad_workspace_floats(d) floats. */
+int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d);
+int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
+                             float* workspace, void* stream);
+/* Backward of the fused epilogue act(v) (+bcast[b,c]) (+skip): dv = dy*act'(v) (from act_out = act(v);
+ * GELU from pre_act = v), dbias[c] = sum dv, dbcast[b,c] = sum_hw dy.  dv / dbias / dbcast may be NULL;
+ * dv may alias dy. */
+int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B, int32_t C,
+                     int32_t HW, float* dv, float* dbias, float* dbcast, void* stream);
+/* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
+ * y = its output, x = its input; dx / dweight / dbias may be NULL. */
+int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
+                           const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
+                           int32_t HW, float* dx, float* dweight, float* dbias, void* stream);
+/* Backward of ldm_attention_core: dq [B,E,L], dkv [B,2E,S] (dK then dV). */
+int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv, int32_t B,
+                           int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream);
+
+/* ---- optimiser: torch.optim.Adam (train.py:156) + torch.amp.GradScaler (train.py:157,189-201) ----
+ * Multi-tensor: `slots` (device array) lists the parameters; the work is cut into chunks of
+ * chunk_len elements, chunk i covering slots[chunk_tensor[i]] from element chunk_start[i]. */
+typedef struct ldm_tensor_slot {
+    float* param;
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+} ldm_tensor_slot;
+/* scaler.unscale_: grad *= inv_scale[0] (device scalar, NULL = 1); found_inf[0] |= any non-finite. */
+int ldm_unscale_check(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                      int32_t nchunks, int32_t chunk_len, const float* inv_scale, int32_t* found_inf, void* stream);
+/* optimizer.step() (skipped entirely when found_inf[0] != 0, as scaler.step does). step = 1-based.
+ * decoupled = 0: torch.optim.Adam (L2 added to the gradient); 1: torch.optim.AdamW (train.py:44).
+ * Hyper-parameters are the optimizer's python floats (double); derived scalars are formed in double
+ * and cast once to fp32, as torch's Adam does. */
+int ldm_adam_step(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                  int32_t nchunks, int32_t chunk_len, double lr, double beta1, double beta2, double eps,
+                  double weight_decay, int32_t decoupled, int32_t step, const int32_t* found_inf, void* stream);
+/* scaler.update(): scale *= backoff on inf (tracker = 0), *= growth after growth_interval clean steps. */
+int ldm_update_scale(float* scale, int32_t* growth_tracker, const int32_t* found_inf, float growth_factor,
+                     float backoff_factor, int32_t growth_interval, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,514 @@
+// Backward kernels of the LDM train step (LDMTrainer.train_step, train.py:163-208): conv weight
+// gradients, activation / bias / time-embedding gradients, train-mode BatchNorm backward,
+// cross-attention backward, and the Adam update with GradScaler semantics (train.py:156-157,189-201).
+// Data gradients of convs reuse the forward implicit-GEMM kernel (conv <-> transposed conv duality).
+// Every reduction has a fixed partition and order: results are bitwise reproducible run to run.
+#include <algorithm>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace ldm {
+
+// ================================================================================================
+// weight gradient:  out[m][c][t] = sum_{b,q} Dense[b][m][q] * Gath[b][c][q*s + d_t]
+//   conv  (w [Cout][Cin][k][k]):  Dense = dY (m = co, q over Hout x Wout), Gath = X,  s = stride
+//   convT (w [Cin][Cout][k][k]):  Dense = X  (m = ci, q over Hin  x Win ), Gath = dY, s = stride
+//   d_t = (kh - pad, kw - pad); out-of-window gathers are 0.
+// GEMM M = m, N = C*T, K = B*Hq*Wq on v_mfma_f32_16x16x4_f32.  A 16-deep K chunk is 16 consecutive q
+// of one sample; lane group g holds k = 4g + j at MFMA step j (A arrives as one float4 per lane).
+// K is split over blocks (grid.z); partial tiles go to a workspace and a second kernel sums them in
+// split order.
+// ================================================================================================
+struct WgradArgs {
+    const float* dense;
+    const float* gath;
+    float* partial;   // [S][M][N]
+    int32_t B, M, C, T, N;
+    int32_t Hq, Wq, Hg, Wg, s;
+    int32_t cpb;      // chunks per sample = ceil(Hq*Wq / 16)
+    int32_t nchunk;   // B * cpb
+    int32_t per_split;
+    int32_t kw, pad;
+    FastDiv fd_cpb, fd_wq, fd_t, fd_kw;
+};
+
+__global__ __launch_bounds__(64) void wgrad_kernel(WgradArgs a) {
+    const int lane = threadIdx.x;
+    const int col = lane & 15, g = lane >> 4;
+    const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+    const int split = blockIdx.z;
+    const int HQ = a.Hq * a.Wq, HG = a.Hg * a.Wg;
+    // B-operand lane state: n -> (c, t)
+    const int n = n0 + col;
+    const bool nok = n < a.N;
+    const int c = nok ? a.fd_t.div(n) : 0;
+    const int t = nok ? n - c * a.T : 0;
+    const int kh = a.fd_kw.div(t);
+    const int dy = kh - a.pad, dx = (t - kh * a.kw) - a.pad;
+    const int m = m0 + col;
+    const bool mok = m < a.M;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int c_begin = split * a.per_split;
+    const int c_end = min(a.nchunk, c_begin + a.per_split);
+    const bool vec4 = (HQ % 4) == 0;
+    for (int ch = c_begin; ch < c_end; ++ch) {
+        const int b = a.fd_cpb.div(ch);
+        const int q0 = (ch - b * a.cpb) * 16 + 4 * g;
+        // A: Dense[b][m][q0 .. q0+3]
+        floatx4 av = {0.f, 0.f, 0.f, 0.f};
+        const float* dp = a.dense + ((size_t)b * a.M + (mok ? m : 0)) * HQ;
+        if (vec4 && q0 + 3 < HQ) {
+            av = *(const floatx4*)(dp + q0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[j] = q0 + j < HQ ? dp[q0 + j] : 0.f;
+        }
+        if (!mok) av = floatx4{0.f, 0.f, 0.f, 0.f};
+        float bv[4];
+        const float* gp = a.gath + ((size_t)b * a.C + c) * HG;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = q0 + j;
+            const int qy = a.fd_wq.div(q), qx = q - qy * a.Wq;
+            const int iy = qy * a.s + dy, ix = qx * a.s + dx;
+            const bool ok = nok && q < HQ && (unsigned)iy < (unsigned)a.Hg && (unsigned)ix < (unsigned)a.Wg;
+            const float v = gp[ok ? iy * a.Wg + ix : 0];
+            bv[j] = ok ? v : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+    }
+    float* out = a.partial + (size_t)split * a.M * a.N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int mm = m0 + 4 * g + r;
+        if (mm < a.M && nok) out[(size_t)mm * a.N + n] = acc[r];
+    }
+}
+
+// sum of split partials in split order.  Tap t is the kernel-window index (kh*kw + kw), so the
+// [m][c*T + t] GEMM layout IS the torch weight layout [m][c][kh][kw].
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial, int S, int MN,
+                                                           float* __restrict__ dw, int accumulate) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= MN) return;
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v = v + partial[(size_t)s * MN + i];
+    dw[i] = accumulate ? dw[i] + v : v;
+}
+
+// ================================================================================================
+// activation / bias / broadcast gradients of the fused conv epilogue y = act(v) (+bcast[b,c]) (+skip):
+//   dv = dy * act'(v) (act' from the saved post-activation value a = act(v)), dbias[c] = sum dv,
+//   dbcast[b][c] = sum_q dy.  One block per channel, fixed-order reductions.
+// ================================================================================================
+__device__ __forceinline__ float act_grad(int act, float a) {
+    switch (act) {
+        case LDM_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+        case LDM_ACT_TANH: return 1.f - a * a;
+        case LDM_ACT_TANH_HALF: {   // a = (tanh(v)+1)/2 -> da/dv = (1 - tanh^2)/2
+            const float th = 2.f * a - 1.f;
+            return 0.5f * (1.f - th * th);
+        }
+        default: return 1.f;
+    }
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += red[w];
+    return s;
+}
+
+__global__ __launch_bounds__(256) void act_backward_kernel(const float* __restrict__ dy, const float* __restrict__ aval,
+                                                           const float* __restrict__ pre, int act, int B, int C, int HW,
+                                                           float* __restrict__ dv, float* __restrict__ dbias,
+                                                           float* __restrict__ dbcast) {
+    __shared__ float red[8];
+    const int c = blockIdx.x;
+    float sb = 0.f;
+    for (int b = 0; b < B; ++b) {
+        const size_t base = ((size_t)b * C + c) * HW;
+        float sbc = 0.f;
+        for (int q = threadIdx.x; q < HW; q += blockDim.x) {
+            const float g = dy[base + q];
+            float d;
+            if (act == LDM_ACT_GELU) {   // needs the pre-activation v
+                const float v = pre[base + q];
+                const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752440f));
+                const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
+                d = g * (cdf + v * pdf);
+            } else {
+                d = g * act_grad(act, aval ? aval[base + q] : 0.f);
+            }
+            if (dv) dv[base + q] = d;
+            sb += d;
+            sbc += g;
+        }
+        if (dbcast) {
+            const float s = block_sum(sbc, red);
+            if (threadIdx.x == 0) dbcast[(size_t)b * C + c] = s;
+        }
+    }
+    if (dbias) {
+        const float s = block_sum(sb, red);
+        if (threadIdx.x == 0) dbias[c] = s;
+    }
+}
+
+// ================================================================================================
+// train-mode BatchNorm2d backward (+ activation): y = act(xhat*w + b), xhat = (x - mean)*invstd
+//   g = dy * act'(y);  dw = sum g*xhat;  db = sum g;  dx = w*invstd*(g - db/N - xhat*dw/N)
+// ================================================================================================
+__global__ __launch_bounds__(256) void bn_backward_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                          const float* __restrict__ x, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, const float* __restrict__ w,
+                                                          int act, int B, int C, int HW, float* __restrict__ dx,
+                                                          float* __restrict__ dw, float* __restrict__ db) {
+    __shared__ float red[8];
+    const int c = blockIdx.x;
+    const float mu = mean[c], is = invstd[c];
+    float sg = 0.f, sgx = 0.f;
+    for (int b = 0; b < B; ++b) {
+        const size_t base = ((size_t)b * C + c) * HW;
+        for (int q = threadIdx.x; q < HW; q += blockDim.x) {
+            const float g = dy[base + q] * act_grad(act, y[base + q]);
+            const float xh = (x[base + q] - mu) * is;
+            sg += g;
+            sgx += g * xh;
+        }
+    }
+    sg = block_sum(sg, red);
+    sgx = block_sum(sgx, red);
+    const float N = (float)B * (float)HW;
+    const float k = (w ? w[c] : 1.f) * is;
+    if (dx) {
+        for (int b = 0; b < B; ++b) {
+            const size_t base = ((size_t)b * C + c) * HW;
+            for (int q = threadIdx.x; q < HW; q += blockDim.x) {
+                const float g = dy[base + q] * act_grad(act, y[base + q]);
+                const float xh = (x[base + q] - mu) * is;
+                dx[base + q] = k * ((g - sg / N) - xh * (sgx / N));
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (dw) dw[c] = sgx;
+        if (db) db[c] = sg;
+    }
+}
+
+// ================================================================================================
+// cross-attention backward, one block per (b, head); recomputes P from q, k:
+//   dV = dO P ; dP = dO^T V ; dS = P*(dP - rowsum(dP*P)) ; dq = scale*(K dS^T) ; dK = qs dS
+// q [B,E,L], kv [B,2E,S] (K then V), dout [B,E,L] -> dq [B,E,L], dkv [B,2E,S].
+// LDS: X1 [d][L], X2 [d][S] (Q,K then dO,V then Q,K again), P [L][S], dP [L][S].
+// ================================================================================================
+__global__ __launch_bounds__(256) void attention_backward_kernel(const float* __restrict__ q,
+                                                                 const float* __restrict__ kv,
+                                                                 const float* __restrict__ dout, float* __restrict__ dq,
+                                                                 float* __restrict__ dkv, int E, int heads, int L, int S,
+                                                                 float scale) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int d = E / heads;
+    const int h = blockIdx.x % heads, b = blockIdx.x / heads;
+    float* X1 = sm;              // [d][L]
+    float* X2 = X1 + d * L;      // [d][S]
+    float* P = X2 + d * S;       // [L][S]
+    float* dP = P + L * S;       // [L][S]
+    const size_t qo = ((size_t)b * E + (size_t)h * d) * L;
+    const size_t ko = ((size_t)b * 2 * E + (size_t)h * d) * S;
+    const size_t vo = ((size_t)b * 2 * E + E + (size_t)h * d) * S;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+    // phase 1: P = softmax((q*scale)^T k)
+    for (int e = tid; e < d * L; e += nt) X1[e] = q[qo + e] * scale;
+    for (int e = tid; e < d * S; e += nt) X2[e] = kv[ko + e];
+    __syncthreads();
+    for (int e = tid; e < L * S; e += nt) {
+        const int l = e / S, s = e - l * S;
+        float acc = 0.f;
+        for (int c = 0; c < d; ++c) acc = fmaf(X1[c * L + l], X2[c * S + s], acc);
+        P[e] = acc;
+    }
+    __syncthreads();
+    for (int l = wave; l < L; l += nw) {
+        float* row = P + l * S;
+        float mx = -INFINITY;
+        for (int s = lane; s < S; s += 64) mx = fmaxf(mx, row[s]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        float sum = 0.f;
+        for (int s = lane; s < S; s += 64) {
+            const float ex = expf(row[s] - mx);
+            row[s] = ex;
+            sum += ex;
+        }
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        for (int s = lane; s < S; s += 64) row[s] = row[s] / sum;
+    }
+    __syncthreads();
+    // phase 2: X1 <- dO [d][L], X2 <- V [d][S]; dV = dO P -> global; dP = dO^T V -> LDS
+    for (int e = tid; e < d * L; e += nt) X1[e] = dout[qo + e];
+    for (int e = tid; e < d * S; e += nt) X2[e] = kv[vo + e];
+    __syncthreads();
+    for (int e = tid; e < d * S; e += nt) {
+        const int c = e / S, s = e - c * S;
+        float acc = 0.f;
+        for (int l = 0; l < L; ++l) acc = fmaf(X1[c * L + l], P[l * S + s], acc);
+        dkv[vo + e] = acc;
+    }
+    for (int e = tid; e < L * S; e += nt) {
+        const int l = e / S, s = e - l * S;
+        float acc = 0.f;
+        for (int c = 0; c < d; ++c) acc = fmaf(X1[c * L + l], X2[c * S + s], acc);
+        dP[e] = acc;
+    }
+    __syncthreads();
+    // phase 3: dS = P * (dP - rowsum(dP * P))  (in place in dP)
+    for (int l = wave; l < L; l += nw) {
+        float s0 = 0.f;
+        for (int s = lane; s < S; s += 64) s0 += dP[l * S + s] * P[l * S + s];
+        for (int o = 32; o > 0; o >>= 1) s0 += __shfl_xor(s0, o);
+        for (int s = lane; s < S; s += 64) dP[l * S + s] = P[l * S + s] * (dP[l * S + s] - s0);
+    }
+    __syncthreads();
+    // phase 4: X1 <- qs, X2 <- K; dq = scale * K dS^T ; dK = qs dS
+    for (int e = tid; e < d * L; e += nt) X1[e] = q[qo + e] * scale;
+    for (int e = tid; e < d * S; e += nt) X2[e] = kv[ko + e];
+    __syncthreads();
+    for (int e = tid; e < d * L; e += nt) {
+        const int c = e / L, l = e - c * L;
+        float acc = 0.f;
+        for (int s = 0; s < S; ++s) acc = fmaf(dP[l * S + s], X2[c * S + s], acc);
+        dq[qo + e] = acc * scale;
+    }
+    for (int e = tid; e < d * S; e += nt) {
+        const int c = e / S, s = e - c * S;
+        float acc = 0.f;
+        for (int l = 0; l < L; ++l) acc = fmaf(dP[l * S + s], X1[c * L + l], acc);
+        dkv[ko + e] = acc;
+    }
+}
+
+// ================================================================================================
+// multi-tensor Adam (torch.optim.Adam, train.py:156) with GradScaler unscale / inf check / skip
+// ================================================================================================
+__global__ __launch_bounds__(256) void unscale_check_kernel(const ldm_tensor_slot* __restrict__ slots,
+                                                            const int32_t* __restrict__ chunk_tensor,
+                                                            const int64_t* __restrict__ chunk_start, int chunk_len,
+                                                            const float* __restrict__ inv_scale,
+                                                            int32_t* __restrict__ found_inf) {
+    const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
+    const int64_t s0 = chunk_start[blockIdx.x];
+    const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
+    const float is = inv_scale ? inv_scale[0] : 1.f;
+    bool bad = false;
+    for (int64_t i = s0 + threadIdx.x; i < e0; i += blockDim.x) {
+        const float g = sl.grad[i] * is;
+        sl.grad[i] = g;
+        bad |= !isfinite(g);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found_inf, 1);   // a flag, not a sum: order-free
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(const ldm_tensor_slot* __restrict__ slots,
+                                                   const int32_t* __restrict__ chunk_tensor,
+                                                   const int64_t* __restrict__ chunk_start, int chunk_len,
+                                                   float one_m_beta1, float beta2, float one_m_beta2, float eps,
+                                                   float weight_decay, float decay_mul, float step_size,
+                                                   float bias_correction2_sqrt, const int32_t* __restrict__ found_inf) {
+    if (found_inf && found_inf[0]) return;   // GradScaler.step skips the update on inf/nan
+    const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
+    const int64_t s0 = chunk_start[blockIdx.x];
+    const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
+    // scalars arrive as torch's: host doubles cast once to fp32 (1-beta computed in double)
+    for (int64_t i = s0 + threadIdx.x; i < e0; i += blockDim.x) {
+        float g = sl.grad[i];
+        float p = sl.param[i];
+        if (decay_mul != 1.f) p = p * decay_mul;          // AdamW: param.mul_(1 - lr * weight_decay)
+        else if (weight_decay != 0.f) g = g + weight_decay * p;   // Adam: grad.add(param, alpha=wd)
+        float m = sl.exp_avg[i], v = sl.exp_avg_sq[i];
+        m = m + one_m_beta1 * (g - m);                // exp_avg.lerp_(grad, 1 - beta1)
+        v = v * beta2;                                // exp_avg_sq.mul_(beta2)
+        v = v + (one_m_beta2 * g) * g;                //   .addcmul_(grad, grad, value=1 - beta2)
+        const float denom = sqrtf(v) / bias_correction2_sqrt + eps;
+        p = p + (-step_size) * (m / denom);           // param.addcdiv_(exp_avg, denom, value=-step_size)
+        sl.exp_avg[i] = m;
+        sl.exp_avg_sq[i] = v;
+        sl.param[i] = p;
+    }
+}
+
+// torch.amp.GradScaler._amp_update_scale_: backoff on inf, grow after growth_interval clean steps
+__global__ void update_scale_kernel(float* scale, int32_t* growth_tracker, const int32_t* found_inf,
+                                    float growth_factor, float backoff_factor, int growth_interval) {
+    if (found_inf[0]) {
+        scale[0] = scale[0] * backoff_factor;
+        growth_tracker[0] = 0;
+    } else {
+        const int successful = growth_tracker[0] + 1;
+        if (successful == growth_interval) {
+            scale[0] = scale[0] * growth_factor;
+            growth_tracker[0] = 0;
+        } else {
+            growth_tracker[0] = successful;
+        }
+    }
+}
+
+}  // namespace ldm
+
+using namespace ldm;
+
+// ---- weight gradient ------------------------------------------------------------------------------
+static int wgrad_setup(const ldm_conv_desc& d, WgradArgs& a, int& kk_count) {
+    a = WgradArgs{};
+    LDM_REQUIRE(d.kh > 0 && d.kw > 0 && d.B > 0, "wgrad: bad descriptor");
+    a.B = d.B;
+    a.T = d.kh * d.kw;
+    kk_count = a.T;
+    if (!d.transposed) {
+        a.M = d.Cout;
+        a.C = d.Cin;
+        a.Hq = d.Hout;
+        a.Wq = d.Wout;
+        a.Hg = d.Hin;
+        a.Wg = d.Win;
+    } else {
+        a.M = d.Cin;
+        a.C = d.Cout;
+        a.Hq = d.Hin;
+        a.Wq = d.Win;
+        a.Hg = d.Hout;
+        a.Wg = d.Wout;
+    }
+    a.s = d.stride;
+    a.N = a.C * a.T;
+    a.kw = d.kw;
+    a.pad = d.pad;
+    a.fd_kw = FastDiv::make(d.kw);
+    a.cpb = (a.Hq * a.Wq + 15) / 16;
+    a.nchunk = a.B * a.cpb;
+    a.fd_cpb = FastDiv::make(a.cpb);
+    a.fd_wq = FastDiv::make(a.Wq);
+    a.fd_t = FastDiv::make(a.T);
+    return 0;
+}
+
+static int wgrad_splits(const WgradArgs& a) {
+    const int tiles = ((a.M + 15) / 16) * ((a.N + 15) / 16);
+    int S = 1;
+    while (S < 256 && tiles * S < 2048 && a.nchunk / (S * 2) >= 4) S *= 2;
+    return S;
+}
+
+extern "C" int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d) {
+    if (!d) return -1;
+    WgradArgs a;
+    int kk;
+    if (wgrad_setup(*d, a, kk)) return -1;
+    const int S = wgrad_splits(a);
+    return (int64_t)S * a.M * a.N;
+}
+
+extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                        int32_t accumulate, float* workspace, void* stream) {
+    LDM_REQUIRE(d && x && dy && dw && workspace, "wgrad: null argument");
+    WgradArgs a;
+    int kk;
+    int rc = wgrad_setup(*d, a, kk);
+    if (rc) return rc;
+    a.dense = d->transposed ? x : dy;
+    a.gath = d->transposed ? dy : x;
+    const int S = wgrad_splits(a);
+    a.per_split = (a.nchunk + S - 1) / S;
+    a.partial = workspace;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((a.N + 15) / 16, (a.M + 15) / 16, S);
+    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(64), 0, st, a);
+    LDM_CHECK_LAUNCH("wgrad_kernel");
+    const int MN = a.M * a.N;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)a.partial, S, MN,
+                       dw, accumulate);
+    LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
+    return 0;
+}
+
+extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
+                                int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, void* stream) {
+    LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
+    LDM_REQUIRE(act != LDM_ACT_GELU || pre_act, "act_backward: GELU needs the pre-activation");
+    LDM_REQUIRE(act == LDM_ACT_NONE || act == LDM_ACT_GELU || act_out, "act_backward: needs the activation output");
+    hipLaunchKernelGGL(act_backward_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, act_out, pre_act, act, B, C,
+                       HW, dv, dbias, dbcast);
+    LDM_CHECK_LAUNCH("act_backward_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
+                                      const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
+                                      int32_t HW, float* dx, float* dweight, float* dbias, void* stream) {
+    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
+    hipLaunchKernelGGL(bn_backward_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y, x, save_mean, save_invstd,
+                       weight, act, B, C, HW, dx, dweight, dbias);
+    LDM_CHECK_LAUNCH("bn_backward_kernel");
+    return 0;
+}
+
+extern "C" int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv,
+                                      int32_t B, int32_t E, int32_t heads, int32_t L, int32_t S, float scale,
+                                      void* stream) {
+    LDM_REQUIRE(q && kv && dout && dq && dkv && B > 0 && heads > 0 && E % heads == 0, "attention_backward: bad argument");
+    const int d = E / heads;
+    const size_t lds = ((size_t)d * L + (size_t)d * S + 2 * (size_t)L * S) * sizeof(float);
+    LDM_REQUIRE(lds <= 64 * 1024, "attention_backward: head tile exceeds LDS budget");
+    hipLaunchKernelGGL(attention_backward_kernel, dim3(B * heads), dim3(256), lds, (hipStream_t)stream, q, kv, dout, dq,
+                       dkv, E, heads, L, S, scale);
+    LDM_CHECK_LAUNCH("attention_backward_kernel");
+    return 0;
+}
+
+extern "C" int ldm_unscale_check(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                                 int32_t nchunks, int32_t chunk_len, const float* inv_scale, int32_t* found_inf,
+                                 void* stream) {
+    LDM_REQUIRE(slots && chunk_tensor && chunk_start && found_inf && nchunks >= 0, "unscale_check: bad argument");
+    if (nchunks == 0) return 0;
+    hipLaunchKernelGGL(unscale_check_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, slots, chunk_tensor,
+                       chunk_start, chunk_len, inv_scale, found_inf);
+    LDM_CHECK_LAUNCH("unscale_check_kernel");
+    return 0;
+}
+
+extern "C" int ldm_adam_step(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                             int32_t nchunks, int32_t chunk_len, double lr, double beta1, double beta2, double eps,
+                             double weight_decay, int32_t decoupled, int32_t step, const int32_t* found_inf,
+                             void* stream) {
+    LDM_REQUIRE(slots && chunk_tensor && chunk_start && nchunks >= 0 && step >= 1, "adam_step: bad argument");
+    if (nchunks == 0) return 0;
+    // torch/optim/adam.py (_single_tensor_adam / _multi_tensor_adam, non-capturable): python floats
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    const double step_size = lr / bc1;
+    hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, slots, chunk_tensor, chunk_start,
+                       chunk_len, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                       (float)weight_decay, decoupled ? (float)(1.0 - lr * weight_decay) : 1.f, (float)step_size,
+                       (float)std::sqrt(bc2), found_inf);
+    LDM_CHECK_LAUNCH("adam_kernel");
+    return 0;
+}
+
+extern "C" int ldm_update_scale(float* scale, int32_t* growth_tracker, const int32_t* found_inf, float growth_factor,
+                                float backoff_factor, int32_t growth_interval, void* stream) {
+    LDM_REQUIRE(scale && growth_tracker && found_inf, "update_scale: bad argument");
+    hipLaunchKernelGGL(update_scale_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, scale, growth_tracker, found_inf,
+                       growth_factor, backoff_factor, growth_interval);
+    LDM_CHECK_LAUNCH("update_scale_kernel");
+    return 0;
+}

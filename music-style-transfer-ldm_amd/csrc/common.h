@@ -88,6 +88,7 @@ struct EpiArgs {
     int32_t act;
     const float* bcast;
     const float* skip;
+    float* act_out;   // post-activation value before the adds (training), or NULL
     // fused DDIM reverse update (model.py:442-458) on the conv output eps = noise_pred:
     // x <- sqrt(ab_n)*x0 + sqrt(1-ab_n)*eps + eta*(...) in place, with pred_x0 / noise_pred logs.
     const float* ddim_coef;   // [4] {sqrt(ab_t), sqrt(1-ab_t), sqrt(ab_n), sqrt(1-ab_n)} or NULL

@@ -76,10 +76,30 @@ int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
         pt.ntap[0] = n;
         return 0;
     }
-    // transposed: stride 2 with Hout == 2*Hin (k3 p1 op1, k4 p1 op0) -> 4 parity phases
     const int ho = (d.Hin - 1) * d.stride - 2 * d.pad + d.kh + d.out_pad;
     const int wo = (d.Win - 1) * d.stride - 2 * d.pad + d.kw + d.out_pad;
     LDM_REQUIRE(d.Hout == ho && d.Wout == wo, "conv_transpose: output size mismatch");
+    if (d.stride == 1) {
+        // stride-1 transposed conv (= the data gradient of a stride-1 conv): one phase,
+        // out[o] += x[o + pad - k] * w[k]  ->  dy = pad - kh
+        LDM_REQUIRE(d.kh * d.kw <= kMaxTap, "conv_transpose: kernel larger than 3x3 unsupported at stride 1");
+        pt.nphase = 1;
+        pt.Hq = d.Hout;
+        pt.Wq = d.Wout;
+        pt.sy = 1;
+        pt.osy = 1;
+        int n = 0;
+        for (int a = 0; a < d.kh; ++a)
+            for (int b = 0; b < d.kw; ++b) {
+                pt.dy[0][n] = (int32_t)(d.pad - a);
+                pt.dx[0][n] = (int32_t)(d.pad - b);
+                pt.kk[0][n] = (int32_t)(a * d.kw + b);
+                ++n;
+            }
+        pt.ntap[0] = n;
+        return 0;
+    }
+    // transposed: stride 2 with Hout == 2*Hin (k3 p1 op1, k4 p1 op0) -> 4 parity phases
     LDM_REQUIRE(d.stride == 2 && d.Hout == 2 * d.Hin && d.Wout == 2 * d.Win,
                 "conv_transpose: only stride 2 with Hout == 2*Hin is supported");
     pt.nphase = 4;
@@ -166,6 +186,7 @@ __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx
         v = v * alpha + beta;
     }
     v = apply_act(v, e.act);
+    if (e.act_out) e.act_out[oidx] = v;
     if (e.bcast) v = v + p.bcast;
     if (e.skip) v = v + p.skip;
     if (e.ddim_coef) {
@@ -655,6 +676,7 @@ extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* pla
         e.act = ep->act;
         e.bcast = ep->bcast_add;
         e.skip = ep->skip_add;
+        e.act_out = ep->act_out;
     }
     return conv_forward_ex(*d, *plan, x, w, e, y, (hipStream_t)stream);
 }

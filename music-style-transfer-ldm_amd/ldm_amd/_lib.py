@@ -32,7 +32,7 @@ class ConvDesc(ctypes.Structure):
 
 class Epilogue(ctypes.Structure):
     _fields_ = [("bias", c_fp), ("bn_weight", c_fp), ("bn_bias", c_fp), ("bn_mean", c_fp), ("bn_var", c_fp),
-                ("bn_eps", c_float), ("act", c_int32), ("bcast_add", c_fp), ("skip_add", c_fp)]
+                ("bn_eps", c_float), ("act", c_int32), ("bcast_add", c_fp), ("skip_add", c_fp), ("act_out", c_fp)]
 
 
 class ConvPlan(ctypes.Structure):
@@ -89,7 +89,22 @@ SIGNATURES = {
                                    c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_ddim_sample": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_fp, c_fp, c_vp,
                                   c_fp, c_int32, c_float, c_fp, c_fp, c_fp, c_vp]),
+    # backward / optimiser
+    "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
+    "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
+    "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
+                                         c_fp, c_fp, c_fp, c_vp]),
+    "ldm_attention_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                         c_float, c_vp]),
+    "ldm_unscale_check": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, c_fp, c_vp, c_vp]),
+    "ldm_adam_step": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int32, c_int32, c_vp, c_vp]),
+    "ldm_update_scale": (c_int32, [c_fp, c_vp, c_vp, c_float, c_float, c_int32, c_vp]),
 }
+
+# ldm_tensor_slot: 4 device pointers + int64 numel, packed into an int64 tensor on the device
+TENSOR_SLOT_WORDS = 5
 
 _LIB = None
 

@@ -30,7 +30,7 @@ class _HipOp(torch.autograd.Function):
     @staticmethod
     def forward(ctx, name, fwd, nin, *args):
         tensors = args[:nin]
-        store = {}
+        store = {"grad": True}
         out = fwd(store, *tensors)
         ctx.name = name
         ctx.store = store
@@ -52,10 +52,19 @@ def hip_apply(name, fwd, *tensors):
     """Run fwd(store, *tensors) on the HIP path; build an autograd node only if needed."""
     if _needs_grad(*tensors):
         return _HipOp.apply(name, fwd, len(tensors), *tensors)
-    return fwd({}, *tensors)
+    return fwd({"grad": False}, *tensors)
 
 
 # ------------------------------------------------------------------------------------------------
+def _conv_desc(x, w, cfg):
+    if cfg["transposed"]:
+        cout, kh, kw = w.shape[1], w.shape[2], w.shape[3]
+    else:
+        cout, kh, kw = w.shape[0], w.shape[2], w.shape[3]
+    return ops.make_desc(x.shape[0], x.shape[1], x.shape[2], x.shape[3], cout, kh, kw, cfg["stride"],
+                         cfg["padding"], cfg["output_padding"], cfg["transposed"])
+
+
 def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0, act="none", bcast=None,
          skip=None, bn_eval=None, wkey=None):
     """act(BN_eval(conv(x,w)+b)) + bcast + skip, differentiable in x, weight, bias, bcast, skip.
@@ -64,14 +73,47 @@ def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0
     cfg = dict(stride=stride, padding=padding, transposed=transposed, output_padding=output_padding, act=act)
 
     def fwd(store, x_, w_, b_, bc_, sk_):
-        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, **cfg)
+        aout = None
+        if store["grad"] and act != "none" and (bc_ is not None or sk_ is not None):
+            d = _conv_desc(x_, w_, cfg)
+            aout = torch.empty((d.B, d.Cout, d.Hout, d.Wout), device=x_.device, dtype=torch.float32)
+        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, **cfg)
         store["cfg"] = cfg
         store["bn"] = bn_eval
-        store["saved"] = (x_, w_, y)
-        store["has"] = (b_ is not None, bc_ is not None, sk_ is not None)
+        store["wkey"] = wkey
+        store["saved"] = (x_, w_, y if aout is None else aout)
+        store["bc_shape"] = None if bc_ is None else bc_.shape
         return y
 
     return hip_apply("conv", fwd, x, weight, bias, bcast, skip)
+
+
+@register_backward("conv")
+def _conv_backward(ctx, gy):
+    """conv/convT backward: epilogue (act, bias, bcast, skip, eval-BN scale) -> dgrad on the dual
+    descriptor -> wgrad (fixed-order split-K)."""
+    x, w, a = ctx.saved_tensors
+    cfg, bn = ctx.store["cfg"], ctx.store["bn"]
+    nx, nw, nb, nbc, nsk = ctx.needs_input_grad[3:8]
+    act = cfg["act"]
+    if act == "gelu":
+        raise NotImplementedError("conv backward with a fused GELU epilogue (apply GELU as its own op)")
+    gy = ops.f32c(gy)
+    need_v = nx or nw or nb
+    gv, gb, gbc = ops.act_backward(gy, act, act_out=a, need_dv=need_v, need_bias=nb and bn is None,
+                                   need_bcast=nbc)
+    if bn is not None and need_v:
+        g_, _b, _m, var, eps = bn
+        zero = torch.zeros_like(var)
+        gv = ops.batchnorm_eval(gv, g_, zero, zero, var, eps, "none")     # gv * gamma * invstd
+        if nb:
+            _, gb, _ = ops.act_backward(gv, "none", need_dv=False, need_bias=True)
+    desc = _conv_desc(x, w, cfg)
+    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"]) if nx else None
+    gw = ops.conv_backward_weight(x, gv, desc) if nw else None
+    if gbc is not None:
+        gbc = gbc.reshape(ctx.store["bc_shape"])
+    return gx, gw, gb, gbc, (gy if nsk else None)
 
 
 def linear(x, weight, bias, act="none"):
@@ -93,6 +135,22 @@ def activation(x, act):
         return y
 
     return hip_apply("activation", fwd, x)
+
+
+def _as_nc(t):
+    """[N, C, ...] view for the per-channel kernels (a 1-D tensor is one channel)."""
+    if t.dim() >= 2:
+        return t.reshape(t.shape[0], t.shape[1], -1)
+    return t.reshape(1, 1, -1)
+
+
+@register_backward("activation")
+def _activation_backward(ctx, gy):
+    x, y = ctx.saved_tensors
+    act = ctx.store["act"]
+    dv, _, _ = ops.act_backward(_as_nc(ops.f32c(gy)), act, act_out=_as_nc(y),
+                                pre_act=_as_nc(ops.f32c(x)) if act == "gelu" else None)
+    return (dv.reshape(x.shape),)
 
 
 def batchnorm(x, bn_module, act="none"):
@@ -124,6 +182,15 @@ def batchnorm(x, bn_module, act="none"):
         return y
 
     return hip_apply("batchnorm_train", fwd_train, x, m.weight, m.bias)
+
+
+@register_backward("batchnorm_train")
+def _bn_train_backward(ctx, gy):
+    x, w, b, sm, si, y = ctx.saved_tensors
+    nx, nw, nb = ctx.needs_input_grad[3:6]
+    dx, dw, db = ops.batchnorm_backward(gy, y, x, sm, si, w, ctx.store["act"], need_dx=nx,
+                                        need_w=nw and w is not None, need_b=nb and b is not None)
+    return dx, dw, db
 
 
 def time_mlp(t, w1, b1, w2, b2):
@@ -193,8 +260,15 @@ def _kl_backward(ctx, g):
 def attention_core(q, kv, heads):
     def fwd(store, q_, kv_):
         out = ops.attention_core(q_, kv_, heads)
-        store["saved"] = (q_, kv_, out)
+        store["saved"] = (q_, kv_)
         store["heads"] = heads
         return out
 
     return hip_apply("attention_core", fwd, q, kv)
+
+
+@register_backward("attention_core")
+def _attention_backward(ctx, gout):
+    q, kv = ctx.saved_tensors
+    dq, dkv = ops.attention_backward(q, kv, gout, ctx.store["heads"])
+    return dq, dkv

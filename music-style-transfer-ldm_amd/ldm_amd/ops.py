@@ -136,8 +136,9 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
 # convolution with fused epilogue
 # ------------------------------------------------------------------------------------------------
 def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False, output_padding=0, bn=None,
-                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None):
-    """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps)."""
+                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None, act_out=None):
+    """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps).
+    act_out (preallocated, output-shaped) also receives act(.) before the adds."""
     require_device(x, weight, bias, bcast, skip)
     x = f32c(x)
     B, Cin, H, W = x.shape
@@ -170,9 +171,104 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
         skip = f32c(skip)
         keep.append(skip)
         ep.skip_add = skip.data_ptr()
+    if act_out is not None:
+        require_device(act_out)
+        assert act_out.is_contiguous() and act_out.shape == y.shape
+        ep.act_out = act_out.data_ptr()
     L.call("ldm_conv_forward", byref(desc), byref(plan), x.data_ptr(), _p(wbuf), byref(ep), y.data_ptr(),
            stream_handle())
     return y
+
+
+def dual_desc(desc):
+    """Descriptor whose forward is the data gradient of `desc`: conv <-> transposed conv with the same
+    kernel, stride and padding (the torch weight tensor is reused unchanged in both directions)."""
+    d = L.ConvDesc(desc.B, desc.Cout, desc.Hout, desc.Wout, desc.Cin, desc.Hin, desc.Win, desc.kh, desc.kw,
+                   desc.stride, desc.pad, 0, 1 - desc.transposed)
+    if d.transposed:
+        d.out_pad = desc.Hin - ((desc.Hout - 1) * desc.stride - 2 * desc.pad + desc.kh)
+        if d.out_pad != desc.Win - ((desc.Wout - 1) * desc.stride - 2 * desc.pad + desc.kw) or \
+                not 0 <= d.out_pad < max(1, desc.stride):
+            raise RuntimeError("conv backward: input size not reachable by a transposed conv (ragged stride)")
+    return d
+
+
+def conv_backward_data(dy, weight, desc, wkey=None):
+    """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc)."""
+    dd = dual_desc(desc)
+    plan = get_plan(dd)
+    wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
+    dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
+    L.call("ldm_conv_forward", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), None, dx.data_ptr(), stream_handle())
+    return dx
+
+
+_WS = {}
+
+
+def scratch(name, nfloats, device):
+    """Per-device scratch buffer reused across calls on the current stream (grown on demand)."""
+    key = (name, str(device))
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nfloats:
+        buf = torch.empty(max(int(nfloats), 1), device=device, dtype=torch.float32)
+        _WS[key] = buf
+    return buf
+
+
+def conv_backward_weight(x, dy, desc, dw=None, accumulate=False):
+    """dW (torch layout) of conv/convT `desc` from its input x and pre-epilogue gradient dy."""
+    x = f32c(x)
+    dy = f32c(dy)
+    if desc.transposed:
+        shape = (desc.Cin, desc.Cout, desc.kh, desc.kw)
+    else:
+        shape = (desc.Cout, desc.Cin, desc.kh, desc.kw)
+    if dw is None:
+        dw = torch.empty(shape, device=x.device, dtype=torch.float32)
+    ws = scratch("wgrad", L.load().ldm_conv_wgrad_workspace_floats(byref(desc)), x.device)
+    L.call("ldm_conv_backward_weight", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate),
+           ws.data_ptr(), stream_handle())
+    return dw
+
+
+def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=False, need_bcast=False):
+    """(dv, dbias, dbcast) of y = act(v) (+bcast[b,c]) (+skip) for NCHW dy."""
+    dy = f32c(dy)
+    B, C = dy.shape[0], dy.shape[1]
+    HW = dy.numel() // max(1, B * C)
+    dv = (dy if act == "none" else torch.empty_like(dy)) if need_dv else None
+    db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_bias else None
+    dbc = torch.empty((B, C), device=dy.device, dtype=torch.float32) if need_bcast else None
+    if act == "none" and not need_bias and not need_bcast:
+        return dv, None, None
+    L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(pre_act), L.ACT[act], B, C, HW,
+           _p(dv) if act != "none" else None, _p(db), _p(dbc), stream_handle())
+    return dv, db, dbc
+
+
+def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True):
+    dy = f32c(dy)
+    B, C = dy.shape[0], dy.shape[1]
+    HW = dy.numel() // max(1, B * C)
+    dx = torch.empty_like(dy) if need_dx else None
+    dw = torch.empty(C, device=dy.device, dtype=torch.float32) if need_w else None
+    db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_b else None
+    L.call("ldm_batchnorm_backward", dy.data_ptr(), y.data_ptr(), f32c(x).data_ptr(), save_mean.data_ptr(),
+           save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db), stream_handle())
+    return dx, dw, db
+
+
+def attention_backward(q, kv, dout, heads):
+    q, kv, dout = f32c(q), f32c(kv), f32c(dout)
+    B, E, Lq = q.shape
+    S = kv.shape[2]
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    scale = float(math.sqrt(1.0 / float(E // heads)))
+    L.call("ldm_attention_backward", q.data_ptr(), kv.data_ptr(), dout.data_ptr(), dq.data_ptr(), dkv.data_ptr(), B, E,
+           heads, Lq, S, scale, stream_handle())
+    return dq, dkv
 
 
 def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False):

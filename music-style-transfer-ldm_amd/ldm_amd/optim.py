@@ -1,0 +1,225 @@
+"""Optimiser step of the train path on the HIP kernels.
+
+``Adam`` / ``AdamW`` are torch.optim.Optimizer subclasses (same param_groups, state keys 'step',
+'exp_avg', 'exp_avg_sq', state_dict format, so ReduceLROnPlateau and checkpoints work unchanged) whose
+step() is ONE multi-tensor launch per param group (ldm_adam_step).  ``GradScaler`` mirrors
+torch.amp.GradScaler's API and semantics (scale / unscale_ / step / update, backoff and growth) with
+the unscale + inf check and the scale update as device kernels (ldm_unscale_check, ldm_update_scale).
+
+Reference call sites: torch.optim.Adam + torch.amp.GradScaler in LDMTrainer (train.py:156-157,
+:189-201); torch.optim.AdamW in train_autoencoder (train.py:44).
+"""
+import torch
+
+from . import _lib as L
+from .ops import require_device, stream_handle
+
+CHUNK = 1 << 16   # elements per workgroup-chunk of the multi-tensor kernels
+
+
+class _SlotTable:
+    """Device table of ldm_tensor_slot {param, grad, exp_avg, exp_avg_sq, numel} + chunk map."""
+
+    def __init__(self, params, grads, m, v):
+        dev = params[0].device
+        rows, ct, cs = [], [], []
+        for i, (p, g, a, b) in enumerate(zip(params, grads, m, v)):
+            n = p.numel()
+            rows.append([p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(),
+                         0 if b is None else b.data_ptr(), n])
+            for s in range(0, n, CHUNK):
+                ct.append(i)
+                cs.append(s)
+        self.slots = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=False)
+        self.chunk_tensor = torch.tensor(ct, dtype=torch.int32).to(dev)
+        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(dev)
+        self.nchunks = len(ct)
+        self.key = tuple(r[0] for r in rows) + tuple(r[1] for r in rows)
+
+
+def scale_tensors_(tensors, factor):
+    """t *= factor for every (contiguous fp32 device) tensor, one multi-tensor launch; returns a device
+    int32 [1] flag, nonzero if any result is non-finite."""
+    tensors = [t for t in tensors if t.numel()]
+    if not tensors:
+        return False
+    require_device(*tensors, what="scale_tensors_")
+    tab = _SlotTable(tensors, tensors, [None] * len(tensors), [None] * len(tensors))
+    f = torch.full((1,), float(factor), dtype=torch.float32, device=tensors[0].device)
+    bad = torch.zeros((1,), dtype=torch.int32, device=tensors[0].device)
+    L.call("ldm_unscale_check", tab.slots.data_ptr(), tab.chunk_tensor.data_ptr(), tab.chunk_start.data_ptr(),
+           tab.nchunks, CHUNK, f.data_ptr(), bad.data_ptr(), stream_handle())
+    return bad
+
+
+def _check_params(params):
+    for p in params:
+        require_device(p, what="ldm_amd.optim")
+        if not p.is_contiguous() or (p.grad is not None and not p.grad.is_contiguous()):
+            raise RuntimeError("ldm_amd.optim: parameters and gradients must be contiguous")
+        if p.grad is not None and p.grad.is_sparse:
+            raise RuntimeError("ldm_amd.optim: sparse gradients are not supported")
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, maximize=False, no capturable/differentiable) on one fused
+    multi-tensor kernel per param group."""
+
+    _decoupled = 0
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("ldm_amd.optim.Adam: amsgrad is not supported")
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
+        self._tables = {}
+
+    @torch.no_grad()
+    def step(self, closure=None, found_inf=None):
+        """One Adam update.  found_inf (device int32 [1], optional): skip on the device if set."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            _check_params(params)
+            # group the params by their step count (all equal unless params were added later)
+            by_step = {}
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                by_step.setdefault(int(st["step"].item()), []).append(p)
+            beta1, beta2 = group["betas"]
+            for step, ps in by_step.items():
+                grads = [p.grad for p in ps]
+                tab = _SlotTable(ps, grads, [self.state[p]["exp_avg"] for p in ps],
+                                 [self.state[p]["exp_avg_sq"] for p in ps])
+                L.call("ldm_adam_step", tab.slots.data_ptr(), tab.chunk_tensor.data_ptr(), tab.chunk_start.data_ptr(),
+                       tab.nchunks, CHUNK, float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+                       float(group["weight_decay"]), self._decoupled, step,
+                       None if found_inf is None else found_inf.data_ptr(), stream_handle())
+                # the tables are read by the kernel asynchronously: keep them alive until it ran
+                self._tables[(gi, step)] = tab
+        return loss
+
+
+class AdamW(Adam):
+    """torch.optim.AdamW (decoupled weight decay, default 1e-2)."""
+
+    _decoupled = 1
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad)
+
+
+class GradScaler:
+    """torch.amp.GradScaler('cuda') semantics: scale(loss) multiplies by the current scale, step()
+    unscales the grads (device kernel), skips the optimiser step when any grad is inf/nan, update()
+    backs the scale off (x0.5) on inf or grows it (x2) after growth_interval clean steps."""
+
+    def __init__(self, device="cuda", init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5,
+                 growth_interval=2000, enabled=True):
+        self._device = device
+        self._init_scale = init_scale
+        self._growth_factor = growth_factor
+        self._backoff_factor = backoff_factor
+        self._growth_interval = growth_interval
+        self._enabled = enabled
+        self._scale = None
+        self._tracker = None
+        self._found_inf = None
+        self._unscaled = set()
+        self._divisor = 1.0
+
+    def is_enabled(self):
+        return self._enabled
+
+    def set_grad_divisor(self, d):
+        """Extra factor 1/d folded into unscale_ (data-parallel gradient averaging: d = world size)."""
+        self._divisor = float(d)
+
+    def _lazy_init(self, dev):
+        if self._scale is None:
+            self._scale = torch.full((1,), self._init_scale, dtype=torch.float32, device=dev)
+            self._tracker = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self._found_inf = torch.zeros((1,), dtype=torch.int32, device=dev)
+
+    def get_scale(self):
+        return float(self._scale.item()) if self._scale is not None else self._init_scale
+
+    def scale(self, outputs):
+        if not self._enabled:
+            return outputs
+        self._lazy_init(outputs.device)
+        return outputs * self._scale.to(outputs.device)
+
+    def unscale_(self, optimizer):
+        if not self._enabled or id(optimizer) in self._unscaled:
+            return
+        self._lazy_init(next(p.device for g in optimizer.param_groups for p in g["params"]))
+        # GradScaler: scale.double().reciprocal().float()  (x 1/divisor for data-parallel averaging)
+        inv = torch.reciprocal(self._scale.double() * self._divisor).float()
+        self._found_inf.zero_()
+        for group in optimizer.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            _check_params(ps)
+            tab = _SlotTable(ps, [p.grad for p in ps], [None] * len(ps), [None] * len(ps))
+            L.call("ldm_unscale_check", tab.slots.data_ptr(), tab.chunk_tensor.data_ptr(), tab.chunk_start.data_ptr(),
+                   tab.nchunks, CHUNK, inv.data_ptr(), self._found_inf.data_ptr(), stream_handle())
+            group.setdefault("_ldm_tabs", []).append(tab)   # keep alive until the launch ran
+        self._unscaled.add(id(optimizer))
+
+    def step(self, optimizer, *args, **kwargs):
+        if not self._enabled:
+            return optimizer.step(*args, **kwargs)
+        self.unscale_(optimizer)
+        for group in optimizer.param_groups:
+            group.pop("_ldm_tabs", None)
+        # torch's GradScaler also syncs here (found_inf.item()) so that the optimiser's step counters
+        # only advance on applied steps
+        if int(self._found_inf.item()) == 0:
+            return optimizer.step(*args, **kwargs)
+        return None
+
+    def update(self, new_scale=None):
+        if not self._enabled:
+            return
+        if new_scale is not None:
+            self._scale.fill_(float(new_scale))
+        else:
+            L.call("ldm_update_scale", self._scale.data_ptr(), self._tracker.data_ptr(), self._found_inf.data_ptr(),
+                   float(self._growth_factor), float(self._backoff_factor), int(self._growth_interval),
+                   stream_handle())
+        self._unscaled.clear()
+
+    def state_dict(self):
+        if not self._enabled:
+            return {}
+        return {"scale": self.get_scale(), "growth_factor": self._growth_factor,
+                "backoff_factor": self._backoff_factor, "growth_interval": self._growth_interval,
+                "_growth_tracker": int(self._tracker.item()) if self._tracker is not None else 0}
+
+    def load_state_dict(self, sd):
+        if not sd:
+            return
+        self._init_scale = sd["scale"]
+        self._growth_factor = sd["growth_factor"]
+        self._backoff_factor = sd["backoff_factor"]
+        self._growth_interval = sd["growth_interval"]
+        if self._scale is not None:
+            self._scale.fill_(sd["scale"])
+            self._tracker.fill_(sd["_growth_tracker"])

@@ -231,7 +231,7 @@ class _TimeMLP(nn.Sequential):
         lin1, lin2 = self[1], self[3]
         if HF._needs_grad(lin1.weight, lin1.bias, lin2.weight, lin2.bias):
             emb = ops.sinusoid_embed(t, self[0].dim, lin1.weight.device)
-            h = HF.linear(emb, lin1.weight, lin1.bias, act="gelu")
+            h = HF.activation(HF.linear(emb, lin1.weight, lin1.bias), "gelu")
             return HF.linear(h, lin2.weight, lin2.bias)
         return ops.time_mlp(t, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
 

@@ -1,0 +1,247 @@
+"""Drop-in for the reference's models/train.py: LDMTrainer (train_step / train_epoch / train),
+train_autoencoder, train_ldm, main — same signatures, defaults, loss composition, optimiser and
+GradScaler semantics, with forward, backward and optimiser step on libldm_amd.
+
+Differences from the reference, all deliberate:
+  * The "GPU or raise" check runs when an entry point is used, not at import (train.py:21-26), so the
+    API can be imported and inspected on a host without a GPU.
+  * torch.optim.Adam / AdamW are ldm_amd.optim.Adam / AdamW (same update, one fused multi-tensor HIP
+    launch per group); torch.amp.GradScaler is ldm_amd.optim.GradScaler (same scale / skip / growth
+    rules).  Both are torch.optim-compatible (ReduceLROnPlateau and state_dicts work unchanged).
+  * The forward runs inside torch.autocast like the reference (train.py:176), but the HIP kernels
+    compute in fp32 regardless (>= the reference's fp16 autocast precision).
+  * Data-parallel: when torch.distributed is initialised with world_size > 1, each rank trains on its
+    own batch shard and the gradients are all-reduced (bucketed, overlapped with backward) before the
+    optimiser step (ldm_amd.dist.GradAllReduce).  Single-process behaviour is unchanged.
+  * The datasets (dataset.py) are not part of this package (torchvision-based image folders, out of
+    scope for the hot path); train_autoencoder / train_ldm accept ready loaders, else they import the
+    reference-style `dataset` module from sys.path.
+"""
+import argparse
+import os
+
+import torch
+
+try:
+    from .config import config
+    from . import _pathfix  # noqa: F401
+    from .model import LDM, SpectrogramDecoder, SpectrogramEncoder
+    from .loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
+except ImportError:   # reference-style flat imports (models/ on sys.path)
+    from config import config
+    import _pathfix  # noqa: F401
+    from model import LDM, SpectrogramDecoder, SpectrogramEncoder
+    from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
+
+from ldm_amd import dist as hdist
+from ldm_amd import optim as hoptim
+
+
+def _require_gpu():
+    device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    if device.type == "cuda":
+        print("Using GPU")
+    else:
+        raise RuntimeError("GPU not available, please check your setup.")
+    return device
+
+
+def _prepare_loaders(cfg):
+    try:
+        import dataset  # reference-style module on sys.path
+    except ImportError as e:
+        raise RuntimeError("train: no data loader given and no `dataset` module importable "
+                           f"({e}); pass train_loader= explicitly") from e
+    return dataset
+
+
+# ------------------------------------------------------------------------------------------------
+def train_autoencoder(config, train_loader=None, test_loader=None, device=None):
+    """VAE pre-training (reference train.py:28-138): encoder+decoder, AdamW, ReduceLROnPlateau,
+    compression_loss with the configured feature extractor, best-val checkpointing."""
+    device = device or _require_gpu()
+    encoder = SpectrogramEncoder(config["latent_dim_encoder"]).to(device)
+    decoder = SpectrogramDecoder(config["latent_dim_encoder"]).to(device)
+    feature_extractor = VGGishFeatureLoss().to(device)
+    optimizer = hoptim.AdamW(list(encoder.parameters()) + list(decoder.parameters()), lr=config["learning_rate"])
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(
+        optimizer, mode="min", factor=config["learning_rate_factor"], patience=config["learning_rate_patience"],
+        min_lr=config["learning_rate_min"])
+    if train_loader is None:
+        train_loader, test_loader = _prepare_loaders(config).prepare_dataset(config)
+    reducer = None
+    if hdist.world_size() > 1:
+        hdist.broadcast_parameters(encoder)
+        hdist.broadcast_parameters(decoder)
+        reducer = hdist.GradAllReduce(list(encoder.parameters()) + list(decoder.parameters()), average=True)
+
+    num_epochs = config["num_epochs"]
+    train_losses, val_losses = [], []
+    best_val_loss = float("inf")
+    os.makedirs("models/pretrained", exist_ok=True)
+    for epoch in range(num_epochs):
+        running = 0.0
+        encoder.train()
+        decoder.train()
+        for spectrogram in train_loader:
+            spectrogram = spectrogram[0].to(device)
+            latent = encoder(spectrogram)
+            reconstructed = decoder(latent)
+            loss = compression_loss(spectrogram, reconstructed, latent, feature_extractor)
+            running += loss.item()
+            optimizer.zero_grad()
+            loss.backward()
+            if reducer is not None:
+                reducer.finish()
+            optimizer.step()
+        avg_train = running / max(1, len(train_loader))
+        train_losses.append(avg_train)
+
+        encoder.eval()
+        decoder.eval()
+        running_val = 0.0
+        n_val = 0
+        with torch.no_grad():
+            for spectrogram in (test_loader or []):
+                spectrogram = spectrogram[0].to(device)
+                latent = encoder(spectrogram)
+                reconstructed = decoder(latent)
+                running_val += compression_loss(spectrogram, reconstructed, latent, feature_extractor).item()
+                n_val += 1
+        avg_val = running_val / max(1, n_val)
+        val_losses.append(avg_val)
+        scheduler.step(avg_val)
+        if avg_val < best_val_loss and hdist.rank() == 0:
+            best_val_loss = avg_val
+            torch.save(encoder.state_dict(), "models/pretrained/encoder.pth")
+            torch.save(decoder.state_dict(), "models/pretrained/decoder.pth")
+        print(f"Epoch: {epoch}")
+        print(f"Average Train Loss: {avg_train:.6f}")
+        print(f"Average Val Loss: {avg_val:.6f}")
+        print(f"Learning Rate: {optimizer.param_groups[0]['lr']:.6f}")
+    if hdist.rank() == 0:
+        torch.save(encoder.state_dict(), "models/pretrained/encoder.pth")
+        torch.save(decoder.state_dict(), "models/pretrained/decoder.pth")
+    return train_losses, val_losses
+
+
+# ------------------------------------------------------------------------------------------------
+class LDMTrainer:
+    """Reference train.py:140-293."""
+
+    def __init__(self, model, train_loader, device, lr=1e-4, style_loss_weight=0.1):
+        self.model = model.to(device)
+        self.train_loader = train_loader
+        self.device = torch.device(device) if not isinstance(device, torch.device) else device
+        self.style_loss_weight = style_loss_weight
+        trainable_params = [p for p in model.parameters() if p.requires_grad]
+        self.optimizer = hoptim.Adam(trainable_params, lr=lr)
+        self.scaler = hoptim.GradScaler("cuda")
+        self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", factor=0.5,
+                                                                    patience=10)
+        self.reducer = None
+        if hdist.world_size() > 1:
+            hdist.broadcast_parameters(self.model)
+            self.reducer = hdist.GradAllReduce(trainable_params)
+            self.scaler.set_grad_divisor(hdist.world_size())
+
+    def _sample_t(self, batch_size):
+        return torch.randint(0, self.model.num_timesteps, (batch_size,), device=self.device)
+
+    def train_step(self, content_spec, style_spec, t=None, noise=None):
+        """One step (reference train.py:163-208).  t / noise may be injected (parity tests); by default
+        they are drawn like the reference (randint on the device; randn_like inside the scheduler)."""
+        self.optimizer.zero_grad()
+        content_spec = content_spec.float()
+        style_spec = style_spec.float()
+        batch_size = content_spec.shape[0]
+        if t is None:
+            t = self._sample_t(batch_size)
+        with torch.autocast(device_type=self.device.type):
+            outputs = self.model(content_spec, style_spec, t, noise=noise)
+            noise_pred = outputs["noise_pred"]
+            noise = outputs["noise"]
+            z_0 = outputs["z_0"]
+            reconstructed = outputs["reconstructed"]
+            denoisinsg_loss = diffusion_loss(noise_pred, noise)
+            compression_loss_ = compression_loss(content_spec, reconstructed, z_0, self.model.feature_loss_net)
+            style_loss_ = style_loss(reconstructed, style_spec, self.model.feature_loss_net)
+            total_loss = compression_loss_ + denoisinsg_loss + self.style_loss_weight * style_loss_
+        self.scaler.scale(total_loss).backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        return {
+            "compression_loss": compression_loss_.item(),
+            "denoisinsg_loss": denoisinsg_loss.item(),
+            "style_loss": style_loss_.item(),
+            "total_loss": total_loss.item(),
+        }
+
+    def train_epoch(self, epoch):
+        self.model.train()
+        total_loss = total_compression = total_denoise = total_style = 0
+        num_batches = len(self.train_loader)
+        for batch_idx, element in enumerate(self.train_loader):
+            (content_spec, content_label), (style_spec, style_label) = element
+            content_spec = content_spec.to(self.device)
+            style_spec = style_spec.to(self.device)
+            losses = self.train_step(content_spec, style_spec)
+            total_loss += losses["total_loss"]
+            total_compression += losses["compression_loss"]
+            total_denoise += losses["denoisinsg_loss"]
+            total_style += losses["style_loss"]
+        k = config["training_iteration_noise"]     # the reference's reporting multiplier (train.py:240-243)
+        n = max(1, num_batches)
+        return total_loss / n * k, total_compression / n * k, total_denoise / n * k, total_style / n * k
+
+    def train(self, num_epochs):
+        best_loss = float("inf")  # noqa: F841  (kept from the reference)
+        train_losses, compression_losses, denoise_losses, style_losses = [], [], [], []
+        for epoch in range(num_epochs):
+            train_loss, comp, den, sty = self.train_epoch(epoch)
+            print(f"Epoch {epoch}: Train Loss = {train_loss:.4f}")
+            self.scheduler.step(train_loss)
+            train_losses.append(train_loss)
+            compression_losses.append(comp)
+            denoise_losses.append(den)
+            style_losses.append(sty)
+            print(f"Compression Loss: {comp:.4f}")
+            print(f"Denoisinsg Loss: {den:.4f}")
+            print(f"Style Loss: {sty:.4f}")
+            if epoch % 100 == 0 and hdist.rank() == 0:
+                os.makedirs("models/pretrained", exist_ok=True)
+                torch.save(self.model.state_dict(), f"models/pretrained/ldm_{epoch}.pth")
+        return train_losses, compression_losses, denoise_losses, style_losses
+
+
+def train_ldm(config, train_loader=None, device=None):
+    """Reference train.py:296-316."""
+    device = device or _require_gpu()
+    model = LDM(latent_dim=config["latent_dim_encoder"], load_full_model=False).to(device)
+    if train_loader is None:
+        ds = _prepare_loaders(config)
+        style_dataset = ds.SpectrogramPairDataset(config["processed_spectograms_dataset_folderpath"],
+                                                  config["pairing_file_path"])
+        train_dataset, _test = torch.utils.data.random_split(style_dataset, [0.8, 0.2])
+        train_loader = torch.utils.data.DataLoader(train_dataset, batch_size=config["batch_size"], shuffle=True,
+                                                   num_workers=0)
+    trainer = LDMTrainer(model, train_loader, device, lr=config["learning_rate"],
+                         style_loss_weight=config["style_loss_weight"])
+    return trainer.train(config["num_epochs"])
+
+
+def main():
+    parser = argparse.ArgumentParser(description="Train models")
+    parser.add_argument("--model", type=str, required=True, choices=["autoencoder", "ldm"],
+                        help="Which model to train (autoencoder or ldm)")
+    args = parser.parse_args()
+    if args.model == "autoencoder":
+        train_autoencoder(config)
+    elif args.model == "ldm":
+        train_ldm(config)
+
+
+if __name__ == "__main__":
+    main()

@@ -189,6 +189,13 @@ def main():
     G["train_enc_rm0"] = np32(ldm.encoder.encoder[1].running_mean)
     G["train_dec_rv1"] = np32(ldm.decoder.decoder[4].running_var)
 
+    # API surface: state_dict keys / shapes of the reference LDM (checkpoint interchange, §8(b))
+    import json
+    ref = M.LDM(32, pretrained_path="")
+    keys = {k: list(v.shape) for k, v in ref.state_dict().items()}
+    with open(os.path.join(HERE, "ref_state_dict_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0, sort_keys=True)
+
     path = os.path.join(HERE, "ref_goldens.npz")
     np.savez_compressed(path, **G)
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")

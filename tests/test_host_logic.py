@@ -1,0 +1,127 @@
+"""CPU: host-side logic of the drop-in (no kernel launches): API surface vs the reference, state_dict
+keys/shapes, schedule tables, reverse-loop coefficient tables and index lists, plans / phase tables,
+no-CPU-fallback behaviour."""
+import ctypes
+import inspect
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ldm_np as NP
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def M():
+    import models.model as M
+    return M
+
+
+def test_state_dict_keys_and_shapes_match_reference(M):
+    ref = json.load(open(os.path.join(HERE, "golden", "ref_state_dict_keys.json")))
+    mine = {k: list(v.shape) for k, v in M.LDM(32, pretrained_path="").state_dict().items()}
+    assert mine == ref
+
+
+def test_api_signatures(M):
+    import models.loss as L
+    import models.train as T
+    from models.config import config
+    assert config["forward_diffusion_num_timesteps"] == 200 and config["latent_dim_encoder"] == 32
+    sig = inspect.signature(M.LDM.__init__)
+    assert list(sig.parameters)[1:] == ["latent_dim", "pretrained_path", "pretraind_filename", "num_timesteps",
+                                        "load_full_model"]
+    assert sig.parameters["pretrained_path"].default == "models/pretrained/"
+    assert inspect.signature(M.LDM.style_ddim_sample_wrapper).parameters["timesteps"].default == 100
+    assert inspect.signature(M.LDM.content_style_transfer_wrapper).parameters["num_timesteps"].default == 250
+    assert inspect.signature(M.UNet.__init__).parameters["in_channels"].default == 1
+    for name in ("diffusion_loss", "compression_loss", "kl_regularization_loss", "perceptual_loss", "style_loss",
+                 "VGGishFeatureLoss", "gram_matrix", "perceptual_loss_old"):
+        assert hasattr(L, name)
+    for name in ("LDMTrainer", "train_autoencoder", "train_ldm", "main"):
+        assert hasattr(T, name)
+    p = inspect.signature(T.LDMTrainer.__init__).parameters
+    assert p["lr"].default == 1e-4 and p["style_loss_weight"].default == 0.1
+
+
+def test_parameter_counts(M):
+    n = lambda m: sum(p.numel() for p in m.parameters())  # noqa: E731
+    assert n(M.UNet(32, 32, 64)) == 6841504
+    assert n(M.SpectrogramEncoder(32)) == 111840
+    assert n(M.SpectrogramDecoder(32)) == 198209
+    assert n(M.StyleEncoder(1, 64)) == 2729984
+
+
+def test_schedule_buffers_bitexact(M, goldens):
+    fd = M.ForwardDiffusion(200)
+    assert np.array_equal(fd.beta_t.numpy(), goldens["sched_beta"])
+    assert np.array_equal(fd.alpha_bar_t.numpy(), goldens["sched_alpha_bar"])
+
+
+def test_reverse_coefficients_are_torch_fp32(M):
+    fd = M.ForwardDiffusion(200)
+    times = torch.linspace(199, 0, 50).long()
+    c = fd.reverse_coefs(times)
+    ab = fd.alpha_bar_t
+    assert c.shape == (49, 4) and c.dtype == torch.float32
+    assert torch.equal(c[:, 0], torch.sqrt(ab[times[:-1]]))
+    assert torch.equal(c[:, 3], torch.sqrt(1 - ab[times[1:]]))
+    assert np.array_equal(times.numpy(), NP.ddim_times(200, 50))
+
+
+def test_out_of_range_timesteps_raise_index_error(M):
+    fd = M.ForwardDiffusion(200)
+    with pytest.raises(IndexError):
+        fd.reverse_coefs(torch.linspace(249, 0, 250).long())      # content_style_transfer default (§0.5b)
+    with pytest.raises(IndexError):
+        fd._check_t(torch.tensor([0, 200]))
+
+
+def test_no_cpu_fallback(M):
+    unet = M.UNet(32, 32, 64)
+    z = torch.zeros(1, 32, 16, 16)
+    emb = {"s5": torch.zeros(1, 256, 4, 4), "s6": torch.zeros(1, 512, 2, 2)}
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        with torch.no_grad():
+            unet(z, torch.zeros(1, dtype=torch.long), emb)
+
+
+def test_conv_plans_and_layer_descs():
+    from ldm_amd import _lib as L
+    shape = L.UNetShape(8, 32, 16, 64, 64)
+    outs = []
+    for layer in range(15):
+        d = L.ConvDesc()
+        L.call("ldm_unet_layer_desc", ctypes.byref(shape), layer, ctypes.byref(d))
+        p = L.ConvPlan()
+        L.call("ldm_conv_make_plan", ctypes.byref(d), ctypes.byref(p))
+        outs.append((d.Cout, d.Hout, d.Wout))
+        assert p.kind in (1, 2) and p.packed_floats > 0
+    assert outs[0] == (64, 16, 64) and outs[4] == (512, 2, 8) and outs[5] == (256, 4, 16) and outs[8] == (32, 16, 64)
+    assert L.load().ldm_unet_workspace_floats(ctypes.byref(shape)) > 0
+    assert L.load().ldm_ddim_workspace_floats(ctypes.byref(shape), 49) > L.load().ldm_unet_workspace_floats(
+        ctypes.byref(shape))
+
+
+def test_transposed_conv_phase_geometry():
+    """k3 s2 p1 op1 and k4 s2 p1 transposed convs: the 4 parity phases cover each output once with the
+    right tap counts (1/2/2/4 and 4/4/4/4) — checked through the packed-weight size."""
+    from ldm_amd import _lib as L
+    for k, op, taps in ((3, 1, 9), (4, 0, 16)):
+        d = L.ConvDesc(2, 16, 5, 7, 32, 10, 14, k, k, 2, 1, op, 1)
+        p = L.ConvPlan()
+        L.call("ldm_conv_make_plan_forced", ctypes.byref(d), 2, 1, 1, 1, ctypes.byref(p))
+        assert p.packed_floats == taps * 16 * 32   # sum over phases of ntap * Cin * Mpad(=32)
+
+
+def test_fast_plan_override_table_loads():
+    from ldm_amd import autotune, ops
+    path = autotune.TUNED_PATH
+    if not os.path.exists(path):
+        pytest.skip("no tuned table")
+    n = autotune.load_tuned(path)
+    assert n > 0 and len(ops._PLAN_OVERRIDE) >= n
