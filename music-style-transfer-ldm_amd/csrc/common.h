@@ -57,7 +57,7 @@ struct FastDiv {
 };
 
 constexpr int kMaxPhase = 4;
-constexpr int kMaxTap = 9;
+constexpr int kMaxTap = 16;   // 4x4 windows: the decoder's k4 convT and its k4 s2 data-gradient conv
 
 // Sub-pixel phase decomposition of a (transposed) convolution, see conv.hip.
 struct PhaseTable {

@@ -53,12 +53,11 @@ struct ConvArgs {
 int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
     pt = PhaseTable{};
     LDM_REQUIRE(d.B > 0 && d.Cin > 0 && d.Hin > 0 && d.Win > 0 && d.Cout > 0, "conv: empty dimension");
-    LDM_REQUIRE(d.kh > 0 && d.kw > 0 && d.kh * d.kw <= kMaxTap * 2, "conv: unsupported kernel size");
+    LDM_REQUIRE(d.kh > 0 && d.kw > 0 && d.kh * d.kw <= kMaxTap, "conv: kernel larger than 4x4 unsupported");
     if (!d.transposed) {
         const int ho = (d.Hin + 2 * d.pad - d.kh) / d.stride + 1;
         const int wo = (d.Win + 2 * d.pad - d.kw) / d.stride + 1;
         LDM_REQUIRE(d.stride >= 1 && d.Hout == ho && d.Wout == wo, "conv: output size mismatch");
-        LDM_REQUIRE(d.kh * d.kw <= kMaxTap, "conv: kernel larger than 3x3 unsupported");
         pt.nphase = 1;
         pt.Hq = d.Hout;
         pt.Wq = d.Wout;
@@ -82,7 +81,6 @@ int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
     if (d.stride == 1) {
         // stride-1 transposed conv (= the data gradient of a stride-1 conv): one phase,
         // out[o] += x[o + pad - k] * w[k]  ->  dy = pad - kh
-        LDM_REQUIRE(d.kh * d.kw <= kMaxTap, "conv_transpose: kernel larger than 3x3 unsupported at stride 1");
         pt.nphase = 1;
         pt.Hq = d.Hout;
         pt.Wq = d.Wout;

@@ -54,8 +54,13 @@ def gather_batch(x, n_total):
     cap = max(hi - lo for lo, hi in sizes)
     pad = torch.zeros((cap,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     pad[: x.shape[0]].copy_(x)
-    out = torch.empty((w * cap,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    tdist.all_gather_into_tensor(out, pad)
+    if tdist.get_backend() == "gloo":        # CPU tests: gloo has no all_gather_into_tensor
+        chunks = [torch.empty_like(pad) for _ in range(w)]
+        tdist.all_gather(chunks, pad)
+        out = torch.cat(chunks, 0)
+    else:
+        out = torch.empty((w * cap,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        tdist.all_gather_into_tensor(out, pad)
     parts = [out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)]
     return torch.cat(parts, 0)
 
