@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="latents per GPU")
     ap.add_argument("--timesteps", type=int, default=50)
     ap.add_argument("--eta", type=float, default=0.0)
+    ap.add_argument("--split", type=int, default=1,
+                    help="run the per-GPU batch as this many sub-batch chains on separate streams (one graph)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -190,7 +192,7 @@ def main():
     with torch.no_grad():
         emb = ldm.style_encoder(style)
         eng = M.engine_for(ldm.unet)
-        gd = GraphedDDIM(eng, z_T, emb["s5"], emb["s6"], t_table, coefs, args.eta, logs=True)
+        gd = GraphedDDIM(eng, z_T, emb["s5"], emb["s6"], t_table, coefs, args.eta, logs=True, split=args.split)
         for _ in range(args.warmup):
             gd.replay()
         torch.cuda.synchronize()
@@ -222,7 +224,7 @@ def main():
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (U[0,1) style mel, N(0,1) z_T; random-init weights)",
         "config": {"workload": f"config 2: {args.timesteps}-step DDIM reverse sample ({n_iter} UNet+update "
                                f"iterations per step), batch {B}/GPU, 1x128x512 mel -> [{B},32,16,64] latents, "
-                               f"eta={args.eta}, hipGraph replay", "global_batch": B * world,
+                               f"eta={args.eta}, hipGraph replay of {args.split} concurrent sub-batch chains", "global_batch": B * world,
                    "latent": [B, 32, 16, 64], "parallelism": f"dp{world} (independent batch shards)"},
         "us_per_denoise_iteration": round(us_iter, 2),
     }

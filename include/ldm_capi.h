@@ -190,14 +190,17 @@ int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights* w, const f
 /* Reverse loop (style_conditioned_ddim_sample model.py:409-465 / content_style_ddim_sample :503-559):
  * x [B,C,H,W] updated in place over nsteps = len(times)-1 steps.  t_table [nsteps,B] int64 holds
  * times[i] repeated over the batch, coef_table [nsteps,4] the per-step coefficients.  x0_logs /
- * eps_logs (may be NULL) are [nsteps,B,C,H,W].  workspace: ldm_ddim_workspace_floats(s, nsteps) floats.
+ * eps_logs (may be NULL) hold step i at x0_logs + i*log_step_stride ([B,C,H,W] each; stride 0 = dense
+ * B*C*H*W), so a sub-batch can write straight into its slice of the full-batch logs.
+ * workspace: ldm_ddim_workspace_floats(s, nsteps) floats.
  * The time MLP for all steps is one launch before the loop; each step's update is fused into dec1's
  * epilogue.  Only launches: the caller may capture the whole loop into one hipGraph (the Python layer
- * does, with torch.cuda.CUDAGraph on the same stream). */
+ * does, with torch.cuda.CUDAGraph, splitting the batch into independent sub-batch chains on separate
+ * streams so that one chain's launch / memory latency overlaps another's work). */
 int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps);
 int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
-                    float* x0_logs, float* eps_logs, float* workspace, void* stream);
+                    float* x0_logs, float* eps_logs, int64_t log_step_stride, float* workspace, void* stream);
 
 /* ---- train step backward (LDMTrainer.train_step, train.py:163-208: scaler.scale(loss).backward()) ---
  * Data gradients of a conv are the forward kernel on the dual descriptor (conv <-> transposed conv);

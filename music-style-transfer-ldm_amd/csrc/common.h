@@ -37,22 +37,35 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Division of a non-negative int < 2^31 by a runtime constant with one mul_hi + shift (Granlund-
 // Montgomery, round-up multiplier): the GPU's integer division is a ~30-instruction VALU sequence.
+// Pin a wave-uniform value to an SGPR (a buffer soffset / resource the compiler leaves in a VGPR is
+// legalised with a waterfall loop around every load).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ void* uni_ptr(const void* p) {
+    const uint64_t u = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return (void*)(((uint64_t)hi << 32) | lo);
+}
+
+// n / d for 0 <= n < 2^31 by multiply-high and shift; branch-free (d == 1 folds in through `one`,
+// so the quotient is umulhi(n, 0) + n) — a data-independent select costs a branch at one wave/SIMD.
 struct FastDiv {
     int32_t d;
-    uint32_t mul, shr;
+    uint32_t mul, shr, one;
     static FastDiv make(int32_t dv) {
-        FastDiv f{dv, 0u, 0u};
+        FastDiv f{dv, 0u, 0u, 0xffffffffu};
         if (dv > 1) {
             uint32_t l = 0;
             while ((1u << l) < (uint32_t)dv) ++l;   // ceil(log2 d)
             const uint32_t p = 31 + l;
             f.mul = (uint32_t)(((1ull << p) + (uint32_t)dv - 1) / (uint32_t)dv);
             f.shr = p - 32;
+            f.one = 0u;
         }
         return f;
     }
     __device__ __forceinline__ int div(int n) const {
-        return d == 1 ? n : (int)(__umulhi((uint32_t)n, mul) >> shr);
+        return (int)((__umulhi((uint32_t)n, mul) >> shr) + ((uint32_t)n & one));
     }
 };
 

@@ -27,6 +27,7 @@
 // Within a K-chunk, lane group lg = lane/TILE holds k = NLG*j + lg for MFMA step j = 0..3 (NLG = 64/TILE).
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -42,16 +43,41 @@ struct ConvArgs {
     int32_t KK;     // kh*kw
     int32_t Mpad;   // rows of the packed weight
     int32_t transposed;
+    int32_t xcd_nfast;     // weight-heavy layer (weights > input bytes)
+    int32_t tile_order;    // 0 natural (N, M, phase), 1 XCD-grouped N-fast, 2 XCD-grouped M-fast
     FastDiv fd_hw, fd_w;   // n -> (b, q) and q -> (qy, qx) of the phase grid
+    FastDiv fd_cpt;        // K chunk -> (tap, channel chunk)
+    FastDiv fd_np, fd_inner;   // block -> (phase, tile), tile -> (outer, inner) of the XCD order
+    FastDiv fd_nn, fd_nm;      // natural order: block -> (N-tile, M-tile, phase)
     PhaseTable pt;
+    // Per-phase scalars of the MFMA kernel, indexed [phase] and read at static offsets (one batch of
+    // scalar loads, then a select by phase: a load indexed by the runtime phase would be a second,
+    // dependent round of kernarg reads).  Tap t = ja*nb + jb of a phase sits at
+    // (dy, dx) = (dy0 + sg*ja, dx0 + sg*jb) — the same order as pt.dy / pt.dx (checked on the host).
+    struct {
+        int32_t ry[kMaxPhase], rx[kMaxPhase];
+        int32_t dy0[kMaxPhase], dx0[kMaxPhase];
+        int32_t na[kMaxPhase], nb[kMaxPhase];
+        int32_t kchunks[kMaxPhase], wofs[kMaxPhase];
+        int32_t sg;
+    } pk;
     EpiArgs ep;
 };
+
+// mask-and-or select (a ?: chain is turned into branches by the compiler)
+__device__ __forceinline__ int sel_phase(const int32_t (&v)[kMaxPhase], int ph) {
+    const int x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
+    return (x0 & -(int)(ph == 0)) | (x1 & -(int)(ph == 1)) | (x2 & -(int)(ph == 2)) | (x3 & -(int)(ph == 3));
+}
 
 // ------------------------------------------------------------------------------------------------
 // phase / tap tables
 // ------------------------------------------------------------------------------------------------
 int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt) {
     pt = PhaseTable{};
+    // unused tap slots point far outside any input: the kernel can scan all kMaxTap slots branch-free
+    for (int p = 0; p < kMaxPhase; ++p)
+        for (int t = 0; t < kMaxTap; ++t) pt.dy[p][t] = -0x4000;
     LDM_REQUIRE(d.B > 0 && d.Cin > 0 && d.Hin > 0 && d.Win > 0 && d.Cout > 0, "conv: empty dimension");
     LDM_REQUIRE(d.kh > 0 && d.kw > 0 && d.kh * d.kw <= kMaxTap, "conv: kernel larger than 4x4 unsupported");
     if (!d.transposed) {
@@ -229,7 +255,10 @@ struct Mfma<2> {
     static __device__ __forceinline__ int row(int r, int lg) { return 4 * lg + r; }
 };
 
-constexpr int kGroup = 4;   // K-chunks per prefetch group
+#ifndef LDM_KGROUP
+#define LDM_KGROUP 4
+#endif
+constexpr int kGroupBase = LDM_KGROUP;   // K-chunks per prefetch group (two groups in flight)
 
 template <int TM, int TN>
 struct Frag {
@@ -241,9 +270,38 @@ struct Frag {
 // kinds 1/2: block = WK waves over one (TILE*TM x TILE*TN) output tile of one phase; each wave owns
 // every WK-th K-chunk, register-pipelined in groups of kGroup chunks.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int TM, int TN, int WK>
+#ifndef LDM_LOOP_OLD   // 1: incremental cursor + skipped tail compute (variant kept for A/B timing)
+#define LDM_LOOP_OLD 0
+#endif
+#ifndef LDM_DIAG   // diagnostic builds only (timing experiments, never shipped): 1 = no B loads,
+#define LDM_DIAG 0 // 2 = no A loads, 3 = neither, 4 = per-block phase timestamps
+#endif
+#if (LDM_DIAG & 4)
+__device__ unsigned long long g_ldm_stamps[1 << 16][6];
+#define LDM_STAMP(k)                                                                               \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < (1u << 16))                                          \
+            g_ldm_stamps[blockIdx.x][k] = ((k) == 0 || (k) == 5) ? __builtin_amdgcn_s_memrealtime()           \
+                                                                 : __builtin_amdgcn_s_memtime();          \
+    } while (0)
+#else
+#define LDM_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
+// NT = tap slots scanned per phase (1 for 1x1 projections, 4 for transposed-conv phases, 9 for 3x3,
+// 16 for 4x4): the per-lane tap offsets are precomputed for NT slots only.
+template <int KIND, int TM, int TN, int WK, int NT>
 __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
+    LDM_STAMP(0);
     using MF = Mfma<KIND>;
+#ifndef LDM_KG_ADAPT
+#define LDM_KG_ADAPT 1
+#endif
+    // prefetch depth scaled to the register tile: 8 chunks per group for 1x1 tiles, 4 for 2x1, 2 for
+    // 2x2 (the same register budget; short K loops then expose one memory latency, not one per group)
+    constexpr int kGroup = LDM_KG_ADAPT ? (TM * TN == 1 ? 8 : (TM * TN == 2 ? 4 : 2)) : kGroupBase;
     constexpr int TILE = MF::TILE, NLG = MF::NLG, CK = 4 * NLG;
     constexpr int BM = TILE * TM, BN = TILE * TN;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -252,10 +310,38 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // lookups below are scalar kernarg loads (lgkmcnt), not per-lane global loads that would force a
     // vmcnt(0) drain of the prefetched operands on every chunk.
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ph = blockIdx.z;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int HqWq = a.pt.Hq * a.pt.Wq;
     const int Nq = a.B * HqWq;
+    // XCD-aware tile order (bijective for any grid size): the dispatcher deals blocks round-robin over
+    // the 8 XCDs, so block b lands with the blocks b' = b mod 8.  Renumber so that each such group gets
+    // a contiguous run of tiles: phase fastest (transposed-conv phases differ in tap count, so every
+    // XCD gets the same mix), then along the operand that is cheaper to re-fetch.  Weight-heavy layers
+    // (a.xcd_nfast) walk N first, so one weight row-block's N-tiles share an XCD's L2 and the packed
+    // weights are fetched once per launch instead of once per XCD; activation-heavy layers walk M
+    // first, so the M-tiles reading the same input columns share it.
+    int ph, m0, n0;
+    {
+        // (divisions by host-precomputed multiply-high constants: no runtime integer division)
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        int mt, nt;
+        if (a.tile_order == 0) {   // natural order: N-tile fastest, then M-tile, then phase
+            const int rest = a.fd_nn.div(orig);
+            nt = orig - rest * a.fd_nn.d;
+            ph = a.fd_nm.div(rest);
+            mt = rest - ph * a.fd_nm.d;
+        } else {
+            const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+            const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+            const int tile = a.fd_np.div(wgid);
+            ph = wgid - tile * a.pt.nphase;
+            const int outer = a.fd_inner.div(tile);
+            const int inner = tile - outer * a.fd_inner.d;
+            mt = a.tile_order == 1 ? outer : inner;
+            nt = a.tile_order == 1 ? inner : outer;
+        }
+        m0 = mt * BM;
+        n0 = nt * BN;
+    }
     const int HWin = a.Hin * a.Win;
     const int col = lane % TILE, lg = lane / TILE;
 
@@ -291,23 +377,30 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             for (int r = 0; r < MF::NACC; ++r) acc[mi][ni][r] = 0.f;
 
     const int cpt = a.Cin / CK;   // chunks per tap
-    const int nchunk = a.pt.kchunks[ph];
+    const int nchunk = sel_phase(a.pk.kchunks, ph);
+    const int ph_ry = sel_phase(a.pk.ry, ph), ph_rx = sel_phase(a.pk.rx, ph);
     const int wstride_b = a.Mpad * CK * 4;                 // bytes per packed chunk
     const int nmine = nchunk > wave ? (nchunk - wave + WK - 1) / WK : 0;
     const int ngrp = (nmine + kGroup - 1) / kGroup;
+    // (uniform values pinned to SGPRs with readfirstlane: a buffer resource or soffset that the
+    // compiler parks in a VGPR turns every load into a waterfall loop)
     const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.B * a.Cin * HWin * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.w + a.pt.wofs[ph]), (short)0, nchunk * wstride_b, 0x00020000);
+        uni_ptr(a.w + sel_phase(a.pk.wofs, ph)), (short)0, uni(nchunk * wstride_b), 0x00020000);
     const int a_voff = ((m0 + col) * CK + lg * 4) * 4;
     const int cstep_b = CK * HWin * 4;                     // bytes per channel chunk in x
 
-    // Epilogue operands of the outputs this thread will finish (element e = tid + k*64*WK of the tile),
-    // issued now so they land while the K loop runs.
     constexpr int EPT = (BM * BN + 64 * WK - 1) / (64 * WK);
     constexpr bool kPre = EPT <= 8;
     EpiPre pre[kPre ? EPT : 1];
     int po[kPre ? EPT : 1], pm[kPre ? EPT : 1];
+
+    // Epilogue operands of the outputs this thread will finish (element e = tid + k*64*WK of the tile),
+    // issued first so their latency (and that of the epilogue pointers' kernarg reads) overlaps the
+    // offset precompute below and the K loop (all index math in 32 bits: the tensors are < 2^31
+    // elements, checked on the host).
+    LDM_STAMP(1);
     if constexpr (kPre) {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
@@ -320,41 +413,59 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             const int r = nn - b * HqWq;
             const int qyy = a.fd_w.div(r);
             const int qxx = r - qyy * a.pt.Wq;
-            const int oy = qyy * a.pt.osy + a.pt.ry[ph], ox = qxx * a.pt.osy + a.pt.rx[ph];
-            const size_t oidx = (((size_t)b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
+            const int oy = qyy * a.pt.osy + ph_ry, ox = qxx * a.pt.osy + ph_rx;
+            const int oidx = ((b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
             pre[k] = epi_prefetch(a, mm, b, oidx);
-            po[k] = valid ? (int)oidx : -1;
+            po[k] = valid ? oidx : -1;
             pm[k] = mm;
         }
     }
 
-    // K cursor (wave-uniform): chunk c = wave + WK*i  <->  (tap t, channel chunk cc), advanced without
-    // division; per-lane tap offsets are recomputed only when the tap changes.
-    int t_ld = wave / cpt, cc_ld = wave - (wave / cpt) * cpt, c_ld = wave;
-    int tcur = -1;
-    int voff[TN];
+    // Per-tap input offsets of this lane's columns, computed once: a tap change in the K loop is a
+    // register pick by a wave-uniform index (no tap-table loads, no divergent branch, no VALU temps
+    // that could alias prefetched registers).
+    // (taps generated arithmetically from the phase's (dy0, dx0, na, nb) — no table loads; slots past
+    // na*nb are out of window)
+    int vtap[NT][TN];
+    {
+        const int dy0 = sel_phase(a.pk.dy0, ph), dx0 = sel_phase(a.pk.dx0, ph);
+        const int na = sel_phase(a.pk.na, ph), nb = sel_phase(a.pk.nb, ph);
+        const int sg = a.pk.sg, ntap = na * nb;
+        int ja = 0, jb = 0;
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni) voff[ni] = kOOB;
+        for (int t = 0; t < NT; ++t) {
+            const int dy = t < ntap ? dy0 + sg * ja : -0x4000;
+            const int dx = dx0 + sg * jb;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) {
+                const bool ok = (unsigned)(iy0[ni] + dy) < (unsigned)a.Hin && (unsigned)(ix0[ni] + dx) < (unsigned)a.Win;
+                vtap[t][ni] = ok ? base4[ni] + (dy * a.Win + dx) * 4 : kOOB;
+            }
+            const bool wrap = jb + 1 == nb;
+            jb = wrap ? 0 : jb + 1;
+            ja += wrap ? 1 : 0;
+        }
+    }
 
-    // Loads are unconditional (past this wave's range the cursor stays on its last chunk and the
-    // compute is skipped): every path has the same loads in flight, so the vmcnt bookkeeping stays
-    // exact and the next group's loads really overlap this group's MFMAs.
+    // The MFMA stream is unconditional and the K cursor is branch-free scalar arithmetic: chunk
+    // c = wave + WK*i -> (tap t, channel chunk cc) by a multiply-high division.  A chunk past this
+    // wave's range loads its weights from an out-of-range offset (the hardware returns 0), so it adds
+    // nothing.  At one wave per SIMD nothing hides a branch or a waitcnt drain, so the loop carries
+    // none: every prefetched register is consumed on every path and the waitcnt pass counts the two
+    // groups in flight exactly.
+    constexpr int kSkipA = 0x40000000;   // soffset past any packed weight buffer
+    const int c_last = wave + WK * (nmine > 0 ? nmine - 1 : 0);
+#if LDM_LOOP_OLD
+    // (variant: incremental cursor, compute skipped past this wave's range, tail group after the loop)
+    int t_ld = uni(a.fd_cpt.div(wave)), cc_ld = wave - t_ld * cpt, c_ld = wave;
+    (void)c_last;
+    (void)kSkipA;
     auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
             const int i = grp * kGroup + q;
-            if (t_ld != tcur) {
-                tcur = t_ld;
-                const int dy = a.pt.dy[ph][t_ld], dx = a.pt.dx[ph][t_ld];
-                const int dxy4 = (dy * a.Win + dx) * 4;   // uniform
-#pragma unroll
-                for (int ni = 0; ni < TN; ++ni) {
-                    const bool ok = (unsigned)(iy0[ni] + dy) < (unsigned)a.Hin && (unsigned)(ix0[ni] + dx) < (unsigned)a.Win;
-                    voff[ni] = ok ? base4[ni] + dxy4 : kOOB;
-                }
-            }
-            const int soff_a = c_ld * wstride_b;
-            const int soff_b = cc_ld * cstep_b;
+            const int soff_a = uni(c_ld * wstride_b);
+            const int soff_b = uni(cc_ld * cstep_b);
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi)
                 f[q].a[mi] = __builtin_bit_cast(
@@ -364,8 +475,8 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     f[q].b[ni][j] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], soff_b + NLG * j * HWin * 4, 0));
-            if (i + 1 < nmine) {   // advance the cursor to this wave's next chunk
+                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, vtap[t_ld][ni], uni(soff_b + NLG * j * HWin * 4), 0));
+            if (i + 1 < nmine) {
                 c_ld += WK;
                 cc_ld += WK;
                 while (cc_ld >= cpt) {
@@ -375,31 +486,103 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             }
         }
     };
+#else
+    auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) {
+            const int i = grp * kGroup + q;
+            const bool live = i < nmine;
+            const int c = live ? wave + WK * i : c_last;
+            const int t_ld = uni(a.fd_cpt.div(c));
+            const int cc_ld = c - t_ld * cpt;
+            const int soff_a = uni(live ? c * wstride_b : kSkipA);
+            const int soff_b = uni(cc_ld * cstep_b);
+            int voff[TN];
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) voff[ni] = vtap[t_ld][ni];
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) {
+                if constexpr (LDM_DIAG & 2) {
+                    const float s = (float)(soff_a + mi) * 1e-30f;
+                    f[q].a[mi] = floatx4{s, s, s, s};
+                } else {
+                    f[q].a[mi] = __builtin_bit_cast(
+                        floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
+                }
+            }
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (LDM_DIAG & 1)
+                        f[q].b[ni][j] = (float)(voff[ni] + soff_b + j) * 1e-30f;
+                    else
+                        f[q].b[ni][j] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], uni(soff_b + NLG * j * HWin * 4), 0));
+                }
+        }
+    };
+#endif
+    // 16x16x4 f32 has a 40-cycle dependent latency vs a 32-cycle issue: a lone accumulator chain
+    // alternates two accumulators (summed before the reduction).
+    constexpr int NCH = (KIND == 2 && TM * TN == 1) ? 2 : 1;
+    typename MF::acc_t acc2[TM][TN];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+            for (int r = 0; r < MF::NACC; ++r) acc2[mi][ni][r] = 0.f;
     auto compute = [&](const Frag<TM, TN>(&f)[kGroup], int grp) {
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-            if (grp * kGroup + q < nmine) {
+#if LDM_LOOP_OLD
+            if (grp * kGroup + q >= nmine) continue;
+#else
+            (void)grp;
+#endif
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int mi = 0; mi < TM; ++mi)
+                for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-                        for (int ni = 0; ni < TN; ++ni)
+                    for (int ni = 0; ni < TN; ++ni) {
+                        if (NCH == 2 && (j & 1))
+                            acc2[mi][ni] = MF::mma(f[q].a[mi][j], f[q].b[ni][j], acc2[mi][ni]);
+                        else
                             acc[mi][ni] = MF::mma(f[q].a[mi][j], f[q].b[ni][j], acc[mi][ni]);
-            }
+                    }
         }
     };
 
+    // Group pairs: an odd group count is padded with one all-zero group, so the loop has no tail and
+    // every register in flight keeps one home across iterations (a tail compute after the loop makes
+    // the compiler rotate the prefetch registers with copies, and a copy waits for its load).
     Frag<TM, TN> f0[kGroup], f1[kGroup];
+    LDM_STAMP(2);
+    if (ngrp > 0) load(f0, 0);
+
     if (ngrp > 0) {
-        load(f0, 0);
         for (int g = 0; g < ngrp; g += 2) {
-            load(f1, g + 1);    // may be past the end: clamped + masked
+            load(f1, g + 1);
             compute(f0, g);
+#if LDM_LOOP_OLD
             if (g + 2 < ngrp) load(f0, g + 2);
+#else
+            load(f0, g + 2);    // past the end on the last pass: zero weights, never consumed
+#endif
             compute(f1, g + 1);
         }
     }
+    if constexpr (NCH == 2) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+                for (int r = 0; r < MF::NACC; ++r) acc[mi][ni][r] = acc[mi][ni][r] + acc2[mi][ni][r];
+    }
+    LDM_STAMP(3);
 
     // split-K partial tiles -> LDS, fixed-order sum, fused epilogue
     float* sw = smem + wave * BM * BN;
@@ -411,6 +594,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             for (int r = 0; r < MF::NACC; ++r)
                 sw[(TILE * mi + MF::row(r, lg)) * BN + TILE * ni + col] = acc[mi][ni][r];
     __syncthreads();
+    LDM_STAMP(4);
     if constexpr (kPre) {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
@@ -433,10 +617,18 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             const int r = n - b * HqWq;
             const int qyy = r / a.pt.Wq;
             const int qxx = r - qyy * a.pt.Wq;
-            epilogue_store(a, m, b, qyy * a.pt.osy + a.pt.ry[ph], qxx * a.pt.osy + a.pt.rx[ph], v);
+            epilogue_store(a, m, b, qyy * a.pt.osy + ph_ry, qxx * a.pt.osy + ph_rx, v);
         }
     }
+    LDM_STAMP(5);
 }
+
+#if (LDM_DIAG & 4)
+extern "C" int ldm_debug_stamps(unsigned long long* host, int nblocks) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ldm_stamps), sizeof(unsigned long long) * 6 * nblocks, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // kind 0: direct VALU conv (Cin not a multiple of 8, or tiny Cout: VAE first/last layers)
@@ -523,8 +715,47 @@ static int make_args(const ldm_conv_desc& d, const ldm_conv_plan& p, ConvArgs& a
     a.Wout = d.Wout;
     a.KK = d.kh * d.kw;
     a.transposed = d.transposed;
+    // weights vs input bytes: group tiles on an XCD along the operand that is larger
+    a.xcd_nfast = (int64_t)d.Cout * d.Cin * d.kh * d.kw > (int64_t)d.B * d.Cin * d.Hin * d.Win;
     a.fd_hw = FastDiv::make(a.pt.Hq * a.pt.Wq);
     a.fd_w = FastDiv::make(a.pt.Wq);
+    a.fd_cpt = FastDiv::make(p.kind ? d.Cin / chunk_k(p.kind) : 1);
+    a.fd_np = FastDiv::make(a.pt.nphase);
+    // per-phase scalars + the arithmetic tap form (dy0 + sg*ja, dx0 + sg*jb), verified against the table
+    a.pk = {};
+    a.pk.sg = d.transposed ? -1 : 1;
+    for (int ph = 0; ph < a.pt.nphase; ++ph) {
+        const int n = a.pt.ntap[ph];
+        int nb = 1;
+        while (nb < n && a.pt.dy[ph][nb] == a.pt.dy[ph][0]) ++nb;
+        LDM_REQUIRE(n % nb == 0, "conv: tap table is not a rectangle");
+        a.pk.ry[ph] = a.pt.ry[ph];
+        a.pk.rx[ph] = a.pt.rx[ph];
+        a.pk.dy0[ph] = a.pt.dy[ph][0];
+        a.pk.dx0[ph] = a.pt.dx[ph][0];
+        a.pk.na[ph] = n / nb;
+        a.pk.nb[ph] = nb;
+        for (int t = 0; t < n; ++t)
+            LDM_REQUIRE(a.pt.dy[ph][t] == a.pk.dy0[ph] + a.pk.sg * (t / nb) &&
+                            a.pt.dx[ph][t] == a.pk.dx0[ph] + a.pk.sg * (t % nb),
+                        "conv: tap table not in (dy0 + sg*ja, dx0 + sg*jb) order");
+        a.pk.kchunks[ph] = a.pt.kchunks[ph];
+        LDM_REQUIRE(a.pt.wofs[ph] < 0x7fffffff, "conv: packed weights too large");
+        a.pk.wofs[ph] = (int32_t)a.pt.wofs[ph];
+    }
+    // tile order: XCD-grouped N-fast for weight-heavy layers (measured: bottleneck -12 %, dec4 -9 %),
+    // natural order otherwise; LDM_TILE_ORDER=0/1/2 forces one (experiments)
+    a.tile_order = a.xcd_nfast ? 1 : 0;
+    if (const char* env = std::getenv("LDM_TILE_ORDER")) a.tile_order = std::atoi(env) % 3;
+    int nN = 1, nM = 1;
+    if (p.kind) {
+        const int bm = tile_m(p.kind) * p.tm, bn = tile_m(p.kind) * p.tn;
+        nN = (int)(((int64_t)d.B * a.pt.Hq * a.pt.Wq + bn - 1) / bn);
+        nM = (d.Cout + bm - 1) / bm;
+    }
+    a.fd_inner = FastDiv::make(a.tile_order == 1 ? nN : nM);
+    a.fd_nn = FastDiv::make(nN);
+    a.fd_nm = FastDiv::make(nM);
     return 0;
 }
 
@@ -607,16 +838,17 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     return 0;
 }
 
-template <int KIND>
-static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
+template <int KIND, int NT>
+static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     const int TILE = Mfma<KIND>::TILE;
     const int BMx = TILE * p.tm, BNx = TILE * p.tn;
     const size_t lds = (size_t)p.wk * BMx * BNx * sizeof(float);
-    dim3 grid((unsigned)((Nq + BNx - 1) / BNx), (unsigned)((a.Cout + BMx - 1) / BMx), a.pt.nphase);
+    // 1-D grid, tile order remapped XCD-aware inside the kernel
+    dim3 grid((unsigned)(((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.pt.nphase));
     dim3 block(64 * p.wk);
     const int code = (p.tm - 1) * 2 + (p.tn - 1);
 #define LDM_CASE(WK, C, TM, TN) \
-    case WK * 10 + C: hipLaunchKernelGGL((conv_mfma_kernel<KIND, TM, TN, WK>), grid, block, lds, st, a); break;
+    case WK * 10 + C: hipLaunchKernelGGL((conv_mfma_kernel<KIND, TM, TN, WK, NT>), grid, block, lds, st, a); break;
     switch (p.wk * 10 + code) {
         LDM_CASE(1, 0, 1, 1) LDM_CASE(1, 1, 1, 2) LDM_CASE(1, 2, 2, 1) LDM_CASE(1, 3, 2, 2)
         LDM_CASE(2, 0, 1, 1) LDM_CASE(2, 1, 1, 2) LDM_CASE(2, 2, 2, 1) LDM_CASE(2, 3, 2, 2)
@@ -627,6 +859,16 @@ static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hi
 #undef LDM_CASE
     LDM_CHECK_LAUNCH("conv_mfma_kernel");
     return 0;
+}
+
+template <int KIND>
+static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
+    int maxtap = 0;
+    for (int i = 0; i < a.pt.nphase; ++i) maxtap = std::max(maxtap, a.pt.ntap[i]);
+    if (maxtap <= 1) return launch_mfma_nt<KIND, 1>(a, p, Nq, st);
+    if (maxtap <= 4) return launch_mfma_nt<KIND, 4>(a, p, Nq, st);
+    if (maxtap <= 9) return launch_mfma_nt<KIND, 9>(a, p, Nq, st);
+    return launch_mfma_nt<KIND, 16>(a, p, Nq, st);
 }
 
 namespace ldm {
@@ -653,7 +895,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk), "conv forward: invalid plan");
     // buffer descriptors use 32-bit byte offsets; padding lanes use offset 0x7ffffff0 (out of range)
     LDM_REQUIRE((int64_t)d.B * d.Cin * d.Hin * d.Win * 4 < 0x7ff00000LL &&
-                    p.packed_floats * 4 < 0x7ff00000LL,
+                    p.packed_floats * 4 < 0x7ff00000LL && (int64_t)d.B * d.Cout * d.Hout * d.Wout < 0x7fffffffLL,
                 "conv forward: tensor too large for 32-bit buffer offsets (split the batch)");
     return p.kind == 1 ? launch_mfma<1>(a, p, Nq, st) : launch_mfma<2>(a, p, Nq, st);
 }

@@ -228,13 +228,16 @@ extern "C" int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights*
 
 extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                                const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps,
-                               float eta, float* x0_logs, float* eps_logs, float* workspace, void* stream) {
+                               float eta, float* x0_logs, float* eps_logs, int64_t log_step_stride, float* workspace,
+                               void* stream) {
     LDM_REQUIRE(s && w && x && s5 && s6 && t_table && coef_table && workspace, "ddim_sample: null argument");
     LDM_REQUIRE(nsteps >= 0, "ddim_sample: negative step count");
     if (nsteps == 0) return 0;
     UNetWs ws = carve(*s, workspace);
     float* temb_all = workspace + ws.total;   // [nsteps*B, 128] (ldm_ddim_workspace_floats)
-    const int64_t n = (int64_t)s->B * s->C * s->H * s->W;
+    const int64_t dense = (int64_t)s->B * s->C * s->H * s->W;
+    LDM_REQUIRE(log_step_stride == 0 || log_step_stride >= dense, "ddim_sample: log stride smaller than a step");
+    const int64_t n = log_step_stride ? log_step_stride : dense;
     hipStream_t st = (hipStream_t)stream;
     // The time MLP depends only on t: all nsteps*B embeddings in one launch before the loop (the same
     // evaluations the reference makes one step at a time, model.py:203).

@@ -41,10 +41,20 @@ def time_plan(desc, cand, x, w, y, reps=30):
             st.cuda_stream)
     for _ in range(3):
         L.check(lib.ldm_conv_forward(*args), "tune")
+    torch.cuda.synchronize()
+    # reps dependent launches captured in one hipGraph and replayed: device time per launch including
+    # the kernel boundary, without the host launch cost that dominates eager timing of short kernels
+    cap = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        a2 = args[:-1] + (cap.cuda_stream,)
+        for _ in range(reps):
+            lib.ldm_conv_forward(*a2)
+    g.replay()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(reps):
-        lib.ldm_conv_forward(*args)
+    g.replay()
     e1.record(st)
     e1.synchronize()
     return e0.elapsed_time(e1) * 1e3 / reps

@@ -110,16 +110,36 @@ class UNetEngine:
         self._bound[skey] = (vkey, w)
         return w
 
-    def workspace(self, shape, device, nsteps=0):
+    def workspace(self, shape, device, nsteps=0, slot=0):
+        """Workspace for this shape; `slot` separates concurrently running sub-batch chains."""
         n = L.load().ldm_ddim_workspace_floats(byref(shape), int(nsteps))
         if n <= 0:
             raise RuntimeError("ldm_ddim_workspace_floats failed")
-        key = (shape.B, shape.C, shape.H, shape.W, shape.nf, str(device))
+        key = (shape.B, shape.C, shape.H, shape.W, shape.nf, str(device), slot)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < n:
             ws = torch.empty(int(n), device=device, dtype=torch.float32)
             self._ws[key] = ws
         return ws
+
+    def side_streams(self, device, k):
+        key = ("streams", str(device))
+        ss = self._graphs.get(key, [])
+        while len(ss) < k:
+            ss.append(torch.cuda.Stream(device=device))
+        self._graphs[key] = ss
+        return ss[:k]
+
+    @staticmethod
+    def split_plan(t_table, B, split):
+        """[(lo, hi, t_sub)] for `split` contiguous sub-batches; t_sub = t_table[:, lo:hi] made contiguous
+        (prepared once, outside any timed / captured region, by GraphedDDIM)."""
+        split = max(1, min(int(split), B))
+        out = []
+        for k in range(split):
+            lo, hi = B * k // split, B * (k + 1) // split
+            out.append((lo, hi, t_table[:, lo:hi].contiguous()))
+        return out
 
     # -------------------------------------------------------------------------------------------
     def forward(self, z, t, s5, s6, out=None):
@@ -142,24 +162,58 @@ class UNetEngine:
                s6.data_ptr(), y.data_ptr(), ws.data_ptr(), ops.stream_handle())
         return y
 
-    def ddim_loop(self, x, s5, s6, t_table, coef_table, eta, x0_logs=None, eps_logs=None):
-        """In-place reverse loop on x ([B,C,H,W] contiguous fp32).  t_table [n,B] int64, coef [n,4] (device)."""
+    def _ddim_call(self, x, s5, s6, t_table, coef_table, eta, x0_logs, eps_logs, log_stride, slot):
         B, C, H, W = x.shape
         shape = self.shape(B, C, H, W)
         w = self.weights(shape)
         n = t_table.shape[0]
-        ws = self.workspace(shape, x.device, n)
+        ws = self.workspace(shape, x.device, n, slot)
         L.call("ldm_ddim_sample", byref(shape), byref(w), x.data_ptr(), s5.data_ptr(), s6.data_ptr(),
                t_table.data_ptr(), coef_table.data_ptr(), n, float(eta), ops._p(x0_logs), ops._p(eps_logs),
-               ws.data_ptr(), ops.stream_handle())
+               int(log_stride), ws.data_ptr(), ops.stream_handle())
+
+    def ddim_loop(self, x, s5, s6, t_table, coef_table, eta, x0_logs=None, eps_logs=None, split=1, plan=None):
+        """In-place reverse loop on x ([B,C,H,W] contiguous fp32).  t_table [n,B] int64, coef [n,4] (device).
+
+        split > 1 runs the batch as that many independent sub-batch chains, each on its own stream
+        (forked from and joined back into the current stream, so it also works under graph capture).
+        The path is per-sample, so the result is the same up to fp32 summation order (a sub-batch
+        size may get a conv plan that splits K differently); the chains' launch and memory latencies
+        overlap each other's work."""
+        B = x.shape[0]
+        if plan is None:
+            plan = self.split_plan(t_table, B, split) if split > 1 else None
+        if not plan or len(plan) == 1:
+            self._ddim_call(x, s5, s6, t_table, coef_table, eta, x0_logs, eps_logs, 0, 0)
+            return x
+        per_step = x[0].numel() * B
+        main = torch.cuda.current_stream(x.device)
+        streams = self.side_streams(x.device, len(plan))
+        C, H, W = x.shape[1:]
+        for k, (lo, hi, t_sub) in enumerate(plan):   # bind / pack / allocate on the main stream first
+            shape = self.shape(hi - lo, C, H, W)
+            self.weights(shape)
+            self.workspace(shape, x.device, t_table.shape[0], k)
+        for k, (lo, hi, t_sub) in enumerate(plan):
+            st = streams[k]
+            st.wait_stream(main)
+            if not torch.cuda.is_current_stream_capturing():
+                t_sub.record_stream(st)
+            with torch.cuda.stream(st):
+                self._ddim_call(x[lo:hi], s5[lo:hi], s6[lo:hi], t_sub, coef_table, eta,
+                                None if x0_logs is None else x0_logs[0, lo:hi],
+                                None if eps_logs is None else eps_logs[0, lo:hi], per_step, k)
+        for st in streams:
+            main.wait_stream(st)
         return x
 
 
 class GraphedDDIM:
     """A captured reverse loop with static buffers: replay() re-runs all n steps from x_init."""
 
-    def __init__(self, engine, x_init, s5, s6, t_table, coef_table, eta, logs=True):
+    def __init__(self, engine, x_init, s5, s6, t_table, coef_table, eta, logs=True, split=1):
         self.engine = engine
+        self.split = split
         dev = x_init.device
         self.x_init = x_init.contiguous().clone()
         self.x = torch.empty_like(self.x_init)
@@ -171,15 +225,45 @@ class GraphedDDIM:
         self.x0_logs = torch.empty((n,) + tuple(x_init.shape), device=dev) if logs else None
         self.eps_logs = torch.empty((n,) + tuple(x_init.shape), device=dev) if logs else None
         self.eta = float(eta)
-        # warm-up (packs weights, allocates workspace) outside capture
+        # static sub-batch timestep tables, made once outside the captured region
+        self.plan = engine.split_plan(self.t_table, x_init.shape[0], split) if split > 1 else None
+        # warm-up (packs weights, allocates workspaces) outside capture
         self.x.copy_(self.x_init)
-        engine.ddim_loop(self.x, self.s5, self.s6, self.t_table, self.coef, self.eta, self.x0_logs, self.eps_logs)
+        self.engine.ddim_loop(self.x, self.s5, self.s6, self.t_table, self.coef, self.eta, self.x0_logs,
+                              self.eps_logs, plan=self.plan)
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.x.copy_(self.x_init)
-            engine.ddim_loop(self.x, self.s5, self.s6, self.t_table, self.coef, self.eta, self.x0_logs, self.eps_logs)
+        if not self.plan:
+            self.graphs = [torch.cuda.CUDAGraph()]
+            self.streams = None
+            with torch.cuda.graph(self.graphs[0]):
+                self.x.copy_(self.x_init)
+                self.engine.ddim_loop(self.x, self.s5, self.s6, self.t_table, self.coef, self.eta, self.x0_logs,
+                                      self.eps_logs)
+            return
+        # One graph per sub-batch chain, each replayed on its own stream: a single graph's parallel
+        # branches are executed one after another, separate graphs on separate streams (hardware
+        # queues) run concurrently.
+        self.streams = engine.side_streams(dev, len(self.plan))
+        self.graphs = []
+        per_step = self.x[0].numel() * self.x.shape[0]
+        for k, (lo, hi, t_sub) in enumerate(self.plan):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.streams[k]):
+                self.x[lo:hi].copy_(self.x_init[lo:hi])
+                engine._ddim_call(self.x[lo:hi], self.s5[lo:hi], self.s6[lo:hi], t_sub, self.coef, self.eta,
+                                  None if self.x0_logs is None else self.x0_logs[0, lo:hi],
+                                  None if self.eps_logs is None else self.eps_logs[0, lo:hi], per_step, k)
+            self.graphs.append(g)
 
     def replay(self):
-        self.graph.replay()
+        if self.streams is None:
+            self.graphs[0].replay()
+            return self.x
+        main = torch.cuda.current_stream()
+        for st, g in zip(self.streams, self.graphs):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                g.replay()
+        for st in self.streams:
+            main.wait_stream(st)
         return self.x

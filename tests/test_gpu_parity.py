@@ -228,6 +228,36 @@ def test_graph_replay_equals_eager(M, cuda):
     assert torch.equal(x, y) and torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("split", [2, 3, 4])
+def test_split_chains_match_single_chain(M, cuda, split):
+    """Sub-batch chains on separate streams (eager and graph-captured) == one chain, logs included."""
+    from ldm_amd.engine import GraphedDDIM
+    unet = M.UNet(32, 32, 64)
+    recipe.fill_module(unet, seed=100)
+    unet = unet.to(cuda)
+    fd = M.ForwardDiffusion(200)
+    times = torch.linspace(199, 0, 6).long()
+    coefs = fd.reverse_coefs(times).to(cuda)
+    B, n = 4, 5
+    x0 = T(recipe.normal((B, 32, 16, 64), 19), cuda)
+    s5 = T(recipe.uniform01((B, 256, 4, 16), 20), cuda)
+    s6 = T(recipe.uniform01((B, 512, 2, 8), 21), cuda)
+    tt = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(cuda)
+    eng = M.engine_for(unet)
+    with torch.no_grad():
+        x1 = x0.clone()
+        l1 = (torch.empty((n, B, 32, 16, 64), device=cuda), torch.empty((n, B, 32, 16, 64), device=cuda))
+        eng.ddim_loop(x1, s5, s6, tt, coefs, 0.3, *l1)
+        x2 = x0.clone()
+        l2 = (torch.empty_like(l1[0]), torch.empty_like(l1[1]))
+        eng.ddim_loop(x2, s5, s6, tt, coefs, 0.3, *l2, split=split)
+        g = GraphedDDIM(eng, x0, s5, s6, tt, coefs, 0.3, logs=True, split=split)
+        y = g.replay().clone()
+    torch.cuda.synchronize()
+    for a, b in ((x1, x2), (x1, y), (l1[0], l2[0]), (l1[1], l2[1]), (l1[0], g.x0_logs), (l1[1], g.eps_logs)):
+        assert rel_err(npy(b), npy(a)) < 1e-5
+
+
 def test_index_error_like_reference(ldm, cuda):
     style = T(recipe.uniform01((1, 1, 128, 128), 701), cuda)
     with pytest.raises(IndexError):
