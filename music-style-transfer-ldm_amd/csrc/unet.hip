@@ -154,9 +154,22 @@ static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& pl
         if (_rc) return _rc;     \
     } while (0)
 
+// K/V projections of the style maps (the key/value half of both cross-attentions' in_proj,
+// model.py:153).  They depend only on s5 / s6, which are fixed for a whole reverse loop.
+static int style_kv(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* s5, const float* s6,
+                    const UNetWs& ws, hipStream_t st) {
+    LDM_TRY(conv_call(s, 10, w.ca_plan_kv[0], s5, w.ca_wkv[0], w.ca_bkv[0], 0, nullptr, nullptr, ws.kv2, st));
+    LDM_TRY(conv_call(s, 13, w.ca_plan_kv[1], s6, w.ca_wkv[1], w.ca_bkv[1], 0, nullptr, nullptr, ws.kv1, st));
+    return 0;
+}
+
+// kv_ready: ws.kv2 / ws.kv1 already hold style_kv() of these s5 / s6 (the reverse loop computes them
+// once, before its first step — the same kernel on the same inputs, so bitwise what each step's
+// in-loop projection would produce).
 static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* z, const void* t,
                         int t_is_float, const float* s5, const float* s6, float* out, const UNetWs& ws,
-                        hipStream_t st, const float* temb_pre = nullptr, const DdimFuse* fuse = nullptr) {
+                        hipStream_t st, const float* temb_pre = nullptr, const DdimFuse* fuse = nullptr,
+                        bool kv_ready = false) {
     const int HW = s.H * s.W;
     const int L2 = HW / 16, L1 = HW / 64;
     // t_embedding = time_mlp(t)[:, :, None, None]                               (model.py:203)
@@ -170,14 +183,13 @@ static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, cons
     LDM_TRY(conv_call(s, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, temb, nullptr, ws.z2, st));
     LDM_TRY(conv_call(s, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
     // z3 = cross_attention2(z3, s5)                                              (model.py:211)
+    if (!kv_ready) LDM_TRY(style_kv(s, w, s5, s6, ws, st));
     LDM_TRY(conv_call(s, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
-    LDM_TRY(conv_call(s, 10, w.ca_plan_kv[0], s5, w.ca_wkv[0], w.ca_bkv[0], 0, nullptr, nullptr, ws.kv2, st));
     LDM_TRY(ldm_attention_core(ws.q2, ws.kv2, ws.a2, s.B, 256, 4, L2, L2, (float)std::sqrt(1.0 / 64.0), st));
     LDM_TRY(conv_call(s, 11, w.ca_plan_o[0], ws.a2, w.ca_wo[0], w.ca_bo[0], 0, nullptr, nullptr, ws.c2, st));
     // z4 = relu(enc4(z3)); z4 = cross_attention1(z4, s6)                         (model.py:212-214)
     LDM_TRY(conv_call(s, 3, w.conv_plan[3], ws.c2, w.conv_w[3], w.conv_b[3], LDM_ACT_RELU, nullptr, nullptr, ws.z4, st));
     LDM_TRY(conv_call(s, 12, w.ca_plan_q[1], ws.z4, w.ca_wq[1], w.ca_bq[1], 0, nullptr, nullptr, ws.q1, st));
-    LDM_TRY(conv_call(s, 13, w.ca_plan_kv[1], s6, w.ca_wkv[1], w.ca_bkv[1], 0, nullptr, nullptr, ws.kv1, st));
     LDM_TRY(ldm_attention_core(ws.q1, ws.kv1, ws.a1, s.B, 512, 4, L1, L1, (float)std::sqrt(1.0 / 128.0), st));
     LDM_TRY(conv_call(s, 14, w.ca_plan_o[1], ws.a1, w.ca_wo[1], w.ca_bo[1], 0, nullptr, nullptr, ws.c1, st));
     // bottleneck + decoder with skips (ReLU before the add)                     (model.py:217-229)
@@ -243,6 +255,8 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
     // evaluations the reference makes one step at a time, model.py:203).
     LDM_TRY(ldm_time_mlp_forward(t_table, 0, nsteps * s->B, 128, w->t_freqs, w->t_w1, w->t_b1, w->t_w2, w->t_b2,
                                  temb_all, st));
+    // Likewise the style maps' K/V projections (model.py:153 with kv = s5 / s6, fixed for the loop).
+    LDM_TRY(style_kv(*s, *w, s5, s6, ws, st));
     for (int i = 0; i < nsteps; ++i) {
         // noise_pred = unet(x, t, style_embedding)                                (model.py:439)
         // and, fused into dec1's epilogue, the x0 / direction / eta update and the two log clones
@@ -250,7 +264,7 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
         DdimFuse fuse{coef_table + 4 * (size_t)i, eta, x, x0_logs ? x0_logs + (size_t)i * n : nullptr,
                       eps_logs ? eps_logs + (size_t)i * n : nullptr};
         LDM_TRY(unet_forward(*s, *w, x, t_table + (size_t)i * s->B, 0, s5, s6, nullptr, ws, st,
-                             temb_all + (size_t)i * s->B * 128, &fuse));
+                             temb_all + (size_t)i * s->B * 128, &fuse, /*kv_ready=*/true));
     }
     return 0;
 }
