@@ -106,13 +106,15 @@ def time_layers(engine, shape, dev, reps=50):
         ep.bias = bptr[i]
         ep.act = 1 if i < 8 else 0
         plan = plans[i]
-        args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr())
+        ws = torch.zeros(max(1, int(plan.ws_floats)), device=dev)     # split-K counters + partials
+        args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr(),
+                ws.data_ptr())
         lib = L.load()
-        L.check(lib.ldm_conv_forward(*args, st.cuda_stream), name)
-        us = _graph_time_us(lambda: lib.ldm_conv_forward(*args, torch.cuda.current_stream().cuda_stream), reps)
+        L.check(lib.ldm_conv_forward_ws(*args, st.cuda_stream), name)
+        us = _graph_time_us(lambda: lib.ldm_conv_forward_ws(*args, torch.cuda.current_stream().cuda_stream), reps)
         fl, by = layer_flops(d), layer_bytes(d)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "plan": [plan.kind, plan.tm, plan.tn, plan.wk]}
+                     "flops": fl, "bytes": by, "plan": list(plan.key())}
     # attention cores
     for name, E, Lt in (("attn2", 256, shape.H * shape.W // 16), ("attn1", 512, shape.H * shape.W // 64)):
         q = torch.randn(shape.B, E, Lt, device=dev)

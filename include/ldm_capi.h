@@ -69,18 +69,28 @@ typedef struct ldm_epilogue {
 typedef struct ldm_conv_plan {
     int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32         */
     int32_t tm, tn, wk;    /* MFMA tiles per wave along M / N, waves splitting K per block      */
+    int32_t ks;            /* blocks splitting K (>1: partial tiles + fixed-order last-arriver sum) */
+    int32_t reserved;
     int64_t packed_floats; /* size of the packed-weight buffer ldm_conv_pack_weight fills (0 = none) */
+    int64_t ws_floats;     /* workspace floats the plan needs (ks > 1): tile counters, then partials */
 } ldm_conv_plan;
 
 int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan);
-/* Force a specific plan (autotuning / tests).  Fills packed_floats; validates. */
-int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, ldm_conv_plan* plan);
+/* Force a specific plan (autotuning / tests).  Fills packed_floats / ws_floats; validates. */
+int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,
+                              ldm_conv_plan* plan);
 /* Re-lay the torch weight into the MFMA fragment order of `plan` (tap-major K, zero padded). */
 int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* w,
                          float* packed, void* stream);
-/* y = epilogue(conv(x, w)).  `w` is the packed buffer for MFMA plans, the torch weight for direct. */
+/* y = epilogue(conv(x, w)).  `w` is the packed buffer for MFMA plans, the torch weight for direct.
+ * Plans with ks > 1 need ldm_conv_forward_ws. */
 int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
                      const ldm_epilogue* ep, float* y, void* stream);
+/* The same with a caller-owned workspace of plan->ws_floats floats (may be NULL when that is 0).
+ * Its leading counter words must be zero before the first call; every call leaves them zero again,
+ * so one zero-initialised workspace serves any number of stream-ordered calls (not concurrent ones). */
+int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
+                        const ldm_epilogue* ep, float* y, float* workspace, void* stream);
 
 /* ---- BatchNorm2d, train mode (model.py:18,21,24,39,42 under .train(); model.py:307,344-347) ----
  * Batch statistics over (B,H,W) per channel, normalise in place, optional activation, and the
@@ -177,8 +187,10 @@ typedef struct ldm_unet_shape {
     int32_t nf;           /* num_filters (64)                                                   */
 } ldm_unet_shape;
 
-/* Workspace floats needed by ldm_unet_forward for this shape. */
-int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s);
+/* Workspace floats needed by ldm_unet_forward for this shape and these plans (w may be NULL: plans
+ * without cross-block K splits).  The workspace must be zero-filled once before its first use (it
+ * holds the split-K tile counters, which every call leaves zero again). */
+int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s, const ldm_unet_weights* w);
 /* Fill the 9+6 conv plans of `w` for this shape (weights must then be packed by the caller). */
 int ldm_unet_make_plans(const ldm_unet_shape* s, ldm_unet_weights* w);
 /* Conv descriptors of the 9 convs + 6 projection GEMMs (index order as in ldm_unet_weights). */
@@ -192,12 +204,12 @@ int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights* w, const f
  * times[i] repeated over the batch, coef_table [nsteps,4] the per-step coefficients.  x0_logs /
  * eps_logs (may be NULL) hold step i at x0_logs + i*log_step_stride ([B,C,H,W] each; stride 0 = dense
  * B*C*H*W), so a sub-batch can write straight into its slice of the full-batch logs.
- * workspace: ldm_ddim_workspace_floats(s, nsteps) floats.
+ * workspace: ldm_ddim_workspace_floats(s, w, nsteps) floats, zero-filled before first use.
  * The time MLP for all steps is one launch before the loop; each step's update is fused into dec1's
  * epilogue.  Only launches: the caller may capture the whole loop into one hipGraph (the Python layer
  * does, with torch.cuda.CUDAGraph, splitting the batch into independent sub-batch chains on separate
  * streams so that one chain's launch / memory latency overlaps another's work). */
-int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps);
+int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, const ldm_unet_weights* w, int32_t nsteps);
 int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
                     float* x0_logs, float* eps_logs, int64_t log_step_stride, float* workspace, void* stream);

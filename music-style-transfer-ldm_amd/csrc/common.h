@@ -112,9 +112,9 @@ struct EpiArgs {
 };
 
 // conv.hip: implicit-GEMM conv with the full internal epilogue (incl. the fused DDIM update); y may be
-// NULL when ep.ddim_coef is set.
+// NULL when ep.ddim_coef is set; ws: p.ws_floats floats (split-K counters + partials) or NULL.
 int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
-                    float* y, hipStream_t st);
+                    float* y, float* ws, hipStream_t st);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.

@@ -45,6 +45,11 @@ struct ConvArgs {
     int32_t transposed;
     int32_t xcd_nfast;     // weight-heavy layer (weights > input bytes)
     int32_t tile_order;    // 0 natural (N, M, phase), 1 XCD-grouped N-fast, 2 XCD-grouped M-fast
+    int32_t ks;            // blocks splitting K (cross-block split-K)
+    int32_t nN, nM;        // N / M tiles per phase
+    float* part;           // ks > 1: partial tiles [phase][M-tile][N-tile][ks][BM*BN]
+    int32_t* cnt;          // ks > 1: arrival counter per tile (zero between launches)
+    FastDiv fd_ks;         // M-tile' -> (M-tile, split)
     FastDiv fd_hw, fd_w;   // n -> (b, q) and q -> (qy, qx) of the phase grid
     FastDiv fd_cpt;        // K chunk -> (tap, channel chunk)
     FastDiv fd_np, fd_inner;   // block -> (phase, tile), tile -> (outer, inner) of the XCD order
@@ -64,8 +69,11 @@ struct ConvArgs {
     EpiArgs ep;
 };
 
-// mask-and-or select (a ?: chain is turned into branches by the compiler)
+// mask-and-or select (a ?: chain is turned into branches by the compiler); single-phase kernels
+// (PH4 = false) read slot 0 only, which keeps 27 scalars of kernarg traffic out of their prologue
+template <bool PH4 = true>
 __device__ __forceinline__ int sel_phase(const int32_t (&v)[kMaxPhase], int ph) {
+    if constexpr (!PH4) return v[0];
     const int x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
     return (x0 & -(int)(ph == 0)) | (x1 & -(int)(ph == 1)) | (x2 & -(int)(ph == 2)) | (x3 & -(int)(ph == 3));
 }
@@ -199,6 +207,38 @@ __device__ __forceinline__ EpiPre epi_prefetch(const ConvArgs& a, int m, int b, 
     return p;
 }
 
+// The same loads, unconditional: one buffer resource per optional operand, with zero records when the
+// operand is absent (its loads then return 0 without touching memory).  No branch, so the loads issue
+// back to back and the waitcnt pass can count them (a branchy prefetch ends in a vmcnt(0) drain
+// in front of the K loop).
+struct EpiSrc {
+    __amdgpu_buffer_rsrc_t bias, bcast, skip, x;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t opt_rsrc(const float* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(uni_ptr(p), (short)0, uni(p ? bytes : 0), 0x00020000);
+}
+
+__device__ __forceinline__ EpiSrc epi_sources(const ConvArgs& a, bool live) {
+    const EpiArgs& e = a.ep;
+    const int ybytes = live ? a.B * a.Cout * a.Hout * a.Wout * 4 : 0;
+    EpiSrc s;
+    s.bias = opt_rsrc(e.bias, live ? a.Cout * 4 : 0);
+    s.bcast = opt_rsrc(e.bcast, live ? a.B * a.Cout * 4 : 0);
+    s.skip = opt_rsrc(e.skip, ybytes);
+    s.x = opt_rsrc(e.ddim_coef ? e.ddim_x : nullptr, ybytes);
+    return s;
+}
+
+__device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, int m, int b, int oidx) {
+    EpiPre p;
+    p.bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bias, m * 4, 0, 0));
+    p.bcast = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bcast, (b * Cout + m) * 4, 0, 0));
+    p.skip = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.skip, oidx * 4, 0, 0));
+    p.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.x, oidx * 4, 0, 0));
+    return p;
+}
+
 __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx, float v, const EpiPre& p) {
     const EpiArgs& e = a.ep;
     if (e.bias) v = v + p.bias;
@@ -255,10 +295,7 @@ struct Mfma<2> {
     static __device__ __forceinline__ int row(int r, int lg) { return 4 * lg + r; }
 };
 
-#ifndef LDM_KGROUP
-#define LDM_KGROUP 4
-#endif
-constexpr int kGroupBase = LDM_KGROUP;   // K-chunks per prefetch group (two groups in flight)
+constexpr int kMaxKSplit = 16;   // blocks splitting K (ldm_conv_plan.ks)
 
 template <int TM, int TN>
 struct Frag {
@@ -267,14 +304,12 @@ struct Frag {
 };
 
 // ------------------------------------------------------------------------------------------------
-// kinds 1/2: block = WK waves over one (TILE*TM x TILE*TN) output tile of one phase; each wave owns
-// every WK-th K-chunk, register-pipelined in groups of kGroup chunks.
+// kinds 1/2: block = WK waves over one (TILE*TM x TILE*TN) output tile of one phase; the ks blocks of a
+// tile and the WK waves of a block deal the K-chunks round-robin, register-pipelined in groups of
+// kGroup chunks per wave.
 // ------------------------------------------------------------------------------------------------
-#ifndef LDM_LOOP_OLD   // 1: incremental cursor + skipped tail compute (variant kept for A/B timing)
-#define LDM_LOOP_OLD 0
-#endif
-#ifndef LDM_DIAG   // diagnostic builds only (timing experiments, never shipped): 1 = no B loads,
-#define LDM_DIAG 0 // 2 = no A loads, 3 = neither, 4 = per-block phase timestamps
+#ifndef LDM_DIAG   // diagnostic builds only (timing experiments, never shipped): 4 = per-block phase
+#define LDM_DIAG 0 // timestamps (tools/stamp_probe.py)
 #endif
 #if (LDM_DIAG & 4)
 __device__ unsigned long long g_ldm_stamps[1 << 16][6];
@@ -290,21 +325,31 @@ __device__ unsigned long long g_ldm_stamps[1 << 16][6];
     } while (0)
 #endif
 
+// Partial-tile hand-off between the ks blocks of one output tile (cross-block split-K).  Stores and
+// loads are agent-scope relaxed atomics, i.e. `global_store/load ... sc1`: written through past the
+// writer's L2 and read past the reader's L1, so no release / acquire fence (each ~1.7 us on gfx950)
+// is needed — MI355X_MICROARCH.md "Workgroup dispatch ... Valid forms", first table row.
+__device__ __forceinline__ void part_store(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float part_load(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // NT = tap slots scanned per phase (1 for 1x1 projections, 4 for transposed-conv phases, 9 for 3x3,
 // 16 for 4x4): the per-lane tap offsets are precomputed for NT slots only.
 template <int KIND, int TM, int TN, int WK, int NT>
 __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     LDM_STAMP(0);
     using MF = Mfma<KIND>;
-#ifndef LDM_KG_ADAPT
-#define LDM_KG_ADAPT 1
-#endif
+    constexpr bool PH4 = NT == 4;   // the 4-phase (stride-2 transposed) instances; all others are 1-phase
     // prefetch depth scaled to the register tile: 8 chunks per group for 1x1 tiles, 4 for 2x1, 2 for
     // 2x2 (the same register budget; short K loops then expose one memory latency, not one per group)
-    constexpr int kGroup = LDM_KG_ADAPT ? (TM * TN == 1 ? 8 : (TM * TN == 2 ? 4 : 2)) : kGroupBase;
+    constexpr int kGroup = TM * TN == 1 ? 8 : (TM * TN == 2 ? 4 : 2);
     constexpr int TILE = MF::TILE, NLG = MF::NLG, CK = 4 * NLG;
     constexpr int BM = TILE * TM, BN = TILE * TN;
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    __shared__ int s_last;
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform: chunk / tap indices then live in SGPRs and the tap-table
     // lookups below are scalar kernarg loads (lgkmcnt), not per-lane global loads that would force a
@@ -318,30 +363,35 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // XCD gets the same mix), then along the operand that is cheaper to re-fetch.  Weight-heavy layers
     // (a.xcd_nfast) walk N first, so one weight row-block's N-tiles share an XCD's L2 and the packed
     // weights are fetched once per launch instead of once per XCD; activation-heavy layers walk M
-    // first, so the M-tiles reading the same input columns share it.
-    int ph, m0, n0;
+    // first, so the M-tiles reading the same input columns share it.  The M index is extended by the
+    // K split (mt' = mt * ks + s): blocks with the same weight slice (mt, s) are the ones grouped.
+    int ph, mt, nt, ksp;
     {
-        // (divisions by host-precomputed multiply-high constants: no runtime integer division)
+        // (divisions by host-precomputed multiply-high constants: no runtime integer division; both
+        // orders are computed and selected arithmetically — a branch on tile_order splits the kernarg
+        // loads of the prologue into dependent rounds)
         const int nwg = gridDim.x, orig = blockIdx.x;
-        int mt, nt;
-        if (a.tile_order == 0) {   // natural order: N-tile fastest, then M-tile, then phase
-            const int rest = a.fd_nn.div(orig);
-            nt = orig - rest * a.fd_nn.d;
-            ph = a.fd_nm.div(rest);
-            mt = rest - ph * a.fd_nm.d;
-        } else {
-            const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
-            const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-            const int tile = a.fd_np.div(wgid);
-            ph = wgid - tile * a.pt.nphase;
-            const int outer = a.fd_inner.div(tile);
-            const int inner = tile - outer * a.fd_inner.d;
-            mt = a.tile_order == 1 ? outer : inner;
-            nt = a.tile_order == 1 ? inner : outer;
-        }
-        m0 = mt * BM;
-        n0 = nt * BN;
+        // natural order: N-tile fastest, then M-tile', then phase
+        const int rest = a.fd_nn.div(orig);
+        const int nt0 = orig - rest * a.fd_nn.d;
+        const int ph0 = PH4 ? a.fd_nm.div(rest) : 0;
+        const int mx0 = rest - ph0 * a.fd_nm.d;
+        // XCD-grouped order
+        const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+        const int tile = PH4 ? (wgid >> 2) : wgid;
+        const int ph1 = PH4 ? (wgid & 3) : 0;
+        const int outer = a.fd_inner.div(tile);
+        const int inner = tile - outer * a.fd_inner.d;
+        const int o = a.tile_order;
+        const int m0_ = -(int)(o == 0), m1_ = -(int)(o == 1), m2_ = -(int)(o == 2);
+        ph = (ph0 & m0_) | (ph1 & ~m0_);
+        const int mtx = (mx0 & m0_) | (outer & m1_) | (inner & m2_);
+        nt = (nt0 & m0_) | (inner & m1_) | (outer & m2_);
+        mt = a.fd_ks.div(mtx);
+        ksp = mtx - mt * a.ks;
     }
+    const int m0 = mt * BM, n0 = nt * BN;
     const int HWin = a.Hin * a.Win;
     const int col = lane % TILE, lg = lane / TILE;
 
@@ -377,17 +427,20 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             for (int r = 0; r < MF::NACC; ++r) acc[mi][ni][r] = 0.f;
 
     const int cpt = a.Cin / CK;   // chunks per tap
-    const int nchunk = sel_phase(a.pk.kchunks, ph);
-    const int ph_ry = sel_phase(a.pk.ry, ph), ph_rx = sel_phase(a.pk.rx, ph);
+    const int nchunk = sel_phase<PH4>(a.pk.kchunks, ph);
+    const int ph_ry = sel_phase<PH4>(a.pk.ry, ph), ph_rx = sel_phase<PH4>(a.pk.rx, ph);
     const int wstride_b = a.Mpad * CK * 4;                 // bytes per packed chunk
-    const int nmine = nchunk > wave ? (nchunk - wave + WK - 1) / WK : 0;
+    // K chunks are dealt round-robin over the ks*WK waves that share this output tile: wave `wave` of
+    // split `ksp` owns chunks g, g + G, g + 2G, ...
+    const int G = uni(a.ks * WK), g = uni(ksp * WK + wave);
+    const int nmine = nchunk > g ? uni((nchunk - g + G - 1) / G) : 0;
     const int ngrp = (nmine + kGroup - 1) / kGroup;
     // (uniform values pinned to SGPRs with readfirstlane: a buffer resource or soffset that the
     // compiler parks in a VGPR turns every load into a waterfall loop)
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.w + sel_phase(a.pk.wofs, ph)), (short)0, uni(nchunk * wstride_b), 0x00020000);
+        uni_ptr(a.w + sel_phase<PH4>(a.pk.wofs, ph)), (short)0, uni(nchunk * wstride_b), 0x00020000);
     const int a_voff = ((m0 + col) * CK + lg * 4) * 4;
     const int cstep_b = CK * HWin * 4;                     // bytes per channel chunk in x
 
@@ -399,25 +452,31 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // Epilogue operands of the outputs this thread will finish (element e = tid + k*64*WK of the tile),
     // issued first so their latency (and that of the epilogue pointers' kernarg reads) overlaps the
     // offset precompute below and the K loop (all index math in 32 bits: the tensors are < 2^31
-    // elements, checked on the host).
+    // elements, checked on the host).  With a K split only the last-arriving block runs the epilogue,
+    // so nobody prefetches.
     LDM_STAMP(1);
     if constexpr (kPre) {
+        // (issued unconditionally — with a K split only the last block runs the epilogue, and its
+        // sources get zero records instead, so the loads return 0 without touching memory)
+        const EpiSrc esrc = epi_sources(a, a.ks == 1);
+        {
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            const int e = (int)threadIdx.x + k * 64 * WK;
-            const int mloc = e / BN, nloc = e - mloc * BN;
-            const int m = m0 + mloc, n = n0 + nloc;
-            const bool valid = e < BM * BN && m < a.Cout && n < Nq;
-            const int mm = valid ? m : 0, nn = valid ? n : 0;
-            const int b = a.fd_hw.div(nn);
-            const int r = nn - b * HqWq;
-            const int qyy = a.fd_w.div(r);
-            const int qxx = r - qyy * a.pt.Wq;
-            const int oy = qyy * a.pt.osy + ph_ry, ox = qxx * a.pt.osy + ph_rx;
-            const int oidx = ((b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
-            pre[k] = epi_prefetch(a, mm, b, oidx);
-            po[k] = valid ? oidx : -1;
-            pm[k] = mm;
+            for (int k = 0; k < EPT; ++k) {
+                const int e = (int)threadIdx.x + k * 64 * WK;
+                const int mloc = e / BN, nloc = e - mloc * BN;
+                const int m = m0 + mloc, n = n0 + nloc;
+                const bool valid = e < BM * BN && m < a.Cout && n < Nq;
+                const int mm = valid ? m : 0, nn = valid ? n : 0;
+                const int b = a.fd_hw.div(nn);
+                const int r = nn - b * HqWq;
+                const int qyy = a.fd_w.div(r);
+                const int qxx = r - qyy * a.pt.Wq;
+                const int oy = qyy * a.pt.osy + ph_ry, ox = qxx * a.pt.osy + ph_rx;
+                const int oidx = ((b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
+                pre[k] = epi_prefetch_buf(esrc, a.Cout, mm, b, oidx);
+                po[k] = valid ? oidx : -1;
+                pm[k] = mm;
+            }
         }
     }
 
@@ -428,8 +487,8 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // na*nb are out of window)
     int vtap[NT][TN];
     {
-        const int dy0 = sel_phase(a.pk.dy0, ph), dx0 = sel_phase(a.pk.dx0, ph);
-        const int na = sel_phase(a.pk.na, ph), nb = sel_phase(a.pk.nb, ph);
+        const int dy0 = sel_phase<PH4>(a.pk.dy0, ph), dx0 = sel_phase<PH4>(a.pk.dx0, ph);
+        const int na = sel_phase<PH4>(a.pk.na, ph), nb = sel_phase<PH4>(a.pk.nb, ph);
         const int sg = a.pk.sg, ntap = na * nb;
         int ja = 0, jb = 0;
 #pragma unroll
@@ -447,25 +506,26 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
         }
     }
 
-    // The MFMA stream is unconditional and the K cursor is branch-free scalar arithmetic: chunk
-    // c = wave + WK*i -> (tap t, channel chunk cc) by a multiply-high division.  A chunk past this
-    // wave's range loads its weights from an out-of-range offset (the hardware returns 0), so it adds
-    // nothing.  At one wave per SIMD nothing hides a branch or a waitcnt drain, so the loop carries
-    // none: every prefetched register is consumed on every path and the waitcnt pass counts the two
-    // groups in flight exactly.
+    // The K cursor is branch-free scalar arithmetic: chunk c = g + G*i -> (tap t, channel chunk cc) by
+    // a multiply-high division.  Loads are unconditional; a chunk past this wave's range loads from
+    // out-of-range offsets (the hardware returns 0 without touching memory) and its MFMAs are skipped
+    // by a wave-uniform branch (measured: the padding MFMAs of short K loops cost up to 1.6x the
+    // useful ones).
     constexpr int kSkipA = 0x40000000;   // soffset past any packed weight buffer
-    const int c_last = wave + WK * (nmine > 0 ? nmine - 1 : 0);
-#if LDM_LOOP_OLD
-    // (variant: incremental cursor, compute skipped past this wave's range, tail group after the loop)
-    int t_ld = uni(a.fd_cpt.div(wave)), cc_ld = wave - t_ld * cpt, c_ld = wave;
-    (void)c_last;
-    (void)kSkipA;
+    const int c_last = uni(g + G * (nmine > 0 ? nmine - 1 : 0));
     auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
             const int i = grp * kGroup + q;
-            const int soff_a = uni(c_ld * wstride_b);
-            const int soff_b = uni(cc_ld * cstep_b);
+            const bool live = i < nmine;
+            const int c = live ? g + G * i : c_last;
+            const int t_ld = uni(a.fd_cpt.div(c));
+            const int cc_ld = c - t_ld * cpt;
+            const int soff_a = uni(live ? c * wstride_b : kSkipA);
+            const int soff_b = uni(live ? cc_ld * cstep_b : kSkipA);
+            int voff[TN];
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) voff[ni] = vtap[t_ld][ni];
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi)
                 f[q].a[mi] = __builtin_bit_cast(
@@ -475,54 +535,9 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     f[q].b[ni][j] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, vtap[t_ld][ni], uni(soff_b + NLG * j * HWin * 4), 0));
-            if (i + 1 < nmine) {
-                c_ld += WK;
-                cc_ld += WK;
-                while (cc_ld >= cpt) {
-                    cc_ld -= cpt;
-                    ++t_ld;
-                }
-            }
+                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], uni(soff_b + NLG * j * HWin * 4), 0));
         }
     };
-#else
-    auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
-#pragma unroll
-        for (int q = 0; q < kGroup; ++q) {
-            const int i = grp * kGroup + q;
-            const bool live = i < nmine;
-            const int c = live ? wave + WK * i : c_last;
-            const int t_ld = uni(a.fd_cpt.div(c));
-            const int cc_ld = c - t_ld * cpt;
-            const int soff_a = uni(live ? c * wstride_b : kSkipA);
-            const int soff_b = uni(cc_ld * cstep_b);
-            int voff[TN];
-#pragma unroll
-            for (int ni = 0; ni < TN; ++ni) voff[ni] = vtap[t_ld][ni];
-#pragma unroll
-            for (int mi = 0; mi < TM; ++mi) {
-                if constexpr (LDM_DIAG & 2) {
-                    const float s = (float)(soff_a + mi) * 1e-30f;
-                    f[q].a[mi] = floatx4{s, s, s, s};
-                } else {
-                    f[q].a[mi] = __builtin_bit_cast(
-                        floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
-                }
-            }
-#pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if constexpr (LDM_DIAG & 1)
-                        f[q].b[ni][j] = (float)(voff[ni] + soff_b + j) * 1e-30f;
-                    else
-                        f[q].b[ni][j] = __builtin_bit_cast(
-                            float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], uni(soff_b + NLG * j * HWin * 4), 0));
-                }
-        }
-    };
-#endif
     // 16x16x4 f32 has a 40-cycle dependent latency vs a 32-cycle issue: a lone accumulator chain
     // alternates two accumulators (summed before the reduction).
     constexpr int NCH = (KIND == 2 && TM * TN == 1) ? 2 : 1;
@@ -536,11 +551,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     auto compute = [&](const Frag<TM, TN>(&f)[kGroup], int grp) {
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-#if LDM_LOOP_OLD
-            if (grp * kGroup + q >= nmine) continue;
-#else
-            (void)grp;
-#endif
+            if (grp * kGroup + q >= nmine) break;   // wave-uniform: no MFMAs on the padding chunks
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -560,19 +571,25 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // the compiler rotate the prefetch registers with copies, and a copy waits for its load).
     Frag<TM, TN> f0[kGroup], f1[kGroup];
     LDM_STAMP(2);
+    // Groups past this wave's range are not loaded at all: an out-of-range buffer load moves no data
+    // but still costs texture-address cycles, and with short K loops padding groups were ~half of all
+    // vector-memory instructions (rocprofv3 TA_BUSY).  The steady-state loop below always has both
+    // next groups live, so its loads are unconditional and the waitcnt pass keeps the next group in
+    // flight across each compute; the tail (1 or 2 groups) is peeled.
     if (ngrp > 0) load(f0, 0);
-
-    if (ngrp > 0) {
-        for (int g = 0; g < ngrp; g += 2) {
-            load(f1, g + 1);
-            compute(f0, g);
-#if LDM_LOOP_OLD
-            if (g + 2 < ngrp) load(f0, g + 2);
-#else
-            load(f0, g + 2);    // past the end on the last pass: zero weights, never consumed
-#endif
-            compute(f1, g + 1);
-        }
+    int gi = 0;
+    for (; gi + 2 < ngrp; gi += 2) {
+        load(f1, gi + 1);
+        compute(f0, gi);
+        load(f0, gi + 2);
+        compute(f1, gi + 1);
+    }
+    if (gi + 1 < ngrp) {
+        load(f1, gi + 1);
+        compute(f0, gi);
+        compute(f1, gi + 1);
+    } else if (gi < ngrp) {
+        compute(f0, gi);
     }
     if constexpr (NCH == 2) {
 #pragma unroll
@@ -584,7 +601,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     }
     LDM_STAMP(3);
 
-    // split-K partial tiles -> LDS, fixed-order sum, fused epilogue
+    // in-block split-K partial tiles -> LDS, fixed-order sum over the WK waves
     float* sw = smem + wave * BM * BN;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -595,34 +612,80 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
                 sw[(TILE * mi + MF::row(r, lg)) * BN + TILE * ni + col] = acc[mi][ni][r];
     __syncthreads();
     LDM_STAMP(4);
-    if constexpr (kPre) {
+    if (a.ks == 1) {
+        if constexpr (kPre) {
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            const int e = (int)threadIdx.x + k * 64 * WK;
-            if (po[k] < 0) continue;
-            float v = smem[e];
+            for (int k = 0; k < EPT; ++k) {
+                const int e = (int)threadIdx.x + k * 64 * WK;
+                if (po[k] < 0) continue;
+                float v = smem[e];
 #pragma unroll
-            for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
-            epi_finish(a, pm[k], (size_t)po[k], v, pre[k]);
+                for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+                epi_finish(a, pm[k], (size_t)po[k], v, pre[k]);
+            }
+        } else {
+            for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
+                const int mloc = e / BN, nloc = e - mloc * BN;
+                const int m = m0 + mloc, n = n0 + nloc;
+                if (m >= a.Cout || n >= Nq) continue;
+                float v = smem[e];
+#pragma unroll
+                for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+                const int b = n / HqWq;
+                const int r = n - b * HqWq;
+                const int qyy = r / a.pt.Wq;
+                const int qxx = r - qyy * a.pt.Wq;
+                epilogue_store(a, m, b, qyy * a.pt.osy + ph_ry, qxx * a.pt.osy + ph_rx, v);
+            }
         }
-    } else {
-        for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
-            const int mloc = e / BN, nloc = e - mloc * BN;
-            const int m = m0 + mloc, n = n0 + nloc;
-            if (m >= a.Cout || n >= Nq) continue;
-            float v = smem[e];
+        LDM_STAMP(5);
+        return;
+    }
+
+    // Cross-block split-K: publish this block's partial tile, count arrivals; the block that arrives
+    // last sums the ks partials in split order (bitwise independent of arrival order) and runs the
+    // fused epilogue.  No block waits for another: nothing here can hang.
+    const int tile = (ph * a.nM + mt) * a.nN + nt;
+    float* tpart = a.part + (size_t)tile * a.ks * (BM * BN);
+    for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
+        float v = smem[e];
 #pragma unroll
-            for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
-            const int b = n / HqWq;
-            const int r = n - b * HqWq;
-            const int qyy = r / a.pt.Wq;
-            const int qxx = r - qyy * a.pt.Wq;
-            epilogue_store(a, m, b, qyy * a.pt.osy + ph_ry, qxx * a.pt.osy + ph_rx, v);
-        }
+        for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+        part_store(tpart + (size_t)ksp * (BM * BN) + e, v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == a.ks - 1;
+        if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
+        const int mloc = e / BN, nloc = e - mloc * BN;
+        const int m = m0 + mloc, n = n0 + nloc;
+        if (m >= a.Cout || n >= Nq) continue;
+        float own = smem[e];
+#pragma unroll
+        for (int w = 1; w < WK; ++w) own = own + smem[w * BM * BN + e];
+        float pv[kMaxKSplit];
+#pragma unroll
+        for (int s2 = 0; s2 < kMaxKSplit; ++s2)
+            if (s2 < a.ks && s2 != ksp) pv[s2] = part_load(tpart + (size_t)s2 * (BM * BN) + e);
+        float v = ksp == 0 ? own : pv[0];
+#pragma unroll
+        for (int s2 = 1; s2 < kMaxKSplit; ++s2)
+            if (s2 < a.ks) v = v + (s2 == ksp ? own : pv[s2]);
+        const int b = n / HqWq;
+        const int r = n - b * HqWq;
+        const int qyy = r / a.pt.Wq;
+        const int qxx = r - qyy * a.pt.Wq;
+        epilogue_store(a, m, b, qyy * a.pt.osy + ph_ry, qxx * a.pt.osy + ph_rx, v);
     }
     LDM_STAMP(5);
 }
-
 #if (LDM_DIAG & 4)
 extern "C" int ldm_debug_stamps(unsigned long long* host, int nblocks) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ldm_stamps), sizeof(unsigned long long) * 6 * nblocks, 0,
@@ -753,17 +816,41 @@ static int make_args(const ldm_conv_desc& d, const ldm_conv_plan& p, ConvArgs& a
         nN = (int)(((int64_t)d.B * a.pt.Hq * a.pt.Wq + bn - 1) / bn);
         nM = (d.Cout + bm - 1) / bm;
     }
-    a.fd_inner = FastDiv::make(a.tile_order == 1 ? nN : nM);
+    a.ks = p.kind ? std::max(1, (int)p.ks) : 1;
+    a.nN = nN;
+    a.nM = nM;
+    a.fd_ks = FastDiv::make(a.ks);
+    a.fd_inner = FastDiv::make(a.tile_order == 1 ? nN : nM * a.ks);
     a.fd_nn = FastDiv::make(nN);
-    a.fd_nm = FastDiv::make(nM);
+    a.fd_nm = FastDiv::make(nM * a.ks);
     return 0;
 }
 
-static bool plan_ok(const ldm_conv_desc& d, int kind, int tm, int tn, int wk) {
-    if (kind == 0) return true;
+// Workspace of a split-K plan: a fixed region of kSplitCounters int32 arrival counters (one per output
+// tile, all phases), then ks partial tiles of BM x BN floats per output tile.  The counter region has
+// the same size and place for every plan, so one zero-filled workspace can serve any sequence of
+// plans: partials never land on a counter word, and every launch leaves its counters zero.
+constexpr int64_t kSplitCounters = 1 << 16;
+
+static int64_t split_tiles(const ldm_conv_desc& d, const ldm_conv_plan& p, const PhaseTable& pt) {
+    const int bm = tile_m(p.kind) * p.tm, bn = tile_m(p.kind) * p.tn;
+    const int64_t nN = ((int64_t)d.B * pt.Hq * pt.Wq + bn - 1) / bn;
+    const int64_t nM = (d.Cout + bm - 1) / bm;
+    return nN * nM * pt.nphase;
+}
+
+static int64_t split_ws_floats(const ldm_conv_desc& d, const ldm_conv_plan& p, const PhaseTable& pt) {
+    if (p.kind == 0 || p.ks <= 1) return 0;
+    const int bm = tile_m(p.kind) * p.tm, bn = tile_m(p.kind) * p.tn;
+    return kSplitCounters + split_tiles(d, p, pt) * p.ks * bm * bn;
+}
+
+static bool plan_ok(const ldm_conv_desc& d, int kind, int tm, int tn, int wk, int ks) {
+    if (kind == 0) return ks == 1;
     if (kind != 1 && kind != 2) return false;
     if (tm < 1 || tm > 2 || tn < 1 || tn > 2) return false;
     if (wk != 1 && wk != 2 && wk != 4 && wk != 8) return false;
+    if (ks < 1 || ks > kMaxKSplit || (ks & (ks - 1))) return false;
     if (d.Cin % chunk_k(kind) != 0) return false;
     const int bm = tile_m(kind) * tm, bn = tile_m(kind) * tn;
     if ((int64_t)wk * bm * bn * 4 > 64 * 1024) return false;
@@ -774,20 +861,24 @@ static bool plan_ok(const ldm_conv_desc& d, int kind, int tm, int tn, int wk) {
 
 using namespace ldm;
 
-extern "C" int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, ldm_conv_plan* plan) {
+extern "C" int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,
+                                         ldm_conv_plan* plan) {
     LDM_REQUIRE(d && plan, "conv plan: null argument");
-    LDM_REQUIRE(plan_ok(*d, kind, tm, tn, wk), "conv plan: unsupported (kind, tm, tn, wk) for this layer");
+    LDM_REQUIRE(plan_ok(*d, kind, tm, tn, wk, ks), "conv plan: unsupported (kind, tm, tn, wk, ks) for this layer");
     ldm_conv_plan p{};
     p.kind = kind;
     p.tm = kind ? tm : 1;
     p.tn = kind ? tn : 1;
     p.wk = kind ? wk : 1;
+    p.ks = kind ? ks : 1;
     PhaseTable pt;
     int Mpad;
     int64_t floats;
     int rc = layout_for_plan(*d, p, pt, Mpad, floats);
     if (rc) return rc;
     p.packed_floats = floats;
+    LDM_REQUIRE(p.ks == 1 || split_tiles(*d, p, pt) <= kSplitCounters, "conv plan: too many tiles for a K split");
+    p.ws_floats = split_ws_floats(*d, p, pt);
     *plan = p;
     return 0;
 }
@@ -802,14 +893,14 @@ extern "C" int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan) {
     int maxtap = 0;
     for (int i = 0; i < pt.nphase; ++i) maxtap = std::max(maxtap, pt.ntap[i]);
     // direct VALU path: no 8-aligned channel chunks, or tiny output channel count
-    if (d->Cin % 8 != 0 || M < 16) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, plan);
+    if (d->Cin % 8 != 0 || M < 16) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, 1, plan);
     // Heuristic (refined by the Python-side autotuner): fill >= ~2048 waves (2 per SIMD).
     auto tiles_for = [&](int kind, int tm, int tn) {
         const int bm = tile_m(kind) * tm, bn = tile_m(kind) * tn;
         return (int64_t)((M + bm - 1) / bm) * ((Nq + bn - 1) / bn) * pt.nphase;
     };
     int kind = (M >= 32 && Nq >= 32) ? 1 : 2;
-    if (kind == 2 && d->Cin % 16 != 0) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, plan);
+    if (kind == 2 && d->Cin % 16 != 0) return ldm_conv_make_plan_forced(d, 0, 1, 1, 1, 1, plan);
     int64_t tiles = tiles_for(kind, 1, 1);
     if (kind == 1 && tiles * 8 < 1024 && d->Cin % 16 == 0) {
         kind = 2;
@@ -818,7 +909,7 @@ extern "C" int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan) {
     const int64_t chunks = (int64_t)maxtap * (d->Cin / chunk_k(kind));
     int wk = 1;
     while (wk < 8 && tiles * wk < 2048 && chunks / (wk * 2) >= 2) wk *= 2;
-    return ldm_conv_make_plan_forced(d, kind, 1, 1, wk, plan);
+    return ldm_conv_make_plan_forced(d, kind, 1, 1, wk, 1, plan);
 }
 
 extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* w, float* packed,
@@ -844,7 +935,7 @@ static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq,
     const int BMx = TILE * p.tm, BNx = TILE * p.tn;
     const size_t lds = (size_t)p.wk * BMx * BNx * sizeof(float);
     // 1-D grid, tile order remapped XCD-aware inside the kernel
-    dim3 grid((unsigned)(((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.pt.nphase));
+    dim3 grid((unsigned)(((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.ks * a.pt.nphase));
     dim3 block(64 * p.wk);
     const int code = (p.tm - 1) * 2 + (p.tn - 1);
 #define LDM_CASE(WK, C, TM, TN) \
@@ -865,8 +956,13 @@ template <int KIND>
 static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     int maxtap = 0;
     for (int i = 0; i < a.pt.nphase; ++i) maxtap = std::max(maxtap, a.pt.ntap[i]);
+    // NT = 4 <=> the 4-phase kernels (kMaxTap per phase of a stride-2 transposed conv with k <= 4 is 4)
+    if (a.pt.nphase == 4) {
+        if (maxtap > 4) return fail(3, "conv: 4-phase layer with more than 4 taps per phase");
+        return launch_mfma_nt<KIND, 4>(a, p, Nq, st);
+    }
+    if (a.pt.nphase != 1) return fail(3, "conv: unsupported phase count");
     if (maxtap <= 1) return launch_mfma_nt<KIND, 1>(a, p, Nq, st);
-    if (maxtap <= 4) return launch_mfma_nt<KIND, 4>(a, p, Nq, st);
     if (maxtap <= 9) return launch_mfma_nt<KIND, 9>(a, p, Nq, st);
     return launch_mfma_nt<KIND, 16>(a, p, Nq, st);
 }
@@ -874,8 +970,9 @@ static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hi
 namespace ldm {
 
 int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
-                    float* y, hipStream_t st) {
+                    float* y, float* ws, hipStream_t st) {
     LDM_REQUIRE(x && w && (y || ep.ddim_coef), "conv forward: null argument");
+    LDM_REQUIRE(p.ws_floats == 0 || ws, "conv forward: this plan splits K across blocks and needs a workspace");
     LDM_REQUIRE(!ep.ddim_coef || ep.ddim_x, "conv forward: fused DDIM update needs x");
     ConvArgs a;
     int rc = make_args(d, p, a);
@@ -892,18 +989,25 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
         LDM_CHECK_LAUNCH("conv_direct_kernel");
         return 0;
     }
-    LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk), "conv forward: invalid plan");
+    LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk, p.ks), "conv forward: invalid plan");
+    if (a.ks > 1) {
+        PhaseTable pt2;
+        LDM_REQUIRE(build_phase_table(d, pt2) == 0 && p.ws_floats == split_ws_floats(d, p, pt2),
+                    "conv forward: plan workspace size does not match the descriptor");
+        a.cnt = reinterpret_cast<int32_t*>(ws);
+        a.part = ws + kSplitCounters;
+    }
     // buffer descriptors use 32-bit byte offsets; padding lanes use offset 0x7ffffff0 (out of range)
     LDM_REQUIRE((int64_t)d.B * d.Cin * d.Hin * d.Win * 4 < 0x7ff00000LL &&
-                    p.packed_floats * 4 < 0x7ff00000LL && (int64_t)d.B * d.Cout * d.Hout * d.Wout < 0x7fffffffLL,
+                    p.packed_floats * 4 < 0x7ff00000LL && (int64_t)d.B * d.Cout * d.Hout * d.Wout * 4 < 0x7ff00000LL,
                 "conv forward: tensor too large for 32-bit buffer offsets (split the batch)");
     return p.kind == 1 ? launch_mfma<1>(a, p, Nq, st) : launch_mfma<2>(a, p, Nq, st);
 }
 
 }  // namespace ldm
 
-extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
-                                const ldm_epilogue* ep, float* y, void* stream) {
+extern "C" int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
+                                   const ldm_epilogue* ep, float* y, float* workspace, void* stream) {
     LDM_REQUIRE(d && plan && x && w && y, "conv forward: null argument");
     EpiArgs e{};
     if (ep) {
@@ -918,5 +1022,10 @@ extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* pla
         e.skip = ep->skip_add;
         e.act_out = ep->act_out;
     }
-    return conv_forward_ex(*d, *plan, x, w, e, y, (hipStream_t)stream);
+    return conv_forward_ex(*d, *plan, x, w, e, y, workspace, (hipStream_t)stream);
+}
+
+extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
+                                const ldm_epilogue* ep, float* y, void* stream) {
+    return ldm_conv_forward_ws(d, plan, x, w, ep, y, nullptr, stream);
 }

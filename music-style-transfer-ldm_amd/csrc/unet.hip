@@ -82,11 +82,25 @@ static int layer_desc(const ldm_unet_shape& s, int layer, ldm_conv_desc& d) {
 }
 
 struct UNetWs {
-    float *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
+    float *convws, *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
     int64_t total;
 };
 
-static UNetWs carve(const ldm_unet_shape& s, float* base) {
+// Largest split-K workspace over the 15 layers' plans (layers run one after another on one stream, so
+// they share it; its counters are zero between launches).
+static int64_t conv_ws_floats(const ldm_unet_weights* w) {
+    if (!w) return 0;
+    int64_t m = 0;
+    for (int i = 0; i < 9; ++i) m = m > w->conv_plan[i].ws_floats ? m : w->conv_plan[i].ws_floats;
+    for (int j = 0; j < 2; ++j) {
+        m = m > w->ca_plan_q[j].ws_floats ? m : w->ca_plan_q[j].ws_floats;
+        m = m > w->ca_plan_kv[j].ws_floats ? m : w->ca_plan_kv[j].ws_floats;
+        m = m > w->ca_plan_o[j].ws_floats ? m : w->ca_plan_o[j].ws_floats;
+    }
+    return m;
+}
+
+static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float* base) {
     const int64_t B = s.B, nf = s.nf, HW = (int64_t)s.H * s.W;
     const int64_t HW2 = HW / 4, L2 = HW / 16, L1 = HW / 64;
     UNetWs w{};
@@ -96,6 +110,7 @@ static UNetWs carve(const ldm_unet_shape& s, float* base) {
         off += (n + 63) / 64 * 64;   // 256-byte aligned sub-buffers
         return p;
     };
+    w.convws = take(conv_ws_floats(wts));   // first: the zero-filled counters live here
     w.temb = take(B * 128);
     w.z1 = take(B * nf * HW);
     w.z2 = take(B * 2 * nf * HW2);
@@ -127,7 +142,7 @@ struct DdimFuse {
     float* eps_log;
 };
 
-static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& plan, const float* x, const float* w,
+static int conv_call(const ldm_unet_shape& s, float* convws, int layer, const ldm_conv_plan& plan, const float* x, const float* w,
                      const float* bias, int act, const float* bcast, const float* skip, float* y, hipStream_t st,
                      const DdimFuse* fuse = nullptr) {
     ldm_conv_desc d;
@@ -145,7 +160,7 @@ static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& pl
         ep.ddim_x0_log = fuse->x0_log;
         ep.ddim_eps_log = fuse->eps_log;
     }
-    return conv_forward_ex(d, plan, x, w, ep, y, st);
+    return conv_forward_ex(d, plan, x, w, ep, y, convws, st);
 }
 
 #define LDM_TRY(expr)            \
@@ -158,8 +173,8 @@ static int conv_call(const ldm_unet_shape& s, int layer, const ldm_conv_plan& pl
 // model.py:153).  They depend only on s5 / s6, which are fixed for a whole reverse loop.
 static int style_kv(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* s5, const float* s6,
                     const UNetWs& ws, hipStream_t st) {
-    LDM_TRY(conv_call(s, 10, w.ca_plan_kv[0], s5, w.ca_wkv[0], w.ca_bkv[0], 0, nullptr, nullptr, ws.kv2, st));
-    LDM_TRY(conv_call(s, 13, w.ca_plan_kv[1], s6, w.ca_wkv[1], w.ca_bkv[1], 0, nullptr, nullptr, ws.kv1, st));
+    LDM_TRY(conv_call(s, ws.convws, 10, w.ca_plan_kv[0], s5, w.ca_wkv[0], w.ca_bkv[0], 0, nullptr, nullptr, ws.kv2, st));
+    LDM_TRY(conv_call(s, ws.convws, 13, w.ca_plan_kv[1], s6, w.ca_wkv[1], w.ca_bkv[1], 0, nullptr, nullptr, ws.kv1, st));
     return 0;
 }
 
@@ -179,25 +194,25 @@ static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, cons
         temb = ws.temb;
     }
     // z1 = relu(enc1(z)); z2 = relu(enc2(z1)) + t_emb; z3 = relu(enc3(z2))      (model.py:205-209)
-    LDM_TRY(conv_call(s, 0, w.conv_plan[0], z, w.conv_w[0], w.conv_b[0], LDM_ACT_RELU, nullptr, nullptr, ws.z1, st));
-    LDM_TRY(conv_call(s, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, temb, nullptr, ws.z2, st));
-    LDM_TRY(conv_call(s, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
+    LDM_TRY(conv_call(s, ws.convws, 0, w.conv_plan[0], z, w.conv_w[0], w.conv_b[0], LDM_ACT_RELU, nullptr, nullptr, ws.z1, st));
+    LDM_TRY(conv_call(s, ws.convws, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, temb, nullptr, ws.z2, st));
+    LDM_TRY(conv_call(s, ws.convws, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
     // z3 = cross_attention2(z3, s5)                                              (model.py:211)
     if (!kv_ready) LDM_TRY(style_kv(s, w, s5, s6, ws, st));
-    LDM_TRY(conv_call(s, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
+    LDM_TRY(conv_call(s, ws.convws, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
     LDM_TRY(ldm_attention_core(ws.q2, ws.kv2, ws.a2, s.B, 256, 4, L2, L2, (float)std::sqrt(1.0 / 64.0), st));
-    LDM_TRY(conv_call(s, 11, w.ca_plan_o[0], ws.a2, w.ca_wo[0], w.ca_bo[0], 0, nullptr, nullptr, ws.c2, st));
+    LDM_TRY(conv_call(s, ws.convws, 11, w.ca_plan_o[0], ws.a2, w.ca_wo[0], w.ca_bo[0], 0, nullptr, nullptr, ws.c2, st));
     // z4 = relu(enc4(z3)); z4 = cross_attention1(z4, s6)                         (model.py:212-214)
-    LDM_TRY(conv_call(s, 3, w.conv_plan[3], ws.c2, w.conv_w[3], w.conv_b[3], LDM_ACT_RELU, nullptr, nullptr, ws.z4, st));
-    LDM_TRY(conv_call(s, 12, w.ca_plan_q[1], ws.z4, w.ca_wq[1], w.ca_bq[1], 0, nullptr, nullptr, ws.q1, st));
+    LDM_TRY(conv_call(s, ws.convws, 3, w.conv_plan[3], ws.c2, w.conv_w[3], w.conv_b[3], LDM_ACT_RELU, nullptr, nullptr, ws.z4, st));
+    LDM_TRY(conv_call(s, ws.convws, 12, w.ca_plan_q[1], ws.z4, w.ca_wq[1], w.ca_bq[1], 0, nullptr, nullptr, ws.q1, st));
     LDM_TRY(ldm_attention_core(ws.q1, ws.kv1, ws.a1, s.B, 512, 4, L1, L1, (float)std::sqrt(1.0 / 128.0), st));
-    LDM_TRY(conv_call(s, 14, w.ca_plan_o[1], ws.a1, w.ca_wo[1], w.ca_bo[1], 0, nullptr, nullptr, ws.c1, st));
+    LDM_TRY(conv_call(s, ws.convws, 14, w.ca_plan_o[1], ws.a1, w.ca_wo[1], w.ca_bo[1], 0, nullptr, nullptr, ws.c1, st));
     // bottleneck + decoder with skips (ReLU before the add)                     (model.py:217-229)
-    LDM_TRY(conv_call(s, 4, w.conv_plan[4], ws.c1, w.conv_w[4], w.conv_b[4], LDM_ACT_RELU, nullptr, nullptr, ws.zb, st));
-    LDM_TRY(conv_call(s, 5, w.conv_plan[5], ws.zb, w.conv_w[5], w.conv_b[5], LDM_ACT_RELU, nullptr, ws.z3, ws.d4, st));
-    LDM_TRY(conv_call(s, 6, w.conv_plan[6], ws.d4, w.conv_w[6], w.conv_b[6], LDM_ACT_RELU, nullptr, ws.z2, ws.d3, st));
-    LDM_TRY(conv_call(s, 7, w.conv_plan[7], ws.d3, w.conv_w[7], w.conv_b[7], LDM_ACT_RELU, nullptr, ws.z1, ws.d2, st));
-    LDM_TRY(conv_call(s, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, out, st,
+    LDM_TRY(conv_call(s, ws.convws, 4, w.conv_plan[4], ws.c1, w.conv_w[4], w.conv_b[4], LDM_ACT_RELU, nullptr, nullptr, ws.zb, st));
+    LDM_TRY(conv_call(s, ws.convws, 5, w.conv_plan[5], ws.zb, w.conv_w[5], w.conv_b[5], LDM_ACT_RELU, nullptr, ws.z3, ws.d4, st));
+    LDM_TRY(conv_call(s, ws.convws, 6, w.conv_plan[6], ws.d4, w.conv_w[6], w.conv_b[6], LDM_ACT_RELU, nullptr, ws.z2, ws.d3, st));
+    LDM_TRY(conv_call(s, ws.convws, 7, w.conv_plan[7], ws.d3, w.conv_w[7], w.conv_b[7], LDM_ACT_RELU, nullptr, ws.z1, ws.d2, st));
+    LDM_TRY(conv_call(s, ws.convws, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, out, st,
                       fuse));
     return 0;
 }
@@ -211,9 +226,9 @@ extern "C" int ldm_unet_layer_desc(const ldm_unet_shape* s, int32_t layer, ldm_c
     return layer_desc(*s, layer, *d);
 }
 
-extern "C" int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s) {
+extern "C" int64_t ldm_unet_workspace_floats(const ldm_unet_shape* s, const ldm_unet_weights* w) {
     if (!s) return -1;
-    return carve(*s, nullptr).total;
+    return carve(*s, w, nullptr).total;
 }
 
 extern "C" int ldm_unet_make_plans(const ldm_unet_shape* s, ldm_unet_weights* w) {
@@ -234,7 +249,7 @@ extern "C" int ldm_unet_forward(const ldm_unet_shape* s, const ldm_unet_weights*
                                 int32_t t_is_float, const float* s5, const float* s6, float* out, float* workspace,
                                 void* stream) {
     LDM_REQUIRE(s && w && z && t && s5 && s6 && out && workspace, "unet_forward: null argument");
-    UNetWs ws = carve(*s, workspace);
+    UNetWs ws = carve(*s, w, workspace);
     return unet_forward(*s, *w, z, t, t_is_float, s5, s6, out, ws, (hipStream_t)stream);
 }
 
@@ -245,7 +260,7 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
     LDM_REQUIRE(s && w && x && s5 && s6 && t_table && coef_table && workspace, "ddim_sample: null argument");
     LDM_REQUIRE(nsteps >= 0, "ddim_sample: negative step count");
     if (nsteps == 0) return 0;
-    UNetWs ws = carve(*s, workspace);
+    UNetWs ws = carve(*s, w, workspace);
     float* temb_all = workspace + ws.total;   // [nsteps*B, 128] (ldm_ddim_workspace_floats)
     const int64_t dense = (int64_t)s->B * s->C * s->H * s->W;
     LDM_REQUIRE(log_step_stride == 0 || log_step_stride >= dense, "ddim_sample: log stride smaller than a step");
@@ -269,7 +284,7 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
     return 0;
 }
 
-extern "C" int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, int32_t nsteps) {
+extern "C" int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, const ldm_unet_weights* w, int32_t nsteps) {
     if (!s || nsteps < 0) return -1;
-    return carve(*s, nullptr).total + (int64_t)nsteps * s->B * 128;
+    return carve(*s, w, nullptr).total + (int64_t)nsteps * s->B * 128;
 }

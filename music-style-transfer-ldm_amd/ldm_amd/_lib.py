@@ -36,10 +36,11 @@ class Epilogue(ctypes.Structure):
 
 
 class ConvPlan(ctypes.Structure):
-    _fields_ = [("kind", c_int32), ("tm", c_int32), ("tn", c_int32), ("wk", c_int32), ("packed_floats", c_int64)]
+    _fields_ = [("kind", c_int32), ("tm", c_int32), ("tn", c_int32), ("wk", c_int32), ("ks", c_int32),
+                ("reserved", c_int32), ("packed_floats", c_int64), ("ws_floats", c_int64)]
 
     def key(self):
-        return (self.kind, self.tm, self.tn, self.wk)
+        return (self.kind, self.tm, self.tn, self.wk, self.ks)
 
 
 class UNetShape(ctypes.Structure):
@@ -62,11 +63,13 @@ SIGNATURES = {
     "ldm_capi_version": (c_int32, []),
     "ldm_device_count": (c_int32, [ctypes.POINTER(c_int32)]),
     "ldm_conv_make_plan": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan)]),
-    "ldm_conv_make_plan_forced": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, c_int32, c_int32, c_int32,
+    "ldm_conv_make_plan_forced": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, c_int32, c_int32, c_int32, c_int32,
                                             ctypes.POINTER(ConvPlan)]),
     "ldm_conv_pack_weight": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp, c_vp]),
     "ldm_conv_forward": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp,
                                    ctypes.POINTER(Epilogue), c_fp, c_vp]),
+    "ldm_conv_forward_ws": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp,
+                                      ctypes.POINTER(Epilogue), c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
                                       c_int32, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_eval": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_int32,
@@ -81,8 +84,8 @@ SIGNATURES = {
     "ldm_ddim_step":(c_int32, [c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_int64, c_vp]),
     "ldm_loss_forward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_vp, c_fp, c_vp]),
     "ldm_loss_backward": (c_int32, [c_int32, c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_vp]),
-    "ldm_unet_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape)]),
-    "ldm_ddim_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape), c_int32]),
+    "ldm_unet_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights)]),
+    "ldm_ddim_workspace_floats": (c_int64, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_int32]),
     "ldm_unet_make_plans": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights)]),
     "ldm_unet_layer_desc": (c_int32, [ctypes.POINTER(UNetShape), c_int32, ctypes.POINTER(ConvDesc)]),
     "ldm_unet_forward": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_vp, c_int32,

@@ -17,16 +17,30 @@ from . import ops
 TUNED_PATH = os.path.join(L.PKG_ROOT, "tuned_plans.json")
 
 
-def candidates(desc):
-    out = [(0, 1, 1, 1)] if desc.Cout <= 64 else []
+def _tiles(desc, kind, tm, tn):
+    tile = 32 if kind == 1 else 16
+    bm, bn = tile * tm, tile * tn
+    ph = 4 if desc.transposed and desc.stride == 2 else 1
+    nq = desc.B * (desc.Hin * desc.Win if ph == 4 else desc.Hout * desc.Wout)
+    return -(-desc.Cout // bm) * -(-nq // bn) * ph
+
+
+def candidates(desc, min_waves=256, max_waves=16384):
+    """Valid (kind, tm, tn, wk, ks) plans whose grid holds between min_waves and max_waves waves."""
+    out = [(0, 1, 1, 1, 1)] if desc.Cout <= 64 else []
     for kind in (1, 2):
         for tm in (1, 2):
             for tn in (1, 2):
+                tiles = _tiles(desc, kind, tm, tn)
                 for wk in (1, 2, 4, 8):
-                    p = L.ConvPlan()
-                    rc = L.load().ldm_conv_make_plan_forced(ctypes.byref(desc), kind, tm, tn, wk, ctypes.byref(p))
-                    if rc == 0:
-                        out.append((kind, tm, tn, wk))
+                    for ks in (1, 2, 4, 8, 16):
+                        if not min_waves <= tiles * wk * ks <= max_waves:
+                            continue
+                        p = L.ConvPlan()
+                        rc = L.load().ldm_conv_make_plan_forced(ctypes.byref(desc), kind, tm, tn, wk, ks,
+                                                                ctypes.byref(p))
+                        if rc == 0:
+                            out.append((kind, tm, tn, wk, ks))
     return out
 
 
@@ -37,10 +51,11 @@ def time_plan(desc, cand, x, w, y, reps=30):
     ep.act = 1
     st = torch.cuda.current_stream()
     lib = L.load()
+    ws = torch.zeros(max(1, int(plan.ws_floats)), device=x.device)
     args = (ctypes.byref(desc), ctypes.byref(plan), x.data_ptr(), wbuf.data_ptr(), ctypes.byref(ep), y.data_ptr(),
-            st.cuda_stream)
+            ws.data_ptr(), st.cuda_stream)
     for _ in range(3):
-        L.check(lib.ldm_conv_forward(*args), "tune")
+        L.check(lib.ldm_conv_forward_ws(*args), "tune")
     torch.cuda.synchronize()
     # reps dependent launches captured in one hipGraph and replayed: device time per launch including
     # the kernel boundary, without the host launch cost that dominates eager timing of short kernels
@@ -49,7 +64,7 @@ def time_plan(desc, cand, x, w, y, reps=30):
     with torch.cuda.graph(g, stream=cap):
         a2 = args[:-1] + (cap.cuda_stream,)
         for _ in range(reps):
-            lib.ldm_conv_forward(*a2)
+            lib.ldm_conv_forward_ws(*a2)
     g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -85,7 +100,7 @@ def load_tuned(path=TUNED_PATH):
         tab = json.load(f)
     n = 0
     for k, v in tab.get("plans", {}).items():
-        ops._PLAN_OVERRIDE[tuple(int(s) for s in k.split(","))] = tuple(v)
+        ops._PLAN_OVERRIDE[tuple(int(s) for s in k.split(","))] = tuple(v) + (1,) * (5 - len(v))
         n += 1
     return n
 

@@ -111,14 +111,16 @@ class UNetEngine:
         return w
 
     def workspace(self, shape, device, nsteps=0, slot=0):
-        """Workspace for this shape; `slot` separates concurrently running sub-batch chains."""
-        n = L.load().ldm_ddim_workspace_floats(byref(shape), int(nsteps))
+        """Workspace for this shape and its bound plans; `slot` separates concurrently running sub-batch
+        chains.  Zero-filled on allocation: it carries the split-K tile counters (ldm_capi.h)."""
+        w = self.weights(shape)
+        n = L.load().ldm_ddim_workspace_floats(byref(shape), byref(w), int(nsteps))
         if n <= 0:
             raise RuntimeError("ldm_ddim_workspace_floats failed")
         key = (shape.B, shape.C, shape.H, shape.W, shape.nf, str(device), slot)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < n:
-            ws = torch.empty(int(n), device=device, dtype=torch.float32)
+            ws = torch.zeros(int(n), device=device, dtype=torch.float32)
             self._ws[key] = ws
         return ws
 

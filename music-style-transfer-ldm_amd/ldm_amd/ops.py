@@ -69,7 +69,7 @@ class IdCache:
 
 
 _PLAN_CACHE = {}
-_PLAN_OVERRIDE = {}      # desc.key() -> (kind, tm, tn, wk), filled by the autotuner / tests
+_PLAN_OVERRIDE = {}      # desc.key() -> (kind, tm, tn, wk, ks), filled by the autotuner / tests
 _PACK_CACHE = IdCache()
 
 
@@ -87,6 +87,7 @@ def get_plan(desc, force=None):
     key = desc.key()
     force = force or _PLAN_OVERRIDE.get(key)
     if force is not None:
+        force = tuple(force) + (1,) * (5 - len(force))     # (kind, tm, tn, wk[, ks])
         plan = L.ConvPlan()
         L.call("ldm_conv_make_plan_forced", byref(desc), *force, byref(plan))
         return plan
@@ -98,8 +99,8 @@ def get_plan(desc, force=None):
     return plan
 
 
-def set_plan_override(desc, kind, tm=1, tn=1, wk=1):
-    _PLAN_OVERRIDE[desc.key()] = (kind, tm, tn, wk)
+def set_plan_override(desc, kind, tm=1, tn=1, wk=1, ks=1):
+    _PLAN_OVERRIDE[desc.key()] = (kind, tm, tn, wk, ks)
 
 
 def clear_plan_overrides():
@@ -175,8 +176,8 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
         require_device(act_out)
         assert act_out.is_contiguous() and act_out.shape == y.shape
         ep.act_out = act_out.data_ptr()
-    L.call("ldm_conv_forward", byref(desc), byref(plan), x.data_ptr(), _p(wbuf), byref(ep), y.data_ptr(),
-           stream_handle())
+    L.call("ldm_conv_forward_ws", byref(desc), byref(plan), x.data_ptr(), _p(wbuf), byref(ep), y.data_ptr(),
+           split_workspace(plan, x.device), stream_handle())
     return y
 
 
@@ -199,7 +200,8 @@ def conv_backward_data(dy, weight, desc, wkey=None):
     plan = get_plan(dd)
     wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
     dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
-    L.call("ldm_conv_forward", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), None, dx.data_ptr(), stream_handle())
+    L.call("ldm_conv_forward_ws", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), None, dx.data_ptr(),
+           split_workspace(plan, dy.device), stream_handle())
     return dx
 
 
@@ -214,6 +216,23 @@ def scratch(name, nfloats, device):
         buf = torch.empty(max(int(nfloats), 1), device=device, dtype=torch.float32)
         _WS[key] = buf
     return buf
+
+
+_SPLIT_WS = {}
+
+
+def split_workspace(plan, device):
+    """Zero-initialised workspace for a plan that splits K across blocks (None when it does not).  One
+    buffer per (device, stream): its tile counters return to zero after every launch, so stream-ordered
+    calls share it; another stream gets its own."""
+    if plan.ws_floats <= 0:
+        return None
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _SPLIT_WS.get(key)
+    if buf is None or buf.numel() < plan.ws_floats:
+        buf = torch.zeros(int(plan.ws_floats), device=device, dtype=torch.float32)
+        _SPLIT_WS[key] = buf
+    return buf.data_ptr()
 
 
 def conv_backward_weight(x, dy, desc, dw=None, accumulate=False):

@@ -262,3 +262,51 @@ def test_index_error_like_reference(ldm, cuda):
     style = T(recipe.uniform01((1, 1, 128, 128), 701), cuda)
     with pytest.raises(IndexError):
         ldm.content_style_transfer_wrapper(style, style, num_timesteps=250)
+
+
+_SPLIT_CASES = {
+    # name: (B, Cin, H, W, Cout, k, stride, transposed, plans)
+    "bottleneck": (8, 512, 2, 8, 512, 3, 1, False, [(1, 1, 1, 4, 4), (1, 2, 2, 2, 8), (2, 1, 1, 2, 16), (1, 1, 2, 1, 16)]),
+    "enc4": (8, 256, 4, 16, 512, 3, 2, False, [(1, 2, 1, 4, 2), (1, 1, 1, 2, 8)]),
+    "dec4": (8, 512, 2, 8, 256, 3, 2, True, [(1, 1, 1, 4, 4), (2, 2, 2, 2, 8), (1, 2, 2, 1, 16)]),
+    "enc1": (2, 32, 16, 64, 64, 3, 1, False, [(1, 2, 2, 4, 2), (1, 1, 2, 8, 4)]),
+    "proj": (8, 512, 1, 16, 1024, 1, 1, False, [(1, 1, 1, 4, 4), (2, 2, 1, 1, 8)]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(_SPLIT_CASES))
+def test_split_k_plans(cuda, name):
+    """Cross-block split-K (partial tiles + last-arriver fixed-order sum): equal to the unsplit plan up
+    to fp32 summation order, bitwise reproducible across launches, and never stale when the input
+    changes between launches (the partial buffers and counters are reused)."""
+    from ldm_amd import _lib as L, ops
+    B, Cin, H, W, Cout, k, stride, tr, plans = _SPLIT_CASES[name]
+    g = torch.Generator().manual_seed(42)
+    wshape = (Cin, Cout, k, k) if tr else (Cout, Cin, k, k)
+    w = (torch.randn(wshape, generator=g) * 0.05).to(cuda)
+    bias = torch.randn(Cout, generator=g).to(cuda)
+    pad, op = (k // 2, 1) if tr else (k // 2, 0)
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, stride, pad, op if tr else 0, tr)
+    xs = [torch.randn(B, Cin, H, W, generator=g).to(cuda) for _ in range(3)]
+    base = ops.get_plan(desc, force=(2, 1, 1, 1, 1))
+
+    def run(x, plan):
+        return ops.conv_forward(x, w, bias, stride=stride, padding=pad, transposed=tr, output_padding=op if tr else 0,
+                                act="relu", plan=plan)
+
+    with torch.no_grad():
+        refs = [run(x, base) for x in xs]
+        x64 = xs[0].double().cpu()
+        if tr:
+            y64 = torch.nn.functional.conv_transpose2d(x64, w.double().cpu(), bias.double().cpu(), stride, pad, op)
+        else:
+            y64 = torch.nn.functional.conv2d(x64, w.double().cpu(), bias.double().cpu(), stride, pad)
+        assert rel_err(npy(refs[0]), y64.clamp_min(0).numpy()) < 1e-5
+        for pl in plans:
+            plan = ops.get_plan(desc, force=pl)
+            assert plan.ks == pl[4] and plan.ws_floats > 0
+            outs = [run(xs[i % 3], plan) for i in range(9)]
+            torch.cuda.synchronize()
+            for i, y in enumerate(outs):
+                assert rel_err(npy(y), npy(refs[i % 3])) < 1e-5, (pl, i)
+                assert torch.equal(y, outs[i % 3]), (pl, i)

@@ -102,9 +102,29 @@ def test_conv_plans_and_layer_descs():
         outs.append((d.Cout, d.Hout, d.Wout))
         assert p.kind in (1, 2) and p.packed_floats > 0
     assert outs[0] == (64, 16, 64) and outs[4] == (512, 2, 8) and outs[5] == (256, 4, 16) and outs[8] == (32, 16, 64)
-    assert L.load().ldm_unet_workspace_floats(ctypes.byref(shape)) > 0
-    assert L.load().ldm_ddim_workspace_floats(ctypes.byref(shape), 49) > L.load().ldm_unet_workspace_floats(
-        ctypes.byref(shape))
+    assert L.load().ldm_unet_workspace_floats(ctypes.byref(shape), None) > 0
+    assert L.load().ldm_ddim_workspace_floats(ctypes.byref(shape), None, 49) > L.load().ldm_unet_workspace_floats(
+        ctypes.byref(shape), None)
+    # plans with cross-block K splits need counter + partial space on top
+    w = L.UNetWeights()
+    L.call("ldm_unet_make_plans", ctypes.byref(shape), ctypes.byref(w))
+    d = L.ConvDesc()
+    L.call("ldm_unet_layer_desc", ctypes.byref(shape), 4, ctypes.byref(d))
+    L.call("ldm_conv_make_plan_forced", ctypes.byref(d), 1, 1, 1, 4, 4, ctypes.byref(w.conv_plan[4]))
+    assert w.conv_plan[4].ws_floats == 4 * 512 * 128 + (1 << 16)
+    assert L.load().ldm_unet_workspace_floats(ctypes.byref(shape), ctypes.byref(w)) >= \
+        L.load().ldm_unet_workspace_floats(ctypes.byref(shape), None) + w.conv_plan[4].ws_floats
+
+
+def test_split_k_plan_validation():
+    from ldm_amd import _lib as L
+    d = L.ConvDesc(8, 512, 2, 8, 512, 2, 8, 3, 3, 1, 1, 0, 0)
+    p = L.ConvPlan()
+    for ks in (1, 2, 4, 8, 16):
+        L.call("ldm_conv_make_plan_forced", ctypes.byref(d), 1, 2, 2, 2, ks, ctypes.byref(p))
+        assert p.ks == ks and (p.ws_floats == 0) == (ks == 1)
+    assert L.load().ldm_conv_make_plan_forced(ctypes.byref(d), 1, 1, 1, 1, 3, ctypes.byref(p)) != 0
+    assert L.load().ldm_conv_make_plan_forced(ctypes.byref(d), 1, 1, 1, 1, 64, ctypes.byref(p)) != 0
 
 
 def test_transposed_conv_phase_geometry():
@@ -114,7 +134,7 @@ def test_transposed_conv_phase_geometry():
     for k, op, taps in ((3, 1, 9), (4, 0, 16)):
         d = L.ConvDesc(2, 16, 5, 7, 32, 10, 14, k, k, 2, 1, op, 1)
         p = L.ConvPlan()
-        L.call("ldm_conv_make_plan_forced", ctypes.byref(d), 2, 1, 1, 1, ctypes.byref(p))
+        L.call("ldm_conv_make_plan_forced", ctypes.byref(d), 2, 1, 1, 1, 1, ctypes.byref(p))
         assert p.packed_floats == taps * 16 * 32   # sum over phases of ntap * Cin * Mpad(=32)
 
 

@@ -47,9 +47,10 @@ def main():
         ep = L.Epilogue()
         ep.act = 1
         lib = L.load()
+        ws = torch.zeros(max(1, int(plan.ws_floats)), device=dev)
         a = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wb.data_ptr(), ctypes.byref(ep), y.data_ptr(),
-             st.cuda_stream)
-        fn = lambda: lib.ldm_conv_forward(*a[:-1], torch.cuda.current_stream().cuda_stream)  # noqa: E731
+             ws.data_ptr(), st.cuda_stream)
+        fn = lambda: lib.ldm_conv_forward_ws(*a[:-1], torch.cuda.current_stream().cuda_stream)  # noqa: E731
         print("plan", plan.key(), "desc", d.key())
     for _ in range(10):
         fn()

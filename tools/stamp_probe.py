@@ -44,14 +44,15 @@ def main():
         ep.bias = bptr[i]
         ep.act = 1 if i < 8 else 0
         plan = plans[i]
+        ws = torch.zeros(max(1, int(plan.ws_floats)), device=dev)
         args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr(),
-                st.cuda_stream)
+                ws.data_ptr(), st.cuda_stream)
         for _ in range(5):
-            L.check(lib.ldm_conv_forward(*args), name)
+            L.check(lib.ldm_conv_forward_ws(*args), name)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        L.check(lib.ldm_conv_forward(*args), name)
+        L.check(lib.ldm_conv_forward_ws(*args), name)
         e1.record(st)
         torch.cuda.synchronize()
         if plan.kind == 0:
@@ -61,7 +62,7 @@ def main():
         bm, bn = tile * plan.tm, tile * plan.tn
         nph = 4 if d.transposed and d.stride == 2 else 1
         nq = d.B * (d.Hin * d.Win if nph == 4 else d.Hout * d.Wout)
-        nblk = ((nq + bn - 1) // bn) * ((d.Cout + bm - 1) // bm) * nph
+        nblk = ((nq + bn - 1) // bn) * ((d.Cout + bm - 1) // bm) * nph * plan.ks
         buf = np.zeros((nblk, 6), dtype=np.uint64)
         assert lib.ldm_debug_stamps(buf.ctypes.data, nblk) == 0
         rt0, rt5 = buf[:, 0].astype(np.float64), buf[:, 5].astype(np.float64)
@@ -71,9 +72,9 @@ def main():
         # MFMAs per wave (ideal): chunks of the slowest phase / wk, x 4 x tm x tn
         taps = d.kh * d.kw if nph == 1 else max(1, (d.kh * d.kw + 3) // 4)
         ck = 8 if plan.kind == 1 else 16
-        mf = -(-(taps * d.Cin // ck) // plan.wk) * 4 * plan.tm * plan.tn
+        mf = -(-(taps * d.Cin // ck) // (plan.wk * plan.ks)) * 4 * plan.tm * plan.tn
         post = (c4 - c1) / (clk * 1e3)
-        print(f"{name:12s} {str((plan.kind, plan.tm, plan.tn, plan.wk)):10s} {nblk:6d} "
+        print(f"{name:12s} {str(plan.key()):10s} {nblk:6d} "
               f"{e0.elapsed_time(e1) * 1e3:8.2f} {(rt0.max() - rt0.min()) * 0.01:8.2f} {np.median(blk_us):7.2f} "
               f"{np.median(blk_us - post):7.2f} {np.median(c2 - c1):8.0f} {np.median(c3 - c2):9.0f} "
               f"{np.median(c4 - c3):8.0f} {clk:7.2f} {mf:6d}")

@@ -19,7 +19,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", nargs="+", default=["8x16x64"])
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--dump", default=None, help="write every candidate's median time (us) as JSON here")
+    ap.add_argument("--out", default=None, help="tuned-plan file (default: the package's tuned_plans.json)")
     args = ap.parse_args()
+    table = {}
     dev = torch.device("cuda:0")
     ops.clear_plan_overrides()
     results = {}
@@ -33,8 +36,15 @@ def main():
                 continue
             best, med = autotune.tune_desc(d, dev, rounds=args.rounds, verbose=True)
             results[d.key()] = best
-    autotune.save_tuned(results, meta={"device": torch.cuda.get_device_name(0)})
-    print("saved", len(results), "plans to", autotune.TUNED_PATH)
+            table[",".join(map(str, d.key()))] = {",".join(map(str, c)): round(t, 3) for c, t in sorted(med.items(),
+                                                                                                 key=lambda kv: kv[1])}
+    out = args.out or autotune.TUNED_PATH
+    autotune.save_tuned(results, path=out, meta={"device": torch.cuda.get_device_name(0)})
+    print("saved", len(results), "plans to", out)
+    if args.dump:
+        import json
+        with open(args.dump, "w") as f:
+            json.dump(table, f, indent=1)
 
 
 if __name__ == "__main__":
