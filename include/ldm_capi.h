@@ -42,6 +42,7 @@ typedef struct ldm_conv_desc {
     int32_t Cout, Hout, Wout;
     int32_t kh, kw, stride, pad, out_pad;
     int32_t transposed; /* 0: Conv2d weight [Cout,Cin,kh,kw]; 1: ConvTranspose2d weight [Cin,Cout,kh,kw] */
+    int32_t layout;     /* activation layouts: bit 0 input NHWC, bit 1 output (and skip) NHWC; 0 = NCHW  */
 } ldm_conv_desc;
 
 enum {

@@ -116,6 +116,11 @@ struct EpiArgs {
 int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
                     float* y, float* ws, hipStream_t st);
 
+// misc.hip: cross-attention core; tok = q / out token-major [B,L,E] (else channel-major [B,E,L]);
+// kv is always channel-major [B,2E,S].
+int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads, int32_t L,
+                      int32_t S, float scale, bool tok, hipStream_t st);
+
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.
 __device__ __forceinline__ float ddim_update(float xv, float e, const float* coef, float eta, float& x0) {

@@ -46,6 +46,7 @@ struct ConvArgs {
     int32_t xcd_nfast;     // weight-heavy layer (weights > input bytes)
     int32_t tile_order;    // 0 natural (N, M, phase), 1 XCD-grouped N-fast, 2 XCD-grouped M-fast
     int32_t ks;            // blocks splitting K (cross-block split-K)
+    int32_t out_nhwc;      // output / skip / fused-update tensors are NHWC (the input layout is a template flag)
     int32_t nN, nM;        // N / M tiles per phase
     float* part;           // ks > 1: partial tiles [phase][M-tile][N-tile][ks][BM*BN]
     int32_t* cnt;          // ks > 1: arrival counter per tile (zero between launches)
@@ -264,8 +265,12 @@ __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx
     a.y[oidx] = v;
 }
 
+__device__ __forceinline__ int out_index(const ConvArgs& a, int m, int b, int oy, int ox) {
+    return a.out_nhwc ? ((b * a.Hout + oy) * a.Wout + ox) * a.Cout + m : ((b * a.Cout + m) * a.Hout + oy) * a.Wout + ox;
+}
+
 __device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, int oy, int ox, float v) {
-    const size_t oidx = (((size_t)b * a.Cout + m) * a.Hout + oy) * a.Wout + ox;
+    const size_t oidx = out_index(a, m, b, oy, ox);
     epi_finish(a, m, oidx, v, epi_prefetch(a, m, b, oidx));
 }
 
@@ -296,6 +301,7 @@ struct Mfma<2> {
 };
 
 constexpr int kMaxKSplit = 16;   // blocks splitting K (ldm_conv_plan.ks)
+constexpr int kMaxConvLds = 160 * 1024;   // gfx950 LDS per CU (dynamic LDS above 64 KiB is opted into per kernel)
 
 template <int TM, int TN>
 struct Frag {
@@ -338,7 +344,7 @@ __device__ __forceinline__ float part_load(const float* p) {
 
 // NT = tap slots scanned per phase (1 for 1x1 projections, 4 for transposed-conv phases, 9 for 3x3,
 // 16 for 4x4): the per-lane tap offsets are precomputed for NT slots only.
-template <int KIND, int TM, int TN, int WK, int NT>
+template <int KIND, int TM, int TN, int WK, int NT, bool NHWC>
 __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     LDM_STAMP(0);
     using MF = Mfma<KIND>;
@@ -348,6 +354,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     constexpr int kGroup = TM * TN == 1 ? 8 : (TM * TN == 2 ? 4 : 2);
     constexpr int TILE = MF::TILE, NLG = MF::NLG, CK = 4 * NLG;
     constexpr int BM = TILE * TM, BN = TILE * TN;
+    constexpr int LDB = BN + 1, SLAB = BM * LDB;   // LDS partial tile [BM][BN+1]: conflict-free both ways
     extern __shared__ __attribute__((aligned(16))) float smem[];
     __shared__ int s_last;
     const int lane = threadIdx.x & 63;
@@ -413,9 +420,13 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
         const int r = nn - b * HqWq;
         const int qy = a.fd_w.div(r);
         const int qx = r - qy * a.pt.Wq;
-        iy0[ni] = nv ? qy * a.pt.sy : -0x4000000;
+        const int iyv = qy * a.pt.sy;
+        iy0[ni] = nv ? iyv : -0x4000000;
         ix0[ni] = qx * a.pt.sy;
-        base4[ni] = ((b * a.Cin + lg) * HWin + iy0[ni] * a.Win + ix0[ni]) * 4;
+        // lane group lg holds k-local 4*lg + j at MFMA step j: channels 4*lg .. 4*lg+3 of each chunk,
+        // which NHWC stores contiguously (one 16-byte load per chunk instead of four 4-byte ones)
+        base4[ni] = NHWC ? (((b * a.Hin + iyv) * a.Win + ix0[ni]) * a.Cin + 4 * lg) * 4
+                         : ((b * a.Cin + 4 * lg) * HWin + iyv * a.Win + ix0[ni]) * 4;
     }
 
     typename MF::acc_t acc[TM][TN];
@@ -442,12 +453,22 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.w + sel_phase<PH4>(a.pk.wofs, ph)), (short)0, uni(nchunk * wstride_b), 0x00020000);
     const int a_voff = ((m0 + col) * CK + lg * 4) * 4;
-    const int cstep_b = CK * HWin * 4;                     // bytes per channel chunk in x
+    const int cstep_b = NHWC ? CK * 4 : CK * HWin * 4;     // bytes per channel chunk in x
+    const int tap_mul = NHWC ? a.Cin * 4 : 4;              // bytes per input pixel step
 
     constexpr int EPT = (BM * BN + 64 * WK - 1) / (64 * WK);
     constexpr bool kPre = EPT <= 8;
     EpiPre pre[kPre ? EPT : 1];
-    int po[kPre ? EPT : 1], pm[kPre ? EPT : 1];
+    int po[kPre ? EPT : 1], pm[kPre ? EPT : 1], ps[kPre ? EPT : 1];
+    // epilogue element e of the tile -> (mloc, nloc): consecutive threads walk the output's contiguous
+    // dimension (n for NCHW, m = channel for NHWC) so the stores coalesce
+    const bool onhwc = a.out_nhwc != 0;
+    auto elem = [&](int e, int& mloc, int& nloc) {
+        const int nl_c = e / BM, ml_c = e - nl_c * BM;   // NHWC order
+        const int ml_n = e / BN, nl_n = e - ml_n * BN;   // NCHW order
+        mloc = onhwc ? ml_c : ml_n;
+        nloc = onhwc ? nl_c : nl_n;
+    };
 
     // Epilogue operands of the outputs this thread will finish (element e = tid + k*64*WK of the tile),
     // issued first so their latency (and that of the epilogue pointers' kernarg reads) overlaps the
@@ -463,7 +484,8 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
                 const int e = (int)threadIdx.x + k * 64 * WK;
-                const int mloc = e / BN, nloc = e - mloc * BN;
+                int mloc, nloc;
+                elem(e, mloc, nloc);
                 const int m = m0 + mloc, n = n0 + nloc;
                 const bool valid = e < BM * BN && m < a.Cout && n < Nq;
                 const int mm = valid ? m : 0, nn = valid ? n : 0;
@@ -472,10 +494,11 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
                 const int qyy = a.fd_w.div(r);
                 const int qxx = r - qyy * a.pt.Wq;
                 const int oy = qyy * a.pt.osy + ph_ry, ox = qxx * a.pt.osy + ph_rx;
-                const int oidx = ((b * a.Cout + mm) * a.Hout + oy) * a.Wout + ox;
+                const int oidx = out_index(a, mm, b, oy, ox);
                 pre[k] = epi_prefetch_buf(esrc, a.Cout, mm, b, oidx);
                 po[k] = valid ? oidx : -1;
                 pm[k] = mm;
+                ps[k] = mloc * LDB + nloc;
             }
         }
     }
@@ -498,7 +521,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
                 const bool ok = (unsigned)(iy0[ni] + dy) < (unsigned)a.Hin && (unsigned)(ix0[ni] + dx) < (unsigned)a.Win;
-                vtap[t][ni] = ok ? base4[ni] + (dy * a.Win + dx) * 4 : kOOB;
+                vtap[t][ni] = ok ? base4[ni] + (dy * a.Win + dx) * tap_mul : kOOB;
             }
             const bool wrap = jb + 1 == nb;
             jb = wrap ? 0 : jb + 1;
@@ -531,11 +554,19 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
                 f[q].a[mi] = __builtin_bit_cast(
                     floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
+            for (int ni = 0; ni < TN; ++ni) {
+                if constexpr (NHWC) {
+                    const floatx4 v = __builtin_bit_cast(
+                        floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, voff[ni], soff_b, 0));
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    f[q].b[ni][j] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], uni(soff_b + NLG * j * HWin * 4), 0));
+                    for (int j = 0; j < 4; ++j) f[q].b[ni][j] = v[j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        f[q].b[ni][j] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff[ni], uni(soff_b + j * HWin * 4), 0));
+                }
+            }
         }
     };
     // 16x16x4 f32 has a 40-cycle dependent latency vs a 32-cycle issue: a lone accumulator chain
@@ -602,35 +633,37 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     LDM_STAMP(3);
 
     // in-block split-K partial tiles -> LDS, fixed-order sum over the WK waves
-    float* sw = smem + wave * BM * BN;
+    float* sw = smem + wave * SLAB;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
             for (int r = 0; r < MF::NACC; ++r)
-                sw[(TILE * mi + MF::row(r, lg)) * BN + TILE * ni + col] = acc[mi][ni][r];
+                sw[(TILE * mi + MF::row(r, lg)) * LDB + TILE * ni + col] = acc[mi][ni][r];
     __syncthreads();
     LDM_STAMP(4);
     if (a.ks == 1) {
         if constexpr (kPre) {
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
-                const int e = (int)threadIdx.x + k * 64 * WK;
                 if (po[k] < 0) continue;
-                float v = smem[e];
+                const int si = ps[k];
+                float v = smem[si];
 #pragma unroll
-                for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+                for (int w = 1; w < WK; ++w) v = v + smem[w * SLAB + si];
                 epi_finish(a, pm[k], (size_t)po[k], v, pre[k]);
             }
         } else {
             for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
-                const int mloc = e / BN, nloc = e - mloc * BN;
+                int mloc, nloc;
+                elem(e, mloc, nloc);
                 const int m = m0 + mloc, n = n0 + nloc;
                 if (m >= a.Cout || n >= Nq) continue;
-                float v = smem[e];
+                const int si = mloc * LDB + nloc;
+                float v = smem[si];
 #pragma unroll
-                for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+                for (int w = 1; w < WK; ++w) v = v + smem[w * SLAB + si];
                 const int b = n / HqWq;
                 const int r = n - b * HqWq;
                 const int qyy = r / a.pt.Wq;
@@ -648,9 +681,12 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     const int tile = (ph * a.nM + mt) * a.nN + nt;
     float* tpart = a.part + (size_t)tile * a.ks * (BM * BN);
     for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
-        float v = smem[e];
+        int mloc, nloc;
+        elem(e, mloc, nloc);
+        const int si = mloc * LDB + nloc;
+        float v = smem[si];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) v = v + smem[w * BM * BN + e];
+        for (int w = 1; w < WK; ++w) v = v + smem[w * SLAB + si];
         part_store(tpart + (size_t)ksp * (BM * BN) + e, v);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -664,12 +700,14 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     __syncthreads();
     if (!s_last) return;
     for (int e = threadIdx.x; e < BM * BN; e += 64 * WK) {
-        const int mloc = e / BN, nloc = e - mloc * BN;
+        int mloc, nloc;
+        elem(e, mloc, nloc);
         const int m = m0 + mloc, n = n0 + nloc;
         if (m >= a.Cout || n >= Nq) continue;
-        float own = smem[e];
+        const int si = mloc * LDB + nloc;
+        float own = smem[si];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) own = own + smem[w * BM * BN + e];
+        for (int w = 1; w < WK; ++w) own = own + smem[w * SLAB + si];
         float pv[kMaxKSplit];
 #pragma unroll
         for (int s2 = 0; s2 < kMaxKSplit; ++s2)
@@ -751,7 +789,7 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict_
     const int m = (int)(rowid % a.Mpad);
     const int c = (int)(rowid / a.Mpad);
     const int lg = slot >> 2, j = slot & 3;
-    const int k = c * ck + nlg * j + lg;
+    const int k = c * ck + 4 * lg + j;   // MFMA step j, lane group lg <- k-local 4*lg + j (see the kernel)
     const int t = k / a.Cin, ci = k - t * a.Cin;
     float v = 0.f;
     if (m < a.Cout && t < a.pt.ntap[ph]) {
@@ -778,6 +816,7 @@ static int make_args(const ldm_conv_desc& d, const ldm_conv_plan& p, ConvArgs& a
     a.Wout = d.Wout;
     a.KK = d.kh * d.kw;
     a.transposed = d.transposed;
+    a.out_nhwc = (d.layout >> 1) & 1;
     // weights vs input bytes: group tiles on an XCD along the operand that is larger
     a.xcd_nfast = (int64_t)d.Cout * d.Cin * d.kh * d.kw > (int64_t)d.B * d.Cin * d.Hin * d.Win;
     a.fd_hw = FastDiv::make(a.pt.Hq * a.pt.Wq);
@@ -846,14 +885,15 @@ static int64_t split_ws_floats(const ldm_conv_desc& d, const ldm_conv_plan& p, c
 }
 
 static bool plan_ok(const ldm_conv_desc& d, int kind, int tm, int tn, int wk, int ks) {
-    if (kind == 0) return ks == 1;
+    if (d.layout & ~3) return false;
+    if (kind == 0) return ks == 1 && d.layout == 0;   // the direct VALU kernel is NCHW only
     if (kind != 1 && kind != 2) return false;
     if (tm < 1 || tm > 2 || tn < 1 || tn > 2) return false;
     if (wk != 1 && wk != 2 && wk != 4 && wk != 8) return false;
     if (ks < 1 || ks > kMaxKSplit || (ks & (ks - 1))) return false;
     if (d.Cin % chunk_k(kind) != 0) return false;
     const int bm = tile_m(kind) * tm, bn = tile_m(kind) * tn;
-    if ((int64_t)wk * bm * bn * 4 > 64 * 1024) return false;
+    if ((int64_t)wk * bm * (bn + 1) * 4 > kMaxConvLds) return false;
     return true;
 }
 
@@ -929,17 +969,29 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     return 0;
 }
 
-template <int KIND, int NT>
+template <int KIND, int NT, bool NHWC>
 static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     const int TILE = Mfma<KIND>::TILE;
     const int BMx = TILE * p.tm, BNx = TILE * p.tn;
-    const size_t lds = (size_t)p.wk * BMx * BNx * sizeof(float);
+    const size_t lds = (size_t)p.wk * BMx * (BNx + 1) * sizeof(float);
     // 1-D grid, tile order remapped XCD-aware inside the kernel
     dim3 grid((unsigned)(((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.ks * a.pt.nphase));
     dim3 block(64 * p.wk);
     const int code = (p.tm - 1) * 2 + (p.tn - 1);
-#define LDM_CASE(WK, C, TM, TN) \
-    case WK * 10 + C: hipLaunchKernelGGL((conv_mfma_kernel<KIND, TM, TN, WK, NT>), grid, block, lds, st, a); break;
+#define LDM_CASE(WK, C, TM, TN)                                                                              \
+    case WK * 10 + C: {                                                                                      \
+        auto kfn = conv_mfma_kernel<KIND, TM, TN, WK, NT, NHWC>;                                            \
+        if (lds > 64 * 1024) {                                                                               \
+            static size_t opted = 0;                                                                         \
+            if (opted < lds) {                                                                               \
+                LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                (int)lds));                                                  \
+                opted = lds;                                                                                 \
+            }                                                                                                \
+        }                                                                                                    \
+        hipLaunchKernelGGL(kfn, grid, block, lds, st, a);                                                    \
+        break;                                                                                               \
+    }
     switch (p.wk * 10 + code) {
         LDM_CASE(1, 0, 1, 1) LDM_CASE(1, 1, 1, 2) LDM_CASE(1, 2, 2, 1) LDM_CASE(1, 3, 2, 2)
         LDM_CASE(2, 0, 1, 1) LDM_CASE(2, 1, 1, 2) LDM_CASE(2, 2, 2, 1) LDM_CASE(2, 3, 2, 2)
@@ -952,19 +1004,19 @@ static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq,
     return 0;
 }
 
-template <int KIND>
+template <int KIND, bool NHWC>
 static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     int maxtap = 0;
     for (int i = 0; i < a.pt.nphase; ++i) maxtap = std::max(maxtap, a.pt.ntap[i]);
     // NT = 4 <=> the 4-phase kernels (kMaxTap per phase of a stride-2 transposed conv with k <= 4 is 4)
     if (a.pt.nphase == 4) {
         if (maxtap > 4) return fail(3, "conv: 4-phase layer with more than 4 taps per phase");
-        return launch_mfma_nt<KIND, 4>(a, p, Nq, st);
+        return launch_mfma_nt<KIND, 4, NHWC>(a, p, Nq, st);
     }
     if (a.pt.nphase != 1) return fail(3, "conv: unsupported phase count");
-    if (maxtap <= 1) return launch_mfma_nt<KIND, 1>(a, p, Nq, st);
-    if (maxtap <= 9) return launch_mfma_nt<KIND, 9>(a, p, Nq, st);
-    return launch_mfma_nt<KIND, 16>(a, p, Nq, st);
+    if (maxtap <= 1) return launch_mfma_nt<KIND, 1, NHWC>(a, p, Nq, st);
+    if (maxtap <= 9) return launch_mfma_nt<KIND, 9, NHWC>(a, p, Nq, st);
+    return launch_mfma_nt<KIND, 16, NHWC>(a, p, Nq, st);
 }
 
 namespace ldm {
@@ -984,6 +1036,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     LDM_REQUIRE(!a.ep.bn_w || (a.ep.bn_b && a.ep.bn_m && a.ep.bn_v), "conv: incomplete BatchNorm parameters");
     const int64_t Nq = (int64_t)d.B * a.pt.Hq * a.pt.Wq;
     if (p.kind == 0) {
+        LDM_REQUIRE(d.layout == 0, "conv: the direct kernel supports NCHW tensors only");
         const int64_t total = (int64_t)d.B * d.Cout * d.Hout * d.Wout;
         hipLaunchKernelGGL(conv_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
         LDM_CHECK_LAUNCH("conv_direct_kernel");
@@ -1001,7 +1054,9 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     LDM_REQUIRE((int64_t)d.B * d.Cin * d.Hin * d.Win * 4 < 0x7ff00000LL &&
                     p.packed_floats * 4 < 0x7ff00000LL && (int64_t)d.B * d.Cout * d.Hout * d.Wout * 4 < 0x7ff00000LL,
                 "conv forward: tensor too large for 32-bit buffer offsets (split the batch)");
-    return p.kind == 1 ? launch_mfma<1>(a, p, Nq, st) : launch_mfma<2>(a, p, Nq, st);
+    const bool in_nhwc = d.layout & 1;
+    if (p.kind == 1) return in_nhwc ? launch_mfma<1, true>(a, p, Nq, st) : launch_mfma<1, false>(a, p, Nq, st);
+    return in_nhwc ? launch_mfma<2, true>(a, p, Nq, st) : launch_mfma<2, false>(a, p, Nq, st);
 }
 
 }  // namespace ldm

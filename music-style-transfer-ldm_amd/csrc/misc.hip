@@ -151,7 +151,8 @@ struct AMfma<2> {
 // Compile-time padded sizes LP x SP and head dim D (instances in ldm_attention_core); the actual L, S
 // (<= LP, SP) are runtime and masked.  All index math folds to shifts.
 // Each block owns LT query rows of one (b, head): grid = B * heads * (LP / LT).
-template <int KIND, int LP, int SP, int D, int LT>
+// TOK: q and out are token-major [B,L,E] (the UNet engine's NHWC activations) instead of [B,E,L].
+template <int KIND, int LP, int SP, int D, int LT, bool TOK>
 __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                              float* __restrict__ out, int E, int heads, int L, int S,
                                                              float scale) {
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane % TILE, lg = lane / TILE;
-    const float* qb = q + ((size_t)b * E + (size_t)h * D) * L;
+    const float* qb = TOK ? q + (size_t)b * L * E + (size_t)h * D : q + ((size_t)b * E + (size_t)h * D) * L;
+    const int qcs = TOK ? 1 : L, qls = TOK ? E : 1;   // q element (c, l) at qb[c*qcs + l*qls]
     const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
     const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
 
@@ -204,14 +206,14 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         typename MF::acc_t acc;
 #pragma unroll
         for (int r = 0; r < MF::NACC; ++r) acc[r] = 0.f;
-        const float* qp = qb + lg * L + (lok ? l : 0);
+        const float* qp = qb + lg * qcs + (lok ? l : 0) * qls;
         const float* kp = kb + lg * S + (sok ? s : 0);
 #pragma unroll
         for (int k0 = 0; k0 < D; k0 += KBQ * NLG) {
             float av[KBQ], bv[KBQ];
 #pragma unroll
             for (int j = 0; j < KBQ; ++j) {   // the whole batch in flight before its MFMAs
-                av[j] = qp[(k0 + NLG * j) * L];
+                av[j] = qp[(k0 + NLG * j) * qcs];
                 bv[j] = kp[(k0 + NLG * j) * S];
             }
 #pragma unroll
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     __syncthreads();
     // O[c][l] = sum_s V[c][s] P[l][s]
     constexpr int NTC = D / TILE;
-    float* ob = out + ((size_t)b * E + (size_t)h * D) * L;
+    float* ob = TOK ? out + (size_t)b * L * E + (size_t)h * D : out + ((size_t)b * E + (size_t)h * D) * L;
     for (int tile = wave; tile < NTC * NTL; tile += 4) {
         const int ct = tile / NTL, lt = tile % NTL;
         typename MF::acc_t acc;
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         const int l = l0 + lt * TILE + col;
         if (l < L) {
 #pragma unroll
-            for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * L + l] = acc[r];
+            for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * qcs + l * qls] = acc[r];
         }
     }
 }
@@ -526,20 +528,24 @@ extern "C" int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B
     return 0;
 }
 
-extern "C" int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
-                                  int32_t L, int32_t S, float scale, void* stream) {
+namespace ldm {
+int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads, int32_t L,
+                      int32_t S, float scale, bool tok, hipStream_t st) {
     LDM_REQUIRE(q && kv && out, "attention: null argument");
     LDM_REQUIRE(B > 0 && heads > 0 && E % heads == 0 && L > 0 && S > 0, "attention: bad shape");
     const int d = E / heads;
     {
         // compile-time instances covering the UNet's maps (128x512 mel: L=64 / 16; 128x128: 16 / 4)
-        hipStream_t st = (hipStream_t)stream;
         const dim3 blk(256);
 #define LDM_ATT(KIND, LP, SP, D, LT)                                                                      \
     if (d == D && L <= LP && S <= SP) {                                                                   \
         const size_t lds = ((size_t)LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);              \
-        hipLaunchKernelGGL((attention_mfma_kernel<KIND, LP, SP, D, LT>), dim3(B * heads * (LP / LT)), blk, lds, st, \
-                           q, kv, out, E, heads, L, S, scale);                                            \
+        if (tok)                                                                                          \
+            hipLaunchKernelGGL((attention_mfma_kernel<KIND, LP, SP, D, LT, true>), dim3(B * heads * (LP / LT)), blk, \
+                               lds, st, q, kv, out, E, heads, L, S, scale);                               \
+        else                                                                                              \
+            hipLaunchKernelGGL((attention_mfma_kernel<KIND, LP, SP, D, LT, false>), dim3(B * heads * (LP / LT)), \
+                               blk, lds, st, q, kv, out, E, heads, L, S, scale);                          \
         LDM_CHECK_LAUNCH("attention_mfma_kernel");                                                        \
         return 0;                                                                                         \
     }
@@ -552,13 +558,20 @@ extern "C" int ldm_attention_core(const float* q, const float* kv, float* out, i
 #undef LDM_ATT
     }
     // generic VALU fallback (head dims not a multiple of the MFMA tile)
+    LDM_REQUIRE(!tok, "attention: token-major layout needs an MFMA instance for this head size");
     const size_t lds = ((size_t)d * kAttnLT + 2 * (size_t)d * S + (size_t)kAttnLT * S) * sizeof(float);
     LDM_REQUIRE(lds <= 64 * 1024, "attention: head tile exceeds LDS budget");
     const int ltiles = (L + kAttnLT - 1) / kAttnLT;
-    hipLaunchKernelGGL(attention_core_kernel, dim3(B * heads * ltiles), dim3(256), lds, (hipStream_t)stream, q, kv, out,
-                       E, heads, L, S, scale);
+    hipLaunchKernelGGL(attention_core_kernel, dim3(B * heads * ltiles), dim3(256), lds, st, q, kv, out, E, heads, L, S,
+                       scale);
     LDM_CHECK_LAUNCH("attention_core_kernel");
     return 0;
+}
+}  // namespace ldm
+
+extern "C" int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
+                                  int32_t L, int32_t S, float scale, void* stream) {
+    return ldm::attention_core_ex(q, kv, out, B, E, heads, L, S, scale, false, (hipStream_t)stream);
 }
 
 extern "C" int ldm_q_sample(const float* x0, const float* eps, const float* coef_table, int32_t T, const int64_t* t,

@@ -78,6 +78,16 @@ static int layer_desc(const ldm_unet_shape& s, int layer, ldm_conv_desc& d) {
         case 14: proj(512, 512, L1); break;
         default: return fail(2, "unet: layer index out of range");
     }
+    // Activation layouts inside the UNet: everything between the latent input (NCHW, read by enc1)
+    // and the noise prediction (NCHW, written by dec1) is NHWC, so each K-chunk of an implicit-GEMM
+    // operand is one 16-byte load per lane; the style-map K/V projections read the NCHW style maps and
+    // stay channel-major (the attention reads K/V that way); q and the attention output are token-major.
+    switch (layer) {
+        case 0: d.layout = 2; break;           // z (NCHW) -> z1 (NHWC)
+        case 8: d.layout = 1; break;           // d2 (NHWC) -> eps / fused update (NCHW)
+        case 10: case 13: d.layout = 0; break; // s5 / s6 -> kv (channel-major)
+        default: d.layout = 3; break;
+    }
     return 0;
 }
 
@@ -200,12 +210,12 @@ static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, cons
     // z3 = cross_attention2(z3, s5)                                              (model.py:211)
     if (!kv_ready) LDM_TRY(style_kv(s, w, s5, s6, ws, st));
     LDM_TRY(conv_call(s, ws.convws, 9, w.ca_plan_q[0], ws.z3, w.ca_wq[0], w.ca_bq[0], 0, nullptr, nullptr, ws.q2, st));
-    LDM_TRY(ldm_attention_core(ws.q2, ws.kv2, ws.a2, s.B, 256, 4, L2, L2, (float)std::sqrt(1.0 / 64.0), st));
+    LDM_TRY(attention_core_ex(ws.q2, ws.kv2, ws.a2, s.B, 256, 4, L2, L2, (float)std::sqrt(1.0 / 64.0), true, st));
     LDM_TRY(conv_call(s, ws.convws, 11, w.ca_plan_o[0], ws.a2, w.ca_wo[0], w.ca_bo[0], 0, nullptr, nullptr, ws.c2, st));
     // z4 = relu(enc4(z3)); z4 = cross_attention1(z4, s6)                         (model.py:212-214)
     LDM_TRY(conv_call(s, ws.convws, 3, w.conv_plan[3], ws.c2, w.conv_w[3], w.conv_b[3], LDM_ACT_RELU, nullptr, nullptr, ws.z4, st));
     LDM_TRY(conv_call(s, ws.convws, 12, w.ca_plan_q[1], ws.z4, w.ca_wq[1], w.ca_bq[1], 0, nullptr, nullptr, ws.q1, st));
-    LDM_TRY(ldm_attention_core(ws.q1, ws.kv1, ws.a1, s.B, 512, 4, L1, L1, (float)std::sqrt(1.0 / 128.0), st));
+    LDM_TRY(attention_core_ex(ws.q1, ws.kv1, ws.a1, s.B, 512, 4, L1, L1, (float)std::sqrt(1.0 / 128.0), true, st));
     LDM_TRY(conv_call(s, ws.convws, 14, w.ca_plan_o[1], ws.a1, w.ca_wo[1], w.ca_bo[1], 0, nullptr, nullptr, ws.c1, st));
     // bottleneck + decoder with skips (ReLU before the add)                     (model.py:217-229)
     LDM_TRY(conv_call(s, ws.convws, 4, w.conv_plan[4], ws.c1, w.conv_w[4], w.conv_b[4], LDM_ACT_RELU, nullptr, nullptr, ws.zb, st));

@@ -24,7 +24,8 @@ c_fp = ctypes.c_void_p  # device float* as raw address
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in
-                ("B", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kh", "kw", "stride", "pad", "out_pad", "transposed")]
+                ("B", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kh", "kw", "stride", "pad", "out_pad", "transposed",
+                 "layout")]
 
     def key(self):
         return tuple(getattr(self, f[0]) for f in self._fields_)

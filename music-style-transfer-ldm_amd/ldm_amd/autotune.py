@@ -27,7 +27,9 @@ def _tiles(desc, kind, tm, tn):
 
 def candidates(desc, min_waves=256, max_waves=16384):
     """Valid (kind, tm, tn, wk, ks) plans whose grid holds between min_waves and max_waves waves."""
-    out = [(0, 1, 1, 1, 1)] if desc.Cout <= 64 else []
+    out = []
+    if desc.Cout <= 64 and desc.layout == 0:
+        out.append((0, 1, 1, 1, 1))
     for kind in (1, 2):
         for tm in (1, 2):
             for tn in (1, 2):
