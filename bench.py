@@ -129,6 +129,17 @@ def time_layers(engine, shape, dev, reps=50):
         by = 4.0 * shape.B * 4 * E * Lt
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
                      "flops": fl, "bytes": by}
+        # the reverse loop's folded form: scores from the projection input z against scale*Wq^T K
+        z = torch.randn(shape.B, Lt, E, device=dev)
+        kf = torch.randn(shape.B, 4, E, Lt, device=dev)
+        bf = torch.randn(shape.B, 4, Lt, device=dev)
+        us = _graph_time_us(lambda: lib.ldm_attention_folded(z.data_ptr(), kv.data_ptr(), kf.data_ptr(), bf.data_ptr(),
+                                                             o.data_ptr(), shape.B, E, 4, Lt, Lt,
+                                                             torch.cuda.current_stream().cuda_stream), reps)
+        fl = 2.0 * shape.B * 4 * Lt * Lt * E + 2.0 * shape.B * E * Lt * Lt
+        by = 4.0 * shape.B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
+        out[name + "f"] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
+                           "flops": fl, "bytes": by}
     return out
 
 

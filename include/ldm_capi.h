@@ -124,6 +124,22 @@ int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B, int32_t d
  * q [B,E,L] (the Q in-projection output in NCHW token order), kv [B,2E,S] (K channels then V
  * channels), out [B,E,L] = softmax((q*scale)^T k) v per head, written channel-major so the
  * out-projection reads it as NCHW (the reference's two permutes, model.py:144-158, vanish). */
+/* Folded-query form for a fixed key set (the reverse loop's style maps): kf [B,heads,E,S] =
+ * scale * Wq_h^T K_h, bf [B,heads,S] = scale * bq_h^T K_h from kv [B,2E,S] and the Q in-projection
+ * (wq [E,E] torch layout, bq [E]); ldm_attention_folded then takes the projection's input z [B,L,E]
+ * (token-major) and writes out [B,L,E] (token-major) = the same attention as q = Wq z + bq.
+ * Replaces the Q in-projection + score product of nn.MultiheadAttention (model.py:153). */
+int ldm_attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
+                            int32_t S, float scale, float* kf, float* bf, void* stream);
+int ldm_attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out, int32_t B,
+                         int32_t E, int32_t heads, int32_t L, int32_t S, void* stream);
+/* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
+ * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
+ * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that
+ * fall inside the input (padding taps see zeros).  Used for out_proj -> enc4 / bottleneck
+ * (model.py:155-160 then :212 / :217) in the reverse loop. */
+int ldm_fold_conv_proj(const ldm_conv_desc* d, const float* w_conv, const float* b_conv, const float* w_proj,
+                       const float* b_proj, int32_t Cmid, float* w_out, float* pos_bias_out, void* stream);
 int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
                        int32_t L, int32_t S, float scale, void* stream);
 
@@ -181,6 +197,14 @@ typedef struct ldm_unet_weights {
     const float* t_b1;
     const float* t_w2;
     const float* t_b2;
+    /* Re-associated forms used by the reverse loop when use_fold != 0 (ldm_fold_conv_proj,
+     * ldm_attention_fold_keys): raw Q in-projection rows (in_proj_weight[:E], torch layout) of both
+     * cross-attentions, and enc4 / bottleneck composed with the preceding out-projection
+     * (packed with conv_plan[3] / conv_plan[4]) plus their position-dependent biases [Cout,Hout,Wout]. */
+    const float* ca_wq_raw[2];
+    const float* fold_w[2];
+    const float* fold_pb[2];
+    int32_t use_fold;
 } ldm_unet_weights;
 
 typedef struct ldm_unet_shape {

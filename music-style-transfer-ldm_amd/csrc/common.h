@@ -99,6 +99,8 @@ struct EpiArgs {
     const float* bn_v;
     float bn_eps;
     int32_t act;
+    const float* pos_bias;   // [Cout, Hout, Wout] added in place of `bias` (a projection folded into the
+                             // conv, whose bias reaches each output through the taps inside the window)
     const float* bcast;
     const float* skip;
     float* act_out;   // post-activation value before the adds (training), or NULL
@@ -120,6 +122,11 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
 // kv is always channel-major [B,2E,S].
 int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads, int32_t L,
                       int32_t S, float scale, bool tok, hipStream_t st);
+
+int attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out, int32_t B,
+                     int32_t E, int32_t heads, int32_t L, int32_t S, hipStream_t st);
+int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
+                        int32_t S, float scale, float* kf, float* bf, hipStream_t st);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.

@@ -198,10 +198,10 @@ struct EpiPre {
     float bias, bcast, skip, x;
 };
 
-__device__ __forceinline__ EpiPre epi_prefetch(const ConvArgs& a, int m, int b, size_t oidx) {
+__device__ __forceinline__ EpiPre epi_prefetch(const ConvArgs& a, int m, int b, size_t oidx, int pix) {
     const EpiArgs& e = a.ep;
     EpiPre p;
-    p.bias = e.bias ? e.bias[m] : 0.f;
+    p.bias = e.pos_bias ? e.pos_bias[m * a.Hout * a.Wout + pix] : (e.bias ? e.bias[m] : 0.f);
     p.bcast = e.bcast ? e.bcast[(size_t)b * a.Cout + m] : 0.f;
     p.skip = e.skip ? e.skip[oidx] : 0.f;
     p.x = e.ddim_coef ? e.ddim_x[oidx] : 0.f;
@@ -224,16 +224,17 @@ __device__ __forceinline__ EpiSrc epi_sources(const ConvArgs& a, bool live) {
     const EpiArgs& e = a.ep;
     const int ybytes = live ? a.B * a.Cout * a.Hout * a.Wout * 4 : 0;
     EpiSrc s;
-    s.bias = opt_rsrc(e.bias, live ? a.Cout * 4 : 0);
+    s.bias = e.pos_bias ? opt_rsrc(e.pos_bias, live ? a.Cout * a.Hout * a.Wout * 4 : 0)
+                        : opt_rsrc(e.bias, live ? a.Cout * 4 : 0);
     s.bcast = opt_rsrc(e.bcast, live ? a.B * a.Cout * 4 : 0);
     s.skip = opt_rsrc(e.skip, ybytes);
     s.x = opt_rsrc(e.ddim_coef ? e.ddim_x : nullptr, ybytes);
     return s;
 }
 
-__device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, int m, int b, int oidx) {
+__device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, int m, int b, int oidx, int boff) {
     EpiPre p;
-    p.bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bias, m * 4, 0, 0));
+    p.bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bias, boff, 0, 0));
     p.bcast = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bcast, (b * Cout + m) * 4, 0, 0));
     p.skip = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.skip, oidx * 4, 0, 0));
     p.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.x, oidx * 4, 0, 0));
@@ -242,7 +243,7 @@ __device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, in
 
 __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx, float v, const EpiPre& p) {
     const EpiArgs& e = a.ep;
-    if (e.bias) v = v + p.bias;
+    if (e.bias || e.pos_bias) v = v + p.bias;
     if (e.bn_w) {
         // aten batch_norm_cpu_collect_linear_and_constant_terms: alpha = invstd*w, beta = b - mean*alpha
         const float invstd = 1.0f / sqrtf(e.bn_v[m] + e.bn_eps);
@@ -271,7 +272,7 @@ __device__ __forceinline__ int out_index(const ConvArgs& a, int m, int b, int oy
 
 __device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, int oy, int ox, float v) {
     const size_t oidx = out_index(a, m, b, oy, ox);
-    epi_finish(a, m, oidx, v, epi_prefetch(a, m, b, oidx));
+    epi_finish(a, m, oidx, v, epi_prefetch(a, m, b, oidx, oy * a.Wout + ox));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -495,7 +496,8 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
                 const int qxx = r - qyy * a.pt.Wq;
                 const int oy = qyy * a.pt.osy + ph_ry, ox = qxx * a.pt.osy + ph_rx;
                 const int oidx = out_index(a, mm, b, oy, ox);
-                pre[k] = epi_prefetch_buf(esrc, a.Cout, mm, b, oidx);
+                const int boff = (a.ep.pos_bias ? mm * a.Hout * a.Wout + oy * a.Wout + ox : mm) * 4;
+                pre[k] = epi_prefetch_buf(esrc, a.Cout, mm, b, oidx, boff);
                 po[k] = valid ? oidx : -1;
                 pm[k] = mm;
                 ps[k] = mloc * LDB + nloc;

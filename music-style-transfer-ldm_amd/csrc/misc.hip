@@ -152,22 +152,29 @@ struct AMfma<2> {
 // (<= LP, SP) are runtime and masked.  All index math folds to shifts.
 // Each block owns LT query rows of one (b, head): grid = B * heads * (LP / LT).
 // TOK: q and out are token-major [B,L,E] (the UNet engine's NHWC activations) instead of [B,E,L].
-template <int KIND, int LP, int SP, int D, int LT, bool TOK>
+// EQ > 0 (folded query projection, token-major only): `q` is the projection's INPUT z [B,L,E=EQ] and
+// the scores are z^T kf[b,h] + bf[b,h] with kf [B,heads,E,S] = scale*Wq_h^T K_h and bf [B,heads,S] =
+// scale*bq_h^T K_h (ldm_attention_fold_keys) — the same scores as ((Wq z + bq)*scale)^T K re-associated,
+// so the Q in-projection needs no launch of its own.
+template <int KIND, int LP, int SP, int D, int LT, bool TOK, int EQ = 0>
 __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                              float* __restrict__ out, int E, int heads, int L, int S,
-                                                             float scale) {
+                                                             float scale, const float* __restrict__ kf = nullptr,
+                                                             const float* __restrict__ bf = nullptr) {
     using MF = AMfma<KIND>;
     constexpr int TILE = MF::TILE, NLG = MF::NLG;
     static_assert(LT % TILE == 0 && LP % LT == 0, "query split");
-    constexpr int KBQ = D / NLG < 16 ? D / NLG : 16;     // k-steps per register batch (QK^T)
+    static_assert(EQ == 0 || TOK, "folded queries are token-major");
+    constexpr int DQ = EQ ? EQ : D;                       // contraction length of the scores
+    constexpr int KBQ = DQ / NLG < 16 ? DQ / NLG : 16;   // k-steps per register batch (QK^T)
     constexpr int KBP = SP / NLG < 16 ? SP / NLG : 16;    // (PV)
-    static_assert(LP % TILE == 0 && SP % TILE == 0 && D % TILE == 0 && D % (KBQ * NLG) == 0 &&
+    static_assert(LP % TILE == 0 && SP % TILE == 0 && D % TILE == 0 && DQ % (KBQ * NLG) == 0 &&
                       SP % (KBP * NLG) == 0 && SP <= 64 * 64,
                   "attention instance shape");
     constexpr int LDP = SP + 1;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* Ps = sm;               // [LT][SP+1]  (rows l0 .. l0+LT-1)
-    float* Vs = sm + LT * LDP;    // [D][SP+1]
+    float* Ps = sm;                                // [LT][SP+1]  (rows l0 .. l0+LT-1); folded: 4 slabs
+    float* Vs = sm + (EQ > 0 ? 4 : 1) * LT * LDP;  // [D][SP+1]
     constexpr int NSPLIT = LP / LT;
     const int l0 = (blockIdx.x % NSPLIT) * LT;
     const int bh = blockIdx.x / NSPLIT;
@@ -175,9 +182,10 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane % TILE, lg = lane / TILE;
-    const float* qb = TOK ? q + (size_t)b * L * E + (size_t)h * D : q + ((size_t)b * E + (size_t)h * D) * L;
+    const float* qb = EQ ? q + (size_t)b * L * E
+                         : (TOK ? q + (size_t)b * L * E + (size_t)h * D : q + ((size_t)b * E + (size_t)h * D) * L);
     const int qcs = TOK ? 1 : L, qls = TOK ? E : 1;   // q element (c, l) at qb[c*qcs + l*qls]
-    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
+    const float* kb = EQ ? kf + (size_t)(b * heads + h) * E * S : kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
     const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
 
     // stage V [D][S] -> LDS [D][SP+1]: every load of this thread issues before any LDS store
@@ -197,9 +205,45 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
             if (e < D * SP) Vs[c * LDP + s] = s < S ? v[u] : 0.f;
         }
     }
-    // S = (q*scale)^T k for this block's LT rows: tiles round-robin over the 4 waves
     constexpr int NTL = LT / TILE, NTS = SP / TILE;
-    for (int tile = wave; tile < NTL * NTS; tile += 4) {
+    if constexpr (EQ > 0) {
+        // Folded scores z^T kf: the E-long contraction is split over the 4 waves (each covers every tile
+        // of the block over E/4, all of its operand loads in flight at once — a single memory round
+        // trip), partial tiles go to 4 LDS slabs and the softmax pass below sums them in wave order.
+        constexpr int NSTEP = DQ / 4 / NLG;
+        static_assert(DQ % (4 * NLG) == 0 && NTL * NSTEP + NTS * NSTEP <= 96, "folded score tile too large");
+        const int kbase = wave * (DQ / 4);
+        float av[NTL][NSTEP], bv[NTS][NSTEP];
+#pragma unroll
+        for (int lt = 0; lt < NTL; ++lt) {
+            const int l = l0 + lt * TILE + col;
+            const float* zp = qb + (size_t)(l < L ? l : 0) * E + kbase + lg;
+#pragma unroll
+            for (int j = 0; j < NSTEP; ++j) av[lt][j] = l < L ? zp[NLG * j] : 0.f;
+        }
+#pragma unroll
+        for (int st = 0; st < NTS; ++st) {
+            const int s = st * TILE + col;
+            const float* kp = kb + (size_t)(kbase + lg) * S + (s < S ? s : 0);
+#pragma unroll
+            for (int j = 0; j < NSTEP; ++j) bv[st][j] = s < S ? kp[(size_t)NLG * j * S] : 0.f;
+        }
+        float* Pw = Ps + (size_t)wave * LT * LDP;
+#pragma unroll
+        for (int lt = 0; lt < NTL; ++lt)
+#pragma unroll
+            for (int st = 0; st < NTS; ++st) {
+                typename MF::acc_t acc;
+#pragma unroll
+                for (int r = 0; r < MF::NACC; ++r) acc[r] = 0.f;
+#pragma unroll
+                for (int j = 0; j < NSTEP; ++j) acc = MF::mma(av[lt][j], bv[st][j], acc);
+#pragma unroll
+                for (int r = 0; r < MF::NACC; ++r) Pw[(lt * TILE + MF::row(r, lg)) * LDP + st * TILE + col] = acc[r];
+            }
+    }
+    // S = (q*scale)^T k for this block's LT rows: tiles round-robin over the 4 waves
+    for (int tile = wave; tile < (EQ > 0 ? 0 : NTL * NTS); tile += 4) {
         const int lt = tile / NTS, st = tile % NTS;
         const int l = l0 + lt * TILE + col, s = st * TILE + col;
         const bool lok = l < L, sok = s < S;
@@ -209,7 +253,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         const float* qp = qb + lg * qcs + (lok ? l : 0) * qls;
         const float* kp = kb + lg * S + (sok ? s : 0);
 #pragma unroll
-        for (int k0 = 0; k0 < D; k0 += KBQ * NLG) {
+        for (int k0 = 0; k0 < DQ; k0 += KBQ * NLG) {
             float av[KBQ], bv[KBQ];
 #pragma unroll
             for (int j = 0; j < KBQ; ++j) {   // the whole batch in flight before its MFMAs
@@ -217,9 +261,12 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
                 bv[j] = kp[(k0 + NLG * j) * S];
             }
 #pragma unroll
-            for (int j = 0; j < KBQ; ++j)
-                acc = MF::mma(lok ? av[j] * scale : 0.f, sok ? bv[j] : 0.f, acc);   // q_scaled = q * sqrt(1/d)
+            for (int j = 0; j < KBQ; ++j) {
+                if constexpr (EQ) acc = MF::mma(lok ? av[j] : 0.f, sok ? bv[j] : 0.f, acc);
+                else acc = MF::mma(lok ? av[j] * scale : 0.f, sok ? bv[j] : 0.f, acc);   // q_scaled = q * sqrt(1/d)
+            }
         }
+
 #pragma unroll
         for (int r = 0; r < MF::NACC; ++r) Ps[(lt * TILE + MF::row(r, lg)) * LDP + st * TILE + col] = acc[r];
     }
@@ -237,7 +284,14 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
 #pragma unroll
             for (int u = 0; u < SP / SEG; ++u) {
                 const int s = s0 + u * SEG;
-                x[u] = row[s];
+                if constexpr (EQ > 0) {   // sum the 4 wave slabs in wave order, then the folded bias
+                    float v = row[s];
+#pragma unroll
+                    for (int w = 1; w < 4; ++w) v = v + row[s + w * LT * LDP];
+                    x[u] = v + (s < S ? bf[(size_t)(b * heads + h) * S + s] : 0.f);
+                } else {
+                    x[u] = row[s];
+                }
                 if (s < S) mx = fmaxf(mx, x[u]);
             }
 #pragma unroll
@@ -282,6 +336,80 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
 #pragma unroll
             for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * qcs + l * qls] = acc[r];
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Folds for the reverse loop (style fixed over the loop, weights fixed between optimiser steps).
+// ------------------------------------------------------------------------------------------------
+// kf[b,h,e,s] = scale * sum_c Wq[h*d+c, e] K[b, h*d+c, s];  bf[b,h,s] = scale * sum_c bq[h*d+c] K[b,h*d+c,s]
+// (fp64 accumulation, one rounding to fp32).  kv [B,2E,S] channel-major; wq [E,E] torch Linear layout.
+__global__ __launch_bounds__(256) void attention_fold_keys_kernel(const float* __restrict__ kv, const float* __restrict__ wq,
+                                                                  const float* __restrict__ bq, int B, int E, int heads,
+                                                                  int S, float scale, float* __restrict__ kf,
+                                                                  float* __restrict__ bf) {
+    const int d = E / heads;
+    const int64_t nk = (int64_t)B * heads * E * S;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < nk) {
+        const int s = (int)(idx % S);
+        int64_t r = idx / S;
+        const int e = (int)(r % E);
+        r /= E;
+        const int h = (int)(r % heads), b = (int)(r / heads);
+        const float* kr = kv + ((int64_t)b * 2 * E + (int64_t)h * d) * S + s;
+        const float* wr = wq + (int64_t)h * d * E + e;
+        double acc = 0.0;
+        for (int c = 0; c < d; ++c) acc += (double)wr[(int64_t)c * E] * (double)kr[(int64_t)c * S];
+        kf[idx] = (float)(acc * (double)scale);
+    } else if (idx < nk + (int64_t)B * heads * S) {
+        const int64_t j = idx - nk;
+        const int s = (int)(j % S);
+        const int bh = (int)(j / S);
+        const int h = bh % heads, b = bh / heads;
+        const float* kr = kv + ((int64_t)b * 2 * E + (int64_t)h * d) * S + s;
+        double acc = 0.0;
+        for (int c = 0; c < d; ++c) acc += (double)bq[h * d + c] * (double)kr[(int64_t)c * S];
+        bf[j] = (float)(acc * (double)scale);
+    }
+}
+
+// W'[co, ci, t] = sum_j Wc[co, j, t] Wp[j, ci]  (conv after a Linear/1x1 projection, composed), and the
+// projection bias pushed through the window: pb[co, oy, ox] = bc[co] + sum_{taps t inside the input}
+// sum_j Wc[co, j, t] bp[j].  fp64 accumulation, one rounding.
+__global__ __launch_bounds__(256) void fold_conv_proj_kernel(const float* __restrict__ wc, const float* __restrict__ bc,
+                                                             const float* __restrict__ wp, const float* __restrict__ bp,
+                                                             int Cout, int Cmid, int Cin, int kh, int kw, int stride,
+                                                             int pad, int Hin, int Win, int Hout, int Wout,
+                                                             float* __restrict__ w_out, float* __restrict__ pb_out) {
+    const int KK = kh * kw;
+    const int64_t nw = (int64_t)Cout * Cin * KK;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < nw) {
+        const int t = (int)(idx % KK);
+        const int64_t r = idx / KK;
+        const int ci = (int)(r % Cin), co = (int)(r / Cin);
+        const float* wr = wc + (int64_t)co * Cmid * KK + t;
+        double acc = 0.0;
+        for (int j = 0; j < Cmid; ++j) acc += (double)wr[(int64_t)j * KK] * (double)wp[(int64_t)j * Cin + ci];
+        w_out[idx] = (float)acc;
+    } else if (idx < nw + (int64_t)Cout * Hout * Wout) {
+        const int64_t p = idx - nw;
+        const int ox = (int)(p % Wout);
+        const int oy = (int)((p / Wout) % Hout);
+        const int co = (int)(p / ((int64_t)Hout * Wout));
+        double acc = bc ? (double)bc[co] : 0.0;
+        for (int ky = 0; ky < kh; ++ky) {
+            const int iy = oy * stride - pad + ky;
+            if (iy < 0 || iy >= Hin) continue;
+            for (int kx = 0; kx < kw; ++kx) {
+                const int ix = ox * stride - pad + kx;
+                if (ix < 0 || ix >= Win) continue;
+                const float* wr = wc + (int64_t)co * Cmid * KK + ky * kw + kx;
+                for (int j = 0; j < Cmid; ++j) acc += (double)wr[(int64_t)j * KK] * (double)bp[j];
+            }
+        }
+        pb_out[p] = (float)acc;
     }
 }
 
@@ -529,6 +657,39 @@ extern "C" int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B
 }
 
 namespace ldm {
+int attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out, int32_t B,
+                     int32_t E, int32_t heads, int32_t L, int32_t S, hipStream_t st) {
+    LDM_REQUIRE(z && kv && kf && bf && out, "attention (folded): null argument");
+    LDM_REQUIRE(B > 0 && heads == 4 && L > 0 && S > 0, "attention (folded): bad shape");
+    const int d = E / heads;
+    const dim3 blk(256);
+#define LDM_ATTF(LP, SP, D, LT, EQV)                                                                     \
+    if (d == D && E == EQV && L <= LP && S <= SP) {                                                      \
+        const size_t lds = ((size_t)4 * LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);         \
+        hipLaunchKernelGGL((attention_mfma_kernel<2, LP, SP, D, LT, true, EQV>), dim3(B * heads * (LP / LT)), blk, \
+                           lds, st, z, kv, out, E, heads, L, S, 1.0f, kf, bf);                           \
+        LDM_CHECK_LAUNCH("attention_mfma_kernel (folded)");                                              \
+        return 0;                                                                                        \
+    }
+    LDM_ATTF(16, 16, 128, 16, 512)
+    LDM_ATTF(64, 64, 64, 16, 256)
+    LDM_ATTF(32, 32, 64, 16, 256)
+    LDM_ATTF(32, 32, 128, 16, 512)
+    LDM_ATTF(16, 16, 64, 16, 256)
+#undef LDM_ATTF
+    return fail(3, "attention (folded): no instance for this shape");
+}
+
+int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
+                        int32_t S, float scale, float* kf, float* bf, hipStream_t st) {
+    LDM_REQUIRE(kv && wq && bq && kf && bf && B > 0 && heads > 0 && E % heads == 0 && S > 0, "fold keys: bad argument");
+    const int64_t n = (int64_t)B * heads * E * S + (int64_t)B * heads * S;
+    hipLaunchKernelGGL(attention_fold_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, kv, wq, bq, B,
+                       E, heads, S, scale, kf, bf);
+    LDM_CHECK_LAUNCH("attention_fold_keys_kernel");
+    return 0;
+}
+
 int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads, int32_t L,
                       int32_t S, float scale, bool tok, hipStream_t st) {
     LDM_REQUIRE(q && kv && out, "attention: null argument");
@@ -671,5 +832,27 @@ extern "C" int ldm_loss_backward(int32_t kind, const float* a, const float* b, i
     hipLaunchKernelGGL(loss_backward_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind, a, b, n,
                        grad_out, grad_a, grad_b);
     LDM_CHECK_LAUNCH("loss_backward_kernel");
+    return 0;
+}
+
+extern "C" int ldm_attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E,
+                                       int32_t heads, int32_t S, float scale, float* kf, float* bf, void* stream) {
+    return ldm::attention_fold_keys(kv, wq, bq, B, E, heads, S, scale, kf, bf, (hipStream_t)stream);
+}
+
+extern "C" int ldm_attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out,
+                                    int32_t B, int32_t E, int32_t heads, int32_t L, int32_t S, void* stream) {
+    return ldm::attention_folded(z, kv, kf, bf, out, B, E, heads, L, S, (hipStream_t)stream);
+}
+
+extern "C" int ldm_fold_conv_proj(const ldm_conv_desc* d, const float* w_conv, const float* b_conv, const float* w_proj,
+                                  const float* b_proj, int32_t Cmid, float* w_out, float* pos_bias_out, void* stream) {
+    LDM_REQUIRE(d && w_conv && w_proj && b_proj && w_out && pos_bias_out, "fold conv/proj: null argument");
+    LDM_REQUIRE(!d->transposed && d->kh * d->kw > 0 && Cmid > 0, "fold conv/proj: a plain conv after the projection");
+    const int64_t n = (int64_t)d->Cout * d->Cin * d->kh * d->kw + (int64_t)d->Cout * d->Hout * d->Wout;
+    hipLaunchKernelGGL(ldm::fold_conv_proj_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       w_conv, b_conv, w_proj, b_proj, d->Cout, Cmid, d->Cin, d->kh, d->kw, d->stride, d->pad, d->Hin,
+                       d->Win, d->Hout, d->Wout, w_out, pos_bias_out);
+    LDM_CHECK_LAUNCH("fold_conv_proj_kernel");
     return 0;
 }

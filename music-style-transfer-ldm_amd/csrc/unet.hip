@@ -93,6 +93,7 @@ static int layer_desc(const ldm_unet_shape& s, int layer, ldm_conv_desc& d) {
 
 struct UNetWs {
     float *convws, *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
+    float *kf2, *bf2, *kf1, *bf1;   // folded keys of both cross-attentions (reverse loop, use_fold)
     int64_t total;
 };
 
@@ -139,6 +140,10 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.d3 = take(B * 2 * nf * HW2);
     w.d2 = take(B * nf * HW);
     w.eps = take(B * (int64_t)s.C * HW);
+    w.kf2 = take(B * 4 * 256 * L2);
+    w.bf2 = take(B * 4 * L2);
+    w.kf1 = take(B * 4 * 512 * L1);
+    w.bf1 = take(B * 4 * L1);
     w.total = off;
     return w;
 }
@@ -154,12 +159,13 @@ struct DdimFuse {
 
 static int conv_call(const ldm_unet_shape& s, float* convws, int layer, const ldm_conv_plan& plan, const float* x, const float* w,
                      const float* bias, int act, const float* bcast, const float* skip, float* y, hipStream_t st,
-                     const DdimFuse* fuse = nullptr) {
+                     const DdimFuse* fuse = nullptr, const float* pos_bias = nullptr) {
     ldm_conv_desc d;
     int rc = layer_desc(s, layer, d);
     if (rc) return rc;
     EpiArgs ep{};
-    ep.bias = bias;
+    ep.bias = pos_bias ? nullptr : bias;
+    ep.pos_bias = pos_bias;
     ep.act = act;
     ep.bcast = bcast;
     ep.skip = skip;
@@ -227,6 +233,33 @@ static int unet_forward(const ldm_unet_shape& s, const ldm_unet_weights& w, cons
     return 0;
 }
 
+// The reverse loop's step with both cross-attentions re-associated (style and weights are fixed for the
+// whole loop): the Q in-projection folds into the keys (ldm_attention_fold_keys, once per loop) and the
+// out-projection into the following conv (ldm_fold_conv_proj, once per weight version).  11 launches per
+// step instead of 15; the same arithmetic up to fp32 re-association.
+static int unet_forward_folded(const ldm_unet_shape& s, const ldm_unet_weights& w, const float* z, const UNetWs& ws,
+                               hipStream_t st, const float* temb, const DdimFuse* fuse) {
+    const int HW = s.H * s.W;
+    const int L2 = HW / 16, L1 = HW / 64;
+    LDM_TRY(conv_call(s, ws.convws, 0, w.conv_plan[0], z, w.conv_w[0], w.conv_b[0], LDM_ACT_RELU, nullptr, nullptr, ws.z1, st));
+    LDM_TRY(conv_call(s, ws.convws, 1, w.conv_plan[1], ws.z1, w.conv_w[1], w.conv_b[1], LDM_ACT_RELU, temb, nullptr, ws.z2, st));
+    LDM_TRY(conv_call(s, ws.convws, 2, w.conv_plan[2], ws.z2, w.conv_w[2], w.conv_b[2], LDM_ACT_RELU, nullptr, nullptr, ws.z3, st));
+    // cross_attention2 then enc4 (model.py:211-212)
+    LDM_TRY(attention_folded(ws.z3, ws.kv2, ws.kf2, ws.bf2, ws.a2, s.B, 256, 4, L2, L2, st));
+    LDM_TRY(conv_call(s, ws.convws, 3, w.conv_plan[3], ws.a2, w.fold_w[0], nullptr, LDM_ACT_RELU, nullptr, nullptr, ws.z4, st,
+                      nullptr, w.fold_pb[0]));
+    // cross_attention1 then bottleneck (model.py:214-217)
+    LDM_TRY(attention_folded(ws.z4, ws.kv1, ws.kf1, ws.bf1, ws.a1, s.B, 512, 4, L1, L1, st));
+    LDM_TRY(conv_call(s, ws.convws, 4, w.conv_plan[4], ws.a1, w.fold_w[1], nullptr, LDM_ACT_RELU, nullptr, nullptr, ws.zb, st,
+                      nullptr, w.fold_pb[1]));
+    LDM_TRY(conv_call(s, ws.convws, 5, w.conv_plan[5], ws.zb, w.conv_w[5], w.conv_b[5], LDM_ACT_RELU, nullptr, ws.z3, ws.d4, st));
+    LDM_TRY(conv_call(s, ws.convws, 6, w.conv_plan[6], ws.d4, w.conv_w[6], w.conv_b[6], LDM_ACT_RELU, nullptr, ws.z2, ws.d3, st));
+    LDM_TRY(conv_call(s, ws.convws, 7, w.conv_plan[7], ws.d3, w.conv_w[7], w.conv_b[7], LDM_ACT_RELU, nullptr, ws.z1, ws.d2, st));
+    LDM_TRY(conv_call(s, ws.convws, 8, w.conv_plan[8], ws.d2, w.conv_w[8], w.conv_b[8], LDM_ACT_NONE, nullptr, nullptr, nullptr,
+                      st, fuse));
+    return 0;
+}
+
 }  // namespace ldm
 
 using namespace ldm;
@@ -282,6 +315,21 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
                                  temb_all, st));
     // Likewise the style maps' K/V projections (model.py:153 with kv = s5 / s6, fixed for the loop).
     LDM_TRY(style_kv(*s, *w, s5, s6, ws, st));
+    const int HW = s->H * s->W;
+    if (w->use_fold) {
+        LDM_REQUIRE(w->ca_wq_raw[0] && w->ca_wq_raw[1] && w->fold_w[0] && w->fold_w[1] && w->fold_pb[0] && w->fold_pb[1],
+                    "ddim_sample: use_fold needs the folded weights");
+        LDM_TRY(attention_fold_keys(ws.kv2, w->ca_wq_raw[0], w->ca_bq[0], s->B, 256, 4, HW / 16,
+                                    (float)std::sqrt(1.0 / 64.0), ws.kf2, ws.bf2, st));
+        LDM_TRY(attention_fold_keys(ws.kv1, w->ca_wq_raw[1], w->ca_bq[1], s->B, 512, 4, HW / 64,
+                                    (float)std::sqrt(1.0 / 128.0), ws.kf1, ws.bf1, st));
+        for (int i = 0; i < nsteps; ++i) {
+            DdimFuse fuse{coef_table + 4 * (size_t)i, eta, x, x0_logs ? x0_logs + (size_t)i * n : nullptr,
+                          eps_logs ? eps_logs + (size_t)i * n : nullptr};
+            LDM_TRY(unet_forward_folded(*s, *w, x, ws, st, temb_all + (size_t)i * s->B * 128, &fuse));
+        }
+        return 0;
+    }
     for (int i = 0; i < nsteps; ++i) {
         // noise_pred = unet(x, t, style_embedding)                                (model.py:439)
         // and, fused into dec1's epilogue, the x0 / direction / eta update and the two log clones

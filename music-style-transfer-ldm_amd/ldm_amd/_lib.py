@@ -53,7 +53,8 @@ class UNetWeights(ctypes.Structure):
                 ("ca_wq", c_fp * 2), ("ca_bq", c_fp * 2), ("ca_plan_q", ConvPlan * 2),
                 ("ca_wkv", c_fp * 2), ("ca_bkv", c_fp * 2), ("ca_plan_kv", ConvPlan * 2),
                 ("ca_wo", c_fp * 2), ("ca_bo", c_fp * 2), ("ca_plan_o", ConvPlan * 2),
-                ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp)]
+                ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp),
+                ("ca_wq_raw", c_fp * 2), ("fold_w", c_fp * 2), ("fold_pb", c_fp * 2), ("use_fold", c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
@@ -79,6 +80,11 @@ SIGNATURES = {
     "ldm_sinusoid_embed": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_vp]),
     "ldm_time_mlp_forward": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_attention_core": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_vp]),
+    "ldm_attention_fold_keys": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_float, c_fp, c_fp,
+                                          c_vp]),
+    "ldm_attention_folded": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                       c_vp]),
+    "ldm_fold_conv_proj": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_fp, c_int32, c_fp, c_fp, c_vp]),
     "ldm_q_sample": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_predict_start": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_sched_backward": (c_int32, [c_int32, c_fp, c_fp, c_int32, c_vp, c_fp, c_fp, c_int32, c_int64, c_vp]),

@@ -5,6 +5,7 @@ reverse loop is replayed from a captured hipGraph (torch.cuda.CUDAGraph on the s
 Host side only: it owns workspaces (torch allocations) and caches, never computes.
 """
 import ctypes
+import os
 
 import torch
 
@@ -19,8 +20,11 @@ _CONV_NAMES = ("enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "de
 class UNetEngine:
     """Runs `unet` (a models.model.UNet: reference parameter names / shapes) through libldm_amd."""
 
-    def __init__(self, unet):
+    def __init__(self, unet, fold=None):
         self.unet = unet
+        # Re-associated cross-attentions in the reverse loop (ldm_capi.h use_fold); LDM_AMD_FOLD=0 turns
+        # it off (A/B timing, parity of the literal form).
+        self.fold = (os.environ.get("LDM_AMD_FOLD", "1") != "0") if fold is None else bool(fold)
         self._bound = {}      # shape key -> (key of param versions, UNetWeights, keepalive)
         self._ws = {}         # (shape key, device) -> workspace tensor
         self._graphs = {}
@@ -51,7 +55,7 @@ class UNetEngine:
             if not p.is_contiguous():
                 raise RuntimeError("UNet parameters must be contiguous")
         vkey = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params) + \
-            tuple(sorted(ops._PLAN_OVERRIDE.items()))
+            tuple(sorted(ops._PLAN_OVERRIDE.items())) + (self.fold,)
         hit = self._bound.get(skey)
         if hit is not None and hit[0] == vkey:
             return hit[1]
@@ -100,6 +104,22 @@ class UNetEngine:
             w.ca_bq[j] = ipb.data_ptr()
             w.ca_bkv[j] = ipb.data_ptr() + E * 4
             w.ca_bo[j] = a.out_proj.bias.data_ptr()
+        if self.fold:
+            # enc4 o out_proj(CA2) and bottleneck o out_proj(CA1), packed with those layers' plans
+            for j, (layer, conv, ca) in enumerate(((3, u.enc4, u.cross_attention2), (4, u.bottleneck, u.cross_attention1))):
+                a = ca.multihead_attn
+                d = desc(layer)
+                wf = torch.empty_like(conv.weight)
+                pb = torch.empty((d.Cout, d.Hout, d.Wout), device=conv.weight.device, dtype=torch.float32)
+                L.call("ldm_fold_conv_proj", byref(d), conv.weight.data_ptr(), conv.bias.data_ptr(),
+                       a.out_proj.weight.data_ptr(), a.out_proj.bias.data_ptr(), a.embed_dim, wf.data_ptr(),
+                       pb.data_ptr(), ops.stream_handle())
+                buf = ops.packed_weight(wf, d, w.conv_plan[layer])
+                keep += [wf, pb, buf]
+                w.fold_w[j] = buf.data_ptr()
+                w.fold_pb[j] = pb.data_ptr()
+                w.ca_wq_raw[j] = a.in_proj_weight.data_ptr()
+            w.use_fold = 1
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)

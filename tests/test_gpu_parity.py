@@ -310,3 +310,33 @@ def test_split_k_plans(cuda, name):
             for i, y in enumerate(outs):
                 assert rel_err(npy(y), npy(refs[i % 3])) < 1e-5, (pl, i)
                 assert torch.equal(y, outs[i % 3]), (pl, i)
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 64), (3, 16, 32), (1, 16, 16)])
+def test_folded_reverse_loop_matches_literal(M, cuda, shape):
+    """The reverse loop with both cross-attentions re-associated (Q projection folded into the keys,
+    out-projection folded into enc4 / bottleneck) equals the literal per-op loop to fp32 rounding."""
+    from ldm_amd.engine import UNetEngine
+    B, H, W = shape
+    unet = M.UNet(32, 32, 64)
+    recipe.fill_module(unet, seed=100)
+    unet = unet.to(cuda)
+    fd = M.ForwardDiffusion(200)
+    times = torch.linspace(199, 0, 6).long()
+    coefs = fd.reverse_coefs(times).to(cuda)
+    x0 = T(recipe.normal((B, 32, H, W), 31), cuda)
+    s5 = T(recipe.uniform01((B, 256, H // 4, W // 4), 32), cuda)
+    s6 = T(recipe.uniform01((B, 512, H // 8, W // 8), 33), cuda)
+    tt = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(cuda)
+    outs, logs = [], []
+    with torch.no_grad():
+        for fold in (False, True):
+            eng = UNetEngine(unet, fold=fold)
+            x = x0.clone()
+            lg = (torch.empty((5, B, 32, H, W), device=cuda), torch.empty((5, B, 32, H, W), device=cuda))
+            eng.ddim_loop(x, s5, s6, tt, coefs, 0.0, *lg)
+            outs.append(x)
+            logs.append(lg)
+    torch.cuda.synchronize()
+    assert rel_err(npy(outs[1]), npy(outs[0])) < 1e-5
+    assert rel_err(npy(logs[1][1]), npy(logs[0][1])) < 1e-5
