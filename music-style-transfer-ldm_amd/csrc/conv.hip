@@ -316,8 +316,8 @@ struct Frag {
 // kGroup chunks per wave.
 // ------------------------------------------------------------------------------------------------
 #ifndef LDM_DIAG   // diagnostic builds only (timing experiments, never shipped): 4 = per-block phase
-#define LDM_DIAG 0 // timestamps (tools/stamp_probe.py)
-#endif
+#define LDM_DIAG 0 // timestamps (tools/stamp_probe.py); 8 = no K-loop operand loads (MFMAs on register
+#endif             // garbage: the kernel's cost without its operand traffic)
 #if (LDM_DIAG & 4)
 __device__ unsigned long long g_ldm_stamps[1 << 16][6];
 #define LDM_STAMP(k)                                                                               \
@@ -552,12 +552,21 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) voff[ni] = vtap[t_ld][ni];
 #pragma unroll
-            for (int mi = 0; mi < TM; ++mi)
-                f[q].a[mi] = __builtin_bit_cast(
-                    floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
+            for (int mi = 0; mi < TM; ++mi) {
+                if constexpr (LDM_DIAG & 8) {
+                    const float g0 = (float)(soff_a + mi) * 1e-30f;
+                    f[q].a[mi] = floatx4{g0, g0, g0, g0};
+                } else {
+                    f[q].a[mi] = __builtin_bit_cast(
+                        floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, a_voff + mi * TILE * CK * 4, soff_a, 0));
+                }
+            }
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) {
-                if constexpr (NHWC) {
+                if constexpr (LDM_DIAG & 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) f[q].b[ni][j] = (float)(voff[ni] + soff_b + j) * 1e-30f;
+                } else if constexpr (NHWC) {
                     const floatx4 v = __builtin_bit_cast(
                         floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, voff[ni], soff_b, 0));
 #pragma unroll
