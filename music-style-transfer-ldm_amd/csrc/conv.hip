@@ -26,12 +26,17 @@
 //   kind 2: v_mfma_f32_16x16x4_f32  lane l: A[l&15][k=l>>4], B[k=l>>4][l&15]; D row=4(l>>4)+r,            col=l&15
 // Within a K-chunk, lane group lg = lane/TILE holds k = NLG*j + lg for MFMA step j = 0..3 (NLG = 64/TILE).
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
 
 #pragma clang fp contract(off)
+
+#ifndef LDM_DIAG
+#define LDM_DIAG 0
+#endif
 
 namespace ldm {
 
@@ -243,6 +248,11 @@ __device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, in
 
 __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx, float v, const EpiPre& p) {
     const EpiArgs& e = a.ep;
+#if (LDM_DIAG & 32)   // diagnostic: minimal epilogue (bias + relu + store) to size the code-footprint cost
+    v = v + p.bias;
+    a.y[oidx] = v < 0.f ? 0.f : v;
+    return;
+#endif
     if (e.bias || e.pos_bias) v = v + p.bias;
     if (e.bn_w) {
         // aten batch_norm_cpu_collect_linear_and_constant_terms: alpha = invstd*w, beta = b - mean*alpha
@@ -510,11 +520,24 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // that could alias prefetched registers).
     // (taps generated arithmetically from the phase's (dy0, dx0, na, nb) — no table loads; slots past
     // na*nb are out of window)
-    int vtap[NT][TN];
-    {
-        const int dy0 = sel_phase<PH4>(a.pk.dy0, ph), dx0 = sel_phase<PH4>(a.pk.dx0, ph);
-        const int na = sel_phase<PH4>(a.pk.na, ph), nb = sel_phase<PH4>(a.pk.nb, ph);
-        const int sg = a.pk.sg, ntap = na * nb;
+#ifndef LDM_TAP_ARITH
+#define LDM_TAP_ARITH 1
+#endif
+    // tap t -> (dy, dx) = (dy0 + sg*ja, dx0 + sg*jb), (ja, jb) = divmod(t, nb), nb <= 4, t < 16
+    const int tp_dy0 = sel_phase<PH4>(a.pk.dy0, ph), tp_dx0 = sel_phase<PH4>(a.pk.dx0, ph);
+    const int tp_nb = sel_phase<PH4>(a.pk.nb, ph), tp_ntap = sel_phase<PH4>(a.pk.na, ph) * tp_nb;
+    const int tp_mul = uni((32 + tp_nb - 1) / tp_nb), tp_sg = a.pk.sg;
+    const int tp_win = a.Win, tp_hin = a.Hin;
+    auto tap_off = [&](int t, int ni) {   // per-lane byte offset of tap t for column ni (kOOB if padding)
+        const int ja = uni((t * tp_mul) >> 5), jb = uni(t - ja * tp_nb);
+        const int dy = uni(t < tp_ntap ? tp_dy0 + tp_sg * ja : -0x4000), dx = uni(tp_dx0 + tp_sg * jb);
+        const bool ok = (unsigned)(iy0[ni] + dy) < (unsigned)tp_hin && (unsigned)(ix0[ni] + dx) < (unsigned)tp_win;
+        return ok ? base4[ni] + (dy * tp_win + dx) * tap_mul : kOOB;
+    };
+    int vtap[LDM_TAP_ARITH ? 1 : NT][TN];
+    if constexpr (!LDM_TAP_ARITH) {
+        const int dy0 = tp_dy0, dx0 = tp_dx0, nb = tp_nb;
+        const int sg = a.pk.sg, ntap = tp_ntap;
         int ja = 0, jb = 0;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -537,20 +560,32 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     // by a wave-uniform branch (measured: the padding MFMAs of short K loops cost up to 1.6x the
     // useful ones).
     constexpr int kSkipA = 0x40000000;   // soffset past any packed weight buffer
-    const int c_last = uni(g + G * (nmine > 0 ? nmine - 1 : 0));
-    auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp) {
+    // K cursor of this wave (wave-uniform, SGPRs), advanced incrementally chunk by chunk in issue order:
+    // chunk c = g + G*i sits at tap t = c / cpt, channel chunk cc = c % cpt, packed-weight byte offset
+    // c * wstride_b.  (A per-chunk division and the liveness selects cost ~25 scalar instructions per
+    // chunk, issued in one block ahead of the group's MFMAs.)
+    int cur_t = uni(a.fd_cpt.div(g));
+    int cur_cc = uni(g - cur_t * cpt);
+    int cur_sa = uni(g * wstride_b);
+    const int adv_t = uni(G / cpt), adv_cc = uni(G - (G / cpt) * cpt), adv_sa = uni(G * wstride_b);
+    // ALL_LIVE: every chunk of the group is one of this wave's (no liveness selects, no clamping)
+    auto load = [&](Frag<TM, TN>(&f)[kGroup], int grp, auto all_live) {
+        constexpr bool ALL_LIVE = decltype(all_live)::value;
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-            const int i = grp * kGroup + q;
-            const bool live = i < nmine;
-            const int c = live ? g + G * i : c_last;
-            const int t_ld = uni(a.fd_cpt.div(c));
-            const int cc_ld = c - t_ld * cpt;
-            const int soff_a = uni(live ? c * wstride_b : kSkipA);
-            const int soff_b = uni(live ? cc_ld * cstep_b : kSkipA);
+            const bool live = ALL_LIVE || grp * kGroup + q < nmine;
+            const int t_ld = ALL_LIVE ? cur_t : uni(cur_t < NT - 1 ? cur_t : NT - 1);
+            const int soff_a = uni(live ? cur_sa : kSkipA);
+            const int soff_b = uni(live ? cur_cc * cstep_b : kSkipA);
+            cur_sa += adv_sa;
+            cur_t += adv_t;
+            cur_cc += adv_cc;
+            const bool wrap = cur_cc >= cpt;
+            cur_cc = uni(wrap ? cur_cc - cpt : cur_cc);
+            cur_t = uni(cur_t + (wrap ? 1 : 0));
             int voff[TN];
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) voff[ni] = vtap[t_ld][ni];
+            for (int ni = 0; ni < TN; ++ni) voff[ni] = LDM_TAP_ARITH ? tap_off(t_ld, ni) : vtap[LDM_TAP_ARITH ? 0 : t_ld][ni];
 #pragma unroll
             for (int mi = 0; mi < TM; ++mi) {
                 if constexpr (LDM_DIAG & 8) {
@@ -590,10 +625,14 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
         for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
             for (int r = 0; r < MF::NACC; ++r) acc2[mi][ni][r] = 0.f;
-    auto compute = [&](const Frag<TM, TN>(&f)[kGroup], int grp) {
+    auto compute = [&](const Frag<TM, TN>(&f)[kGroup], int grp, auto all_live) {
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-            if (grp * kGroup + q >= nmine) break;   // wave-uniform: no MFMAs on the padding chunks
+            if (!decltype(all_live)::value && grp * kGroup + q >= nmine) break;   // wave-uniform: no MFMAs on padding
+            if constexpr (LDM_DIAG & 16) {          // diagnostic: no MFMAs either (fixed cost only)
+                acc[0][0][0] = acc[0][0][0] + f[q].a[0][0] * f[q].b[0][0];
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -615,23 +654,31 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     LDM_STAMP(2);
     // Groups past this wave's range are not loaded at all: an out-of-range buffer load moves no data
     // but still costs texture-address cycles, and with short K loops padding groups were ~half of all
-    // vector-memory instructions (rocprofv3 TA_BUSY).  The steady-state loop below always has both
-    // next groups live, so its loads are unconditional and the waitcnt pass keeps the next group in
-    // flight across each compute; the tail (1 or 2 groups) is peeled.
-    if (ngrp > 0) load(f0, 0);
+    // vector-memory instructions (rocprofv3 TA_BUSY).  The steady-state loop runs while both next
+    // groups are full (no liveness checks, unconditional loads, so the waitcnt pass keeps the next
+    // group in flight across each compute); the last <= 3 groups are peeled.
+    using Live = std::true_type;
+    using Maybe = std::false_type;
+    const int nfull = nmine / kGroup;
+    if (ngrp > 0) load(f0, 0, Maybe{});
     int gi = 0;
-    for (; gi + 2 < ngrp; gi += 2) {
-        load(f1, gi + 1);
-        compute(f0, gi);
-        load(f0, gi + 2);
-        compute(f1, gi + 1);
+    for (; gi + 2 < nfull; gi += 2) {
+        load(f1, gi + 1, Live{});
+        compute(f0, gi, Live{});
+        load(f0, gi + 2, Live{});
+        compute(f1, gi + 1, Live{});
     }
-    if (gi + 1 < ngrp) {
-        load(f1, gi + 1);
-        compute(f0, gi);
-        compute(f1, gi + 1);
-    } else if (gi < ngrp) {
-        compute(f0, gi);
+    while (gi < ngrp) {   // tail: group gi is in f0
+        if (gi + 1 < ngrp) {
+            load(f1, gi + 1, Maybe{});
+            compute(f0, gi, Maybe{});
+            if (gi + 2 < ngrp) load(f0, gi + 2, Maybe{});
+            compute(f1, gi + 1, Maybe{});
+            gi += 2;
+        } else {
+            compute(f0, gi, Maybe{});
+            gi += 1;
+        }
     }
     if constexpr (NCH == 2) {
 #pragma unroll
