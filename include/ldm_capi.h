@@ -71,13 +71,14 @@ typedef struct ldm_conv_plan {
     int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32         */
     int32_t tm, tn, wk;    /* MFMA tiles per wave along M / N, waves splitting K per block      */
     int32_t ks;            /* blocks splitting K (>1: partial tiles + fixed-order last-arriver sum) */
-    int32_t reserved;
+    int32_t balance;       /* 4-phase transposed convs: phase p splits K ks*ntap_p ways (equal K per block) */
     int64_t packed_floats; /* size of the packed-weight buffer ldm_conv_pack_weight fills (0 = none) */
     int64_t ws_floats;     /* workspace floats the plan needs (ks > 1): tile counters, then partials */
 } ldm_conv_plan;
 
 int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan);
-/* Force a specific plan (autotuning / tests).  Fills packed_floats / ws_floats; validates. */
+/* Force a specific plan (autotuning / tests).  Fills packed_floats / ws_floats; validates.
+ * ks < 0 requests the phase-balanced split with base -ks (4-phase layers only). */
 int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,
                               ldm_conv_plan* plan);
 /* Re-lay the torch weight into the MFMA fragment order of `plan` (tap-major K, zero padded). */

@@ -53,6 +53,10 @@ struct ConvArgs {
     int32_t ks;            // blocks splitting K (cross-block split-K)
     int32_t out_nhwc;      // output / skip / fused-update tensors are NHWC (the input layout is a template flag)
     int32_t nN, nM;        // N / M tiles per phase
+    int32_t balance;       // 4-phase layers: phase p splits K ks_p = ks_base * ntap_p ways (equal work per block)
+    int32_t bofs[kMaxPhase];    // balance: first block of each phase (after the XCD renumbering)
+    int32_t bks_log2[kMaxPhase];  // balance: log2 ks_p
+    int32_t nblocks_bal;          // balance: grid size
     float* part;           // ks > 1: partial tiles [phase][M-tile][N-tile][ks][BM*BN]
     int32_t* cnt;          // ks > 1: arrival counter per tile (zero between launches)
     FastDiv fd_ks;         // M-tile' -> (M-tile, split)
@@ -408,7 +412,24 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
         nt = (nt0 & m0_) | (inner & m1_) | (outer & m2_);
         mt = a.fd_ks.div(mtx);
         ksp = mtx - mt * a.ks;
+        if constexpr (PH4) {
+            if (a.balance) {
+                // phase-balanced split: phase p's tiles are split ks_p = ks * ntap_p ways, so every block
+                // carries the same K; consecutive (XCD-grouped) blocks walk one phase's N-tiles, then its
+                // (M-tile, split) pairs
+                const int p = (int)(wgid >= a.bofs[1]) + (int)(wgid >= a.bofs[2]) + (int)(wgid >= a.bofs[3]);
+                const int local = wgid - sel_phase<true>(a.bofs, p);
+                const int lks = sel_phase<true>(a.bks_log2, p);
+                const int r2 = a.fd_nn.div(local);
+                nt = local - r2 * a.fd_nn.d;
+                mt = r2 >> lks;
+                ksp = r2 - (mt << lks);
+                ph = p;
+            }
+        }
     }
+    // K splits of this block's tile (ks_p in balance mode), and the partial-tile slots per tile
+    const int ksn = uni((PH4 && a.balance) ? 1 << sel_phase<PH4>(a.bks_log2, ph) : a.ks);
     const int m0 = mt * BM, n0 = nt * BN;
     const int HWin = a.Hin * a.Win;
     const int col = lane % TILE, lg = lane / TILE;
@@ -454,7 +475,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     const int wstride_b = a.Mpad * CK * 4;                 // bytes per packed chunk
     // K chunks are dealt round-robin over the ks*WK waves that share this output tile: wave `wave` of
     // split `ksp` owns chunks g, g + G, g + 2G, ...
-    const int G = uni(a.ks * WK), g = uni(ksp * WK + wave);
+    const int G = uni(ksn * WK), g = uni(ksp * WK + wave);
     const int nmine = nchunk > g ? uni((nchunk - g + G - 1) / G) : 0;
     const int ngrp = (nmine + kGroup - 1) / kGroup;
     // (uniform values pinned to SGPRs with readfirstlane: a buffer resource or soffset that the
@@ -490,7 +511,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     if constexpr (kPre) {
         // (issued unconditionally — with a K split only the last block runs the epilogue, and its
         // sources get zero records instead, so the loads return 0 without touching memory)
-        const EpiSrc esrc = epi_sources(a, a.ks == 1);
+        const EpiSrc esrc = epi_sources(a, ksn == 1);
         {
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
@@ -701,7 +722,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
                 sw[(TILE * mi + MF::row(r, lg)) * LDB + TILE * ni + col] = acc[mi][ni][r];
     __syncthreads();
     LDM_STAMP(4);
-    if (a.ks == 1) {
+    if (ksn == 1) {
         if constexpr (kPre) {
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
@@ -751,7 +772,7 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == a.ks - 1;
+        const int last = old == ksn - 1;
         if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = last;
     }
@@ -769,11 +790,11 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
         float pv[kMaxKSplit];
 #pragma unroll
         for (int s2 = 0; s2 < kMaxKSplit; ++s2)
-            if (s2 < a.ks && s2 != ksp) pv[s2] = part_load(tpart + (size_t)s2 * (BM * BN) + e);
+            if (s2 < ksn && s2 != ksp) pv[s2] = part_load(tpart + (size_t)s2 * (BM * BN) + e);
         float v = ksp == 0 ? own : pv[0];
 #pragma unroll
         for (int s2 = 1; s2 < kMaxKSplit; ++s2)
-            if (s2 < a.ks) v = v + (s2 == ksp ? own : pv[s2]);
+            if (s2 < ksn) v = v + (s2 == ksp ? own : pv[s2]);
         const int b = n / HqWq;
         const int r = n - b * HqWq;
         const int qyy = r / a.pt.Wq;
@@ -916,6 +937,22 @@ static int make_args(const ldm_conv_desc& d, const ldm_conv_plan& p, ConvArgs& a
     a.ks = p.kind ? std::max(1, (int)p.ks) : 1;
     a.nN = nN;
     a.nM = nM;
+    a.balance = p.kind && p.balance;
+    for (int i = 0; i < kMaxPhase; ++i) a.bofs[i] = a.bks_log2[i] = 0;
+    if (a.balance) {
+        int ofs = 0, kmax = 1;
+        for (int ph = 0; ph < a.pt.nphase; ++ph) {
+            const int ksp = a.ks * a.pt.ntap[ph];
+            int l2 = 0;
+            while ((1 << l2) < ksp) ++l2;
+            a.bofs[ph] = ofs;
+            a.bks_log2[ph] = l2;
+            ofs += nN * nM * ksp;
+            kmax = std::max(kmax, ksp);
+        }
+        a.nblocks_bal = ofs;
+        a.ks = kmax;   // partial slots per tile
+    }
     a.fd_ks = FastDiv::make(a.ks);
     a.fd_inner = FastDiv::make(a.tile_order == 1 ? nN : nM * a.ks);
     a.fd_nn = FastDiv::make(nN);
@@ -936,10 +973,17 @@ static int64_t split_tiles(const ldm_conv_desc& d, const ldm_conv_plan& p, const
     return nN * nM * pt.nphase;
 }
 
+static int split_slots(const ldm_conv_plan& p, const PhaseTable& pt) {
+    int k = p.ks;
+    if (p.balance)
+        for (int i = 0; i < pt.nphase; ++i) k = std::max(k, p.ks * pt.ntap[i]);
+    return k;
+}
+
 static int64_t split_ws_floats(const ldm_conv_desc& d, const ldm_conv_plan& p, const PhaseTable& pt) {
-    if (p.kind == 0 || p.ks <= 1) return 0;
+    if (p.kind == 0 || split_slots(p, pt) <= 1) return 0;
     const int bm = tile_m(p.kind) * p.tm, bn = tile_m(p.kind) * p.tn;
-    return kSplitCounters + split_tiles(d, p, pt) * p.ks * bm * bn;
+    return kSplitCounters + split_tiles(d, p, pt) * split_slots(p, pt) * bm * bn;
 }
 
 static bool plan_ok(const ldm_conv_desc& d, int kind, int tm, int tn, int wk, int ks) {
@@ -962,6 +1006,8 @@ using namespace ldm;
 extern "C" int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,
                                          ldm_conv_plan* plan) {
     LDM_REQUIRE(d && plan, "conv plan: null argument");
+    const bool balance = ks < 0;   // ks = -k: phase-balanced split (4-phase layers), base k
+    if (balance) ks = -ks;
     LDM_REQUIRE(plan_ok(*d, kind, tm, tn, wk, ks), "conv plan: unsupported (kind, tm, tn, wk, ks) for this layer");
     ldm_conv_plan p{};
     p.kind = kind;
@@ -969,13 +1015,20 @@ extern "C" int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int t
     p.tn = kind ? tn : 1;
     p.wk = kind ? wk : 1;
     p.ks = kind ? ks : 1;
+    p.balance = balance ? 1 : 0;
     PhaseTable pt;
     int Mpad;
     int64_t floats;
     int rc = layout_for_plan(*d, p, pt, Mpad, floats);
     if (rc) return rc;
+    if (balance) {
+        LDM_REQUIRE(kind != 0 && pt.nphase == 4, "conv plan: a phase-balanced split needs a 4-phase (stride-2 transposed) layer");
+        for (int i = 0; i < 4; ++i)
+            LDM_REQUIRE(pt.ntap[i] > 0 && (pt.ntap[i] & (pt.ntap[i] - 1)) == 0 && ks * pt.ntap[i] <= kMaxKSplit,
+                        "conv plan: phase-balanced split needs power-of-two taps per phase and ks*taps <= 16");
+    }
     p.packed_floats = floats;
-    LDM_REQUIRE(p.ks == 1 || split_tiles(*d, p, pt) <= kSplitCounters, "conv plan: too many tiles for a K split");
+    LDM_REQUIRE(split_slots(p, pt) == 1 || split_tiles(*d, p, pt) <= kSplitCounters, "conv plan: too many tiles for a K split");
     p.ws_floats = split_ws_floats(*d, p, pt);
     *plan = p;
     return 0;
@@ -1033,7 +1086,8 @@ static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq,
     const int BMx = TILE * p.tm, BNx = TILE * p.tn;
     const size_t lds = (size_t)p.wk * BMx * (BNx + 1) * sizeof(float);
     // 1-D grid, tile order remapped XCD-aware inside the kernel
-    dim3 grid((unsigned)(((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.ks * a.pt.nphase));
+    dim3 grid((unsigned)(a.balance ? a.nblocks_bal
+                                   : ((Nq + BNx - 1) / BNx) * ((a.Cout + BMx - 1) / BMx) * a.ks * a.pt.nphase));
     dim3 block(64 * p.wk);
     const int code = (p.tm - 1) * 2 + (p.tn - 1);
 #define LDM_CASE(WK, C, TM, TN)                                                                              \
@@ -1101,7 +1155,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
         return 0;
     }
     LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk, p.ks), "conv forward: invalid plan");
-    if (a.ks > 1) {
+    if (a.ks > 1) {   // (balance: a.ks = the largest per-phase split)
         PhaseTable pt2;
         LDM_REQUIRE(build_phase_table(d, pt2) == 0 && p.ws_floats == split_ws_floats(d, p, pt2),
                     "conv forward: plan workspace size does not match the descriptor");

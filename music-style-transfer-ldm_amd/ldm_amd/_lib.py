@@ -38,10 +38,10 @@ class Epilogue(ctypes.Structure):
 
 class ConvPlan(ctypes.Structure):
     _fields_ = [("kind", c_int32), ("tm", c_int32), ("tn", c_int32), ("wk", c_int32), ("ks", c_int32),
-                ("reserved", c_int32), ("packed_floats", c_int64), ("ws_floats", c_int64)]
+                ("balance", c_int32), ("packed_floats", c_int64), ("ws_floats", c_int64)]
 
     def key(self):
-        return (self.kind, self.tm, self.tn, self.wk, self.ks)
+        return (self.kind, self.tm, self.tn, self.wk, -self.ks if self.balance else self.ks)
 
 
 class UNetShape(ctypes.Structure):

@@ -35,8 +35,9 @@ def candidates(desc, min_waves=256, max_waves=16384):
             for tn in (1, 2):
                 tiles = _tiles(desc, kind, tm, tn)
                 for wk in (1, 2, 4, 8):
-                    for ks in (1, 2, 4, 8, 16):
-                        if not min_waves <= tiles * wk * ks <= max_waves:
+                    bal = (-1, -2, -4) if (desc.transposed and desc.stride == 2) else ()
+                    for ks in (1, 2, 4, 8, 16) + bal:
+                        if not min_waves <= tiles * wk * (abs(ks) * (9 if ks < 0 else 4)) // 4 <= max_waves:
                             continue
                         p = L.ConvPlan()
                         rc = L.load().ldm_conv_make_plan_forced(ctypes.byref(desc), kind, tm, tn, wk, ks,

@@ -268,7 +268,9 @@ _SPLIT_CASES = {
     # name: (B, Cin, H, W, Cout, k, stride, transposed, plans)
     "bottleneck": (8, 512, 2, 8, 512, 3, 1, False, [(1, 1, 1, 4, 4), (1, 2, 2, 2, 8), (2, 1, 1, 2, 16), (1, 1, 2, 1, 16)]),
     "enc4": (8, 256, 4, 16, 512, 3, 2, False, [(1, 2, 1, 4, 2), (1, 1, 1, 2, 8)]),
-    "dec4": (8, 512, 2, 8, 256, 3, 2, True, [(1, 1, 1, 4, 4), (2, 2, 2, 2, 8), (1, 2, 2, 1, 16)]),
+    "dec4": (8, 512, 2, 8, 256, 3, 2, True, [(1, 1, 1, 4, 4), (2, 2, 2, 2, 8), (1, 2, 2, 1, 16), (2, 2, 1, 8, -1),
+                                              (2, 2, 2, 4, -2), (1, 1, 1, 2, -4)]),
+    "dec2k4": (2, 64, 32, 32, 16, 4, 2, True, [(2, 1, 1, 2, -1), (2, 1, 2, 4, -2)]),
     "enc1": (2, 32, 16, 64, 64, 3, 1, False, [(1, 2, 2, 4, 2), (1, 1, 2, 8, 4)]),
     "proj": (8, 512, 1, 16, 1024, 1, 1, False, [(1, 1, 1, 4, 4), (2, 2, 1, 1, 8)]),
 }
@@ -285,7 +287,7 @@ def test_split_k_plans(cuda, name):
     wshape = (Cin, Cout, k, k) if tr else (Cout, Cin, k, k)
     w = (torch.randn(wshape, generator=g) * 0.05).to(cuda)
     bias = torch.randn(Cout, generator=g).to(cuda)
-    pad, op = (k // 2, 1) if tr else (k // 2, 0)
+    pad, op = ((1, 1) if k == 3 else (1, 0)) if tr else (k // 2, 0)
     desc = ops.make_desc(B, Cin, H, W, Cout, k, k, stride, pad, op if tr else 0, tr)
     xs = [torch.randn(B, Cin, H, W, generator=g).to(cuda) for _ in range(3)]
     base = ops.get_plan(desc, force=(2, 1, 1, 1, 1))
@@ -304,7 +306,7 @@ def test_split_k_plans(cuda, name):
         assert rel_err(npy(refs[0]), y64.clamp_min(0).numpy()) < 1e-5
         for pl in plans:
             plan = ops.get_plan(desc, force=pl)
-            assert plan.ks == pl[4] and plan.ws_floats > 0
+            assert plan.ks == abs(pl[4]) and plan.balance == (pl[4] < 0) and plan.ws_floats > 0
             outs = [run(xs[i % 3], plan) for i in range(9)]
             torch.cuda.synchronize()
             for i, y in enumerate(outs):
