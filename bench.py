@@ -131,7 +131,7 @@ def time_layers(engine, shape, dev, reps=50):
                      "flops": fl, "bytes": by}
         # the reverse loop's folded form: scores from the projection input z against scale*Wq^T K
         z = torch.randn(shape.B, Lt, E, device=dev)
-        kf = torch.randn(shape.B, 4, E, Lt, device=dev)
+        kf = torch.randn(shape.B, 4, Lt, E, device=dev)
         bf = torch.randn(shape.B, 4, Lt, device=dev)
         us = _graph_time_us(lambda: lib.ldm_attention_folded(z.data_ptr(), kv.data_ptr(), kf.data_ptr(), bf.data_ptr(),
                                                              o.data_ptr(), shape.B, E, 4, Lt, Lt,

@@ -125,7 +125,7 @@ int ldm_time_mlp_forward(const void* t, int32_t t_is_float, int32_t B, int32_t d
  * q [B,E,L] (the Q in-projection output in NCHW token order), kv [B,2E,S] (K channels then V
  * channels), out [B,E,L] = softmax((q*scale)^T k) v per head, written channel-major so the
  * out-projection reads it as NCHW (the reference's two permutes, model.py:144-158, vanish). */
-/* Folded-query form for a fixed key set (the reverse loop's style maps): kf [B,heads,E,S] =
+/* Folded-query form for a fixed key set (the reverse loop's style maps): kf [B,heads,S,E] =
  * scale * Wq_h^T K_h, bf [B,heads,S] = scale * bq_h^T K_h from kv [B,2E,S] and the Q in-projection
  * (wq [E,E] torch layout, bq [E]); ldm_attention_folded then takes the projection's input z [B,L,E]
  * (token-major) and writes out [B,L,E] (token-major) = the same attention as q = Wq z + bq.

@@ -153,11 +153,11 @@ struct AMfma<2> {
 // Each block owns LT query rows of one (b, head): grid = B * heads * (LP / LT).
 // TOK: q and out are token-major [B,L,E] (the UNet engine's NHWC activations) instead of [B,E,L].
 // EQ > 0 (folded query projection, token-major only): `q` is the projection's INPUT z [B,L,E=EQ] and
-// the scores are z^T kf[b,h] + bf[b,h] with kf [B,heads,E,S] = scale*Wq_h^T K_h and bf [B,heads,S] =
+// the scores are z^T kf[b,h] + bf[b,h] with kf [B,heads,S,E] = scale*Wq_h^T K_h and bf [B,heads,S] =
 // scale*bq_h^T K_h (ldm_attention_fold_keys) — the same scores as ((Wq z + bq)*scale)^T K re-associated,
 // so the Q in-projection needs no launch of its own.
-template <int KIND, int LP, int SP, int D, int LT, bool TOK, int EQ = 0>
-__global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+template <int KIND, int LP, int SP, int D, int LT, bool TOK, int EQ = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                              float* __restrict__ out, int E, int heads, int L, int S,
                                                              float scale, const float* __restrict__ kf = nullptr,
                                                              const float* __restrict__ bf = nullptr) {
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     constexpr int LDP = SP + 1;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* Ps = sm;                                // [LT][SP+1]  (rows l0 .. l0+LT-1); folded: 4 slabs
-    float* Vs = sm + (EQ > 0 ? 4 : 1) * LT * LDP;  // [D][SP+1]
+    float* Vs = sm + (EQ > 0 ? NW : 1) * LT * LDP;  // [D][SP+1]
     constexpr int NSPLIT = LP / LT;
     const int l0 = (blockIdx.x % NSPLIT) * LT;
     const int bh = blockIdx.x / NSPLIT;
@@ -189,18 +189,33 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
 
     // stage V [D][S] -> LDS [D][SP+1]: every load of this thread issues before any LDS store
-    {
-        constexpr int NV = (D * SP + 255) / 256;
+    if (S == SP && (D * SP) % (256 * NW) == 0) {   // full rows: 16-byte loads
+        constexpr int NV4 = D * SP / (256 * NW);
+        float4 v[NV4];
+#pragma unroll
+        for (int u = 0; u < NV4; ++u) v[u] = reinterpret_cast<const float4*>(vb)[u * 64 * NW + (int)threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < NV4; ++u) {
+            const int e = 4 * (u * 64 * NW + (int)threadIdx.x);
+            const int c = e / SP, s = e % SP;
+            float* dst = Vs + c * LDP + s;
+            dst[0] = v[u].x;
+            dst[1] = v[u].y;
+            dst[2] = v[u].z;
+            dst[3] = v[u].w;
+        }
+    } else {
+        constexpr int NV = (D * SP + 64 * NW - 1) / (64 * NW);
         float v[NV];
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
-            const int e = u * 256 + (int)threadIdx.x;
+            const int e = u * 64 * NW + (int)threadIdx.x;
             const int c = e / SP, s = e % SP;
             v[u] = vb[(e < D * SP && s < S) ? c * S + s : 0];
         }
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
-            const int e = u * 256 + (int)threadIdx.x;
+            const int e = u * 64 * NW + (int)threadIdx.x;
             const int c = e / SP, s = e % SP;
             if (e < D * SP) Vs[c * LDP + s] = s < S ? v[u] : 0.f;
         }
@@ -210,23 +225,37 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         // Folded scores z^T kf: the E-long contraction is split over the 4 waves (each covers every tile
         // of the block over E/4, all of its operand loads in flight at once — a single memory round
         // trip), partial tiles go to 4 LDS slabs and the softmax pass below sums them in wave order.
-        constexpr int NSTEP = DQ / 4 / NLG;
-        static_assert(DQ % (4 * NLG) == 0 && NTL * NSTEP + NTS * NSTEP <= 96, "folded score tile too large");
-        const int kbase = wave * (DQ / 4);
+        // Both operands are E-contiguous (z token-major, kf [B,heads,S,E]), so MFMA step j = 4*jj + i
+        // takes lane group lg's k = kbase + 16*jj + 4*lg + i: one 16-byte load feeds 4 steps.
+        constexpr int NSTEP = DQ / NW / NLG;
+        static_assert(NLG == 4 && DQ % (NW * 16) == 0 && NTL * NSTEP + NTS * NSTEP <= 96, "folded score tile");
+        const int kbase = wave * (DQ / NW);
         float av[NTL][NSTEP], bv[NTS][NSTEP];
 #pragma unroll
         for (int lt = 0; lt < NTL; ++lt) {
             const int l = l0 + lt * TILE + col;
-            const float* zp = qb + (size_t)(l < L ? l : 0) * E + kbase + lg;
+            const float4* zp = reinterpret_cast<const float4*>(qb + (size_t)(l < L ? l : 0) * E + kbase + 4 * lg);
 #pragma unroll
-            for (int j = 0; j < NSTEP; ++j) av[lt][j] = l < L ? zp[NLG * j] : 0.f;
+            for (int jj = 0; jj < NSTEP / 4; ++jj) {
+                const float4 v = zp[4 * jj];
+                av[lt][4 * jj + 0] = l < L ? v.x : 0.f;
+                av[lt][4 * jj + 1] = l < L ? v.y : 0.f;
+                av[lt][4 * jj + 2] = l < L ? v.z : 0.f;
+                av[lt][4 * jj + 3] = l < L ? v.w : 0.f;
+            }
         }
 #pragma unroll
         for (int st = 0; st < NTS; ++st) {
             const int s = st * TILE + col;
-            const float* kp = kb + (size_t)(kbase + lg) * S + (s < S ? s : 0);
+            const float4* kp = reinterpret_cast<const float4*>(kb + (size_t)(s < S ? s : 0) * E + kbase + 4 * lg);
 #pragma unroll
-            for (int j = 0; j < NSTEP; ++j) bv[st][j] = s < S ? kp[(size_t)NLG * j * S] : 0.f;
+            for (int jj = 0; jj < NSTEP / 4; ++jj) {
+                const float4 v = kp[4 * jj];
+                bv[st][4 * jj + 0] = s < S ? v.x : 0.f;
+                bv[st][4 * jj + 1] = s < S ? v.y : 0.f;
+                bv[st][4 * jj + 2] = s < S ? v.z : 0.f;
+                bv[st][4 * jj + 3] = s < S ? v.w : 0.f;
+            }
         }
         float* Pw = Ps + (size_t)wave * LT * LDP;
 #pragma unroll
@@ -243,7 +272,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
             }
     }
     // S = (q*scale)^T k for this block's LT rows: tiles round-robin over the 4 waves
-    for (int tile = wave; tile < (EQ > 0 ? 0 : NTL * NTS); tile += 4) {
+    for (int tile = wave; tile < (EQ > 0 ? 0 : NTL * NTS); tile += NW) {
         const int lt = tile / NTS, st = tile % NTS;
         const int l = l0 + lt * TILE + col, s = st * TILE + col;
         const bool lok = l < L, sok = s < S;
@@ -276,7 +305,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         constexpr int RPW = SP >= 64 ? 1 : 64 / SP;
         constexpr int SEG = SP >= 64 ? 64 : SP;
         const int sub = lane / SEG, s0 = lane % SEG;
-        for (int r0 = wave * RPW; r0 < LT; r0 += 4 * RPW) {
+        for (int r0 = wave * RPW; r0 < LT; r0 += NW * RPW) {
             const int r = r0 + sub;             // local row; global query row l0 + r
             float* row = Ps + r * LDP;
             float x[SP / SEG];
@@ -287,7 +316,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
                 if constexpr (EQ > 0) {   // sum the 4 wave slabs in wave order, then the folded bias
                     float v = row[s];
 #pragma unroll
-                    for (int w = 1; w < 4; ++w) v = v + row[s + w * LT * LDP];
+                    for (int w = 1; w < NW; ++w) v = v + row[s + w * LT * LDP];
                     x[u] = v + (s < S ? bf[(size_t)(b * heads + h) * S + s] : 0.f);
                 } else {
                     x[u] = row[s];
@@ -313,7 +342,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     // O[c][l] = sum_s V[c][s] P[l][s]
     constexpr int NTC = D / TILE;
     float* ob = TOK ? out + (size_t)b * L * E + (size_t)h * D : out + ((size_t)b * E + (size_t)h * D) * L;
-    for (int tile = wave; tile < NTC * NTL; tile += 4) {
+    for (int tile = wave; tile < NTC * NTL; tile += NW) {
         const int ct = tile / NTL, lt = tile % NTL;
         typename MF::acc_t acc;
 #pragma unroll
@@ -333,8 +362,12 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         }
         const int l = l0 + lt * TILE + col;
         if (l < L) {
+            if constexpr (TOK && KIND == 2) {   // rows 4*lg .. 4*lg+3 = 4 consecutive channels of token l
+                *reinterpret_cast<float4*>(ob + (size_t)l * E + ct * TILE + 4 * lg) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            } else {
 #pragma unroll
-            for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * qcs + l * qls] = acc[r];
+                for (int r = 0; r < MF::NACC; ++r) ob[(ct * TILE + MF::row(r, lg)) * qcs + l * qls] = acc[r];
+            }
         }
     }
 }
@@ -342,7 +375,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
 // ------------------------------------------------------------------------------------------------
 // Folds for the reverse loop (style fixed over the loop, weights fixed between optimiser steps).
 // ------------------------------------------------------------------------------------------------
-// kf[b,h,e,s] = scale * sum_c Wq[h*d+c, e] K[b, h*d+c, s];  bf[b,h,s] = scale * sum_c bq[h*d+c] K[b,h*d+c,s]
+// kf[b,h,s,e] = scale * sum_c Wq[h*d+c, e] K[b, h*d+c, s];  bf[b,h,s] = scale * sum_c bq[h*d+c] K[b,h*d+c,s]
 // (fp64 accumulation, one rounding to fp32).  kv [B,2E,S] channel-major; wq [E,E] torch Linear layout.
 __global__ __launch_bounds__(256) void attention_fold_keys_kernel(const float* __restrict__ kv, const float* __restrict__ wq,
                                                                   const float* __restrict__ bq, int B, int E, int heads,
@@ -351,11 +384,11 @@ __global__ __launch_bounds__(256) void attention_fold_keys_kernel(const float* _
     const int d = E / heads;
     const int64_t nk = (int64_t)B * heads * E * S;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < nk) {
-        const int s = (int)(idx % S);
-        int64_t r = idx / S;
-        const int e = (int)(r % E);
-        r /= E;
+    if (idx < nk) {   // kf [B,heads,S,E]: e fastest (the attention reads 16-byte runs along E)
+        const int e = (int)(idx % E);
+        int64_t r = idx / E;
+        const int s = (int)(r % S);
+        r /= S;
         const int h = (int)(r % heads), b = (int)(r / heads);
         const float* kr = kv + ((int64_t)b * 2 * E + (int64_t)h * d) * S + s;
         const float* wr = wq + (int64_t)h * d * E + e;
@@ -662,20 +695,19 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
     LDM_REQUIRE(z && kv && kf && bf && out, "attention (folded): null argument");
     LDM_REQUIRE(B > 0 && heads == 4 && L > 0 && S > 0, "attention (folded): bad shape");
     const int d = E / heads;
-    const dim3 blk(256);
-#define LDM_ATTF(LP, SP, D, LT, EQV)                                                                     \
+#define LDM_ATTF(LP, SP, D, LT, EQV, NWV)                                                                \
     if (d == D && E == EQV && L <= LP && S <= SP) {                                                      \
-        const size_t lds = ((size_t)4 * LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);         \
-        hipLaunchKernelGGL((attention_mfma_kernel<2, LP, SP, D, LT, true, EQV>), dim3(B * heads * (LP / LT)), blk, \
-                           lds, st, z, kv, out, E, heads, L, S, 1.0f, kf, bf);                           \
+        const size_t lds = ((size_t)NWV * LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);       \
+        hipLaunchKernelGGL((attention_mfma_kernel<2, LP, SP, D, LT, true, EQV, NWV>), dim3(B * heads * (LP / LT)), \
+                           dim3(64 * NWV), lds, st, z, kv, out, E, heads, L, S, 1.0f, kf, bf);           \
         LDM_CHECK_LAUNCH("attention_mfma_kernel (folded)");                                              \
         return 0;                                                                                        \
     }
-    LDM_ATTF(16, 16, 128, 16, 512)
-    LDM_ATTF(64, 64, 64, 16, 256)
-    LDM_ATTF(32, 32, 64, 16, 256)
-    LDM_ATTF(32, 32, 128, 16, 512)
-    LDM_ATTF(16, 16, 64, 16, 256)
+    LDM_ATTF(16, 16, 128, 16, 512, 8)
+    LDM_ATTF(64, 64, 64, 16, 256, 8)
+    LDM_ATTF(32, 32, 64, 16, 256, 8)
+    LDM_ATTF(32, 32, 128, 16, 512, 8)
+    LDM_ATTF(16, 16, 64, 16, 256, 4)
 #undef LDM_ATTF
     return fail(3, "attention (folded): no instance for this shape");
 }
