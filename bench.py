@@ -33,9 +33,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="latents per GPU")
-    ap.add_argument("--timesteps", type=int, default=50)
-    ap.add_argument("--eta", type=float, default=0.0)
+    ap.add_argument("--workload", choices=("sample", "transfer", "train"), default="sample",
+                    help="sample = config 2 (the BASELINE metric, default); transfer = config 5 (content/style "
+                         "transfer loop, T'=100, eta=1.0); train = configs 3/4 (encode -> UNet train step -> decode, "
+                         "batch 32/GPU, RCCL grad all-reduce when N>1)")
+    ap.add_argument("--batch", type=int, default=None, help="latents per GPU (8 sample/transfer, 32 train)")
+    ap.add_argument("--timesteps", type=int, default=None, help="50 for sample, T'=100 for transfer")
+    ap.add_argument("--eta", type=float, default=None, help="0.0 for sample, 1.0 for transfer")
     ap.add_argument("--split", type=int, default=1,
                     help="run the per-GPU batch as this many sub-batch chains on separate streams (one graph)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
@@ -43,7 +47,14 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 32 if a.workload == "train" else 8
+    if a.timesteps is None:
+        a.timesteps = 100 if a.workload == "transfer" else 50
+    if a.eta is None:
+        a.eta = 1.0 if a.workload == "transfer" else 0.0
+    return a
 
 
 def layer_flops(d):
@@ -175,6 +186,68 @@ def cpu_baseline(ldm, batch, times, eta, seconds):
                       f"of the same 50-step schedule, torch-CPU restatement oracle/ldm_torch_cpu.py, {dt:.1f}s"}
 
 
+TRAIN_GFLOP_PER_SAMPLE = 10.7   # frozen VAE enc fwd 0.698 + 3 x (style enc 1.642 + UNet 0.449 + dec 1.242)
+
+
+def run_train(args, world, rank, dev, M):
+    """Configs 3/4: LDMTrainer.train_step (reference train.py:163-208) = VAE encode -> style encode ->
+    q_sample -> UNet -> predict_start -> VAE decode -> losses -> backward -> (RCCL bucketed grad
+    all-reduce when N>1) -> GradScaler + Adam.  Eager (the step ends in the reference's .item() syncs).
+    value = samples/s over all ranks; weak scaling (batch per GPU fixed)."""
+    import torch.distributed as dist
+    from models.train import LDMTrainer
+    torch.manual_seed(0)
+    ldm = M.LDM(32, pretrained_path="").to(dev)               # random-init weights of the architecture
+    if world > 1:
+        from ldm_amd import dist as hdist                      # same initial weights on every rank
+        hdist.broadcast_parameters(ldm)
+    trainer = LDMTrainer(ldm, None, dev, lr=1e-4)                 # LDMTrainer default (train.py:142)
+    ldm.train()
+    B = args.batch
+    g = torch.Generator().manual_seed(11 + rank)
+    content = torch.rand(B, 1, 128, 512, generator=g).to(dev)
+    style = torch.rand(B, 1, 128, 512, generator=g).to(dev)
+    torch.manual_seed(7 + rank)
+    for _ in range(args.warmup):
+        trainer.train_step(content, style)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = trainer.train_step(content, style)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if not all(map(lambda v: v == v and abs(v) != float("inf"), losses.values())):
+        raise SystemExit(f"non-finite losses {losses}")
+    ms_step = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+    flops = TRAIN_GFLOP_PER_SAMPLE * 1e9 * B
+    achieved = flops / (ms_step * 1e-3) / 1e12
+    return {
+        "metric": "LDM train samples/sec (encode -> UNet train step -> decode), 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (U[0,1) content/style mels; random-init weights; t ~ randint on device)",
+        "config": {"workload": f"configs 3/4: LDMTrainer.train_step, batch {B}/GPU, 1x128x512 mels, fp32 kernels "
+                               f"inside the reference's autocast region, Adam + GradScaler"
+                               + (f", RCCL bucketed grad all-reduce over {world} ranks" if world > 1 else ""),
+                   "global_batch": B * world, "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "whole train step (composite)", "bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "traffic": None, "flops_per_step": flops},
+        "last_losses": {k: round(v, 6) for k, v in losses.items()},
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,14 +264,31 @@ def main():
     import models.model as M
     from ldm_amd.engine import GraphedDDIM
 
+    if args.workload == "train":
+        result = run_train(args, world, rank, dev, M)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     torch.manual_seed(0)
     ldm = M.LDM(32, pretrained_path="").to(dev).eval()     # random-init weights of the architecture
     B = args.batch
     g = torch.Generator().manual_seed(1 + rank)
     style = torch.rand(B, 1, 128, 512, generator=g).to(dev)   # synthetic 1x128x512 style mel, U[0,1)
-    torch.manual_seed(1234 + rank)
-    z_T = torch.randn((B, 32, 16, 64)).to(dev)                 # CPU generator like model.py:394
-    times = torch.linspace(ldm.num_timesteps - 1, 0, args.timesteps).long()
+    if args.workload == "transfer":
+        # config 5: encode a content mel, q_sample it at T'-1, then the T'-step loop (model.py:468-559)
+        content = torch.rand(B, 1, 128, 512, generator=torch.Generator().manual_seed(101 + rank)).to(dev)
+        with torch.no_grad():
+            z0 = ldm.encoder(content)
+            t_start = torch.full((B,), args.timesteps - 1, dtype=torch.long, device=dev)
+            z_T, _ = ldm.noise_scheduler(z0, t_start)
+        times = torch.linspace(args.timesteps - 1, 0, args.timesteps).long()          # (model.py:514)
+    else:
+        torch.manual_seed(1234 + rank)
+        z_T = torch.randn((B, 32, 16, 64)).to(dev)                 # CPU generator like model.py:394
+        times = torch.linspace(ldm.num_timesteps - 1, 0, args.timesteps).long()
     n_iter = len(times) - 1
     coefs = ldm.noise_scheduler.reverse_coefs(times).to(dev)
     t_table = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(dev)
@@ -235,9 +325,14 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (U[0,1) style mel, N(0,1) z_T; random-init weights)",
-        "config": {"workload": f"config 2: {args.timesteps}-step DDIM reverse sample ({n_iter} UNet+update "
-                               f"iterations per step), batch {B}/GPU, 1x128x512 mel -> [{B},32,16,64] latents, "
-                               f"eta={args.eta}, hipGraph replay of {args.split} concurrent sub-batch chains", "global_batch": B * world,
+        "config": {"workload": (f"config 2: {args.timesteps}-step DDIM reverse sample ({n_iter} UNet+update "
+                                f"iterations per step), batch {B}/GPU, 1x128x512 mel -> [{B},32,16,64] latents, "
+                                f"eta={args.eta}, hipGraph replay of {args.split} concurrent sub-batch chains")
+                   if args.workload == "sample" else
+                   (f"config 5: content/style transfer loop, T'={args.timesteps} ({n_iter} UNet+update iterations "
+                    f"per step, content encoded and q_sampled at T'-1 before timing), batch {B}/GPU, "
+                    f"eta={args.eta}, fp32 compute and accumulators (>= the config's fp16), hipGraph replay"),
+                   "global_batch": B * world,
                    "latent": [B, 32, 16, 64], "parallelism": f"dp{world} (independent batch shards)"},
         "us_per_denoise_iteration": round(us_iter, 2),
     }

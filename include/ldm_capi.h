@@ -97,10 +97,22 @@ int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* plan, const
 /* ---- BatchNorm2d, train mode (model.py:18,21,24,39,42 under .train(); model.py:307,344-347) ----
  * Batch statistics over (B,H,W) per channel, normalise in place, optional activation, and the
  * running-stat update (momentum, unbiased variance) exactly as nn.BatchNorm2d.  save_mean /
- * save_invstd [C] are written for the backward pass (may be NULL). */
+ * save_invstd [C] are written for the backward pass (may be NULL).  workspace:
+ * ldm_reduce_workspace_floats(B,C,HW) floats, 8-byte aligned (reduce.hip).  Each channel is reduced
+ * by a fixed set of slices in a fixed order (fp64 sums): bitwise reproducible. */
+int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW);
 int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
                         float* running_mean, float* running_var, float momentum, float eps, int32_t act,
-                        float* save_mean, float* save_invstd, void* stream);
+                        float* save_mean, float* save_invstd, float* workspace, void* stream);
+/* The same in two stages, for SyncBatchNorm (replaces torch.nn.SyncBatchNorm's batch_norm_stats /
+ * batch_norm_gather_stats_with_counts / batch_norm_elemt for the data-parallel train path):
+ * stats[2c] = sum x, stats[2c+1] = sum x^2 over this rank's batch (fp64) -> the caller all-reduces
+ * stats over ranks -> apply with count = the global B*H*W. */
+int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
+                        void* stream);
+int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
+                        const float* weight, const float* bias, float* running_mean, float* running_var,
+                        float momentum, float eps, int32_t act, float* save_mean, float* save_invstd, void* stream);
 
 /* ---- eval-mode BatchNorm2d (+activation) as a standalone op, out-of-place (y may equal x) ------ */
 int ldm_batchnorm_eval(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
@@ -251,14 +263,24 @@ int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float
                              float* workspace, void* stream);
 /* Backward of the fused epilogue act(v) (+bcast[b,c]) (+skip): dv = dy*act'(v) (from act_out = act(v);
  * GELU from pre_act = v), dbias[c] = sum dv, dbcast[b,c] = sum_hw dy.  dv / dbias / dbcast may be NULL;
- * dv may alias dy. */
+ * dv may alias dy.  workspace: ldm_reduce_workspace_floats(B,C,HW) floats (NULL when no sums). */
 int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B, int32_t C,
-                     int32_t HW, float* dv, float* dbias, float* dbcast, void* stream);
+                     int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace, void* stream);
 /* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
- * y = its output, x = its input; dx / dweight / dbias may be NULL. */
+ * y = its output, x = its input; dx / dweight / dbias may be NULL.  workspace as ldm_batchnorm_train. */
 int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
                            const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
-                           int32_t HW, float* dx, float* dweight, float* dbias, void* stream);
+                           int32_t HW, float* dx, float* dweight, float* dbias, float* workspace, void* stream);
+/* The same in two stages for SyncBatchNorm: sums[2c] = sum g, sums[2c+1] = sum g*xhat over this rank
+ * (g = dy*act'(y)); dbias / dweight get these local sums (parameter grads stay local, as in
+ * torch.nn.SyncBatchNorm; the DP gradient all-reduce averages them) -> the caller all-reduces sums ->
+ * apply with count = the global B*H*W. */
+int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
+                                  const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
+                                  double* sums, float* dweight, float* dbias, float* workspace, void* stream);
+int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
+                                 const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
+                                 int32_t HW, const double* sums, double count, float* dx, void* stream);
 /* Backward of ldm_attention_core: dq [B,E,L], dkv [B,2E,S] (dK then dV). */
 int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv, int32_t B,
                            int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream);

@@ -100,112 +100,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 }
 
 // ================================================================================================
-// activation / bias / broadcast gradients of the fused conv epilogue y = act(v) (+bcast[b,c]) (+skip):
-//   dv = dy * act'(v) (act' from the saved post-activation value a = act(v)), dbias[c] = sum dv,
-//   dbcast[b][c] = sum_q dy.  One block per channel, fixed-order reductions.
-// ================================================================================================
-__device__ __forceinline__ float act_grad(int act, float a) {
-    switch (act) {
-        case LDM_ACT_RELU: return a > 0.f ? 1.f : 0.f;
-        case LDM_ACT_TANH: return 1.f - a * a;
-        case LDM_ACT_TANH_HALF: {   // a = (tanh(v)+1)/2 -> da/dv = (1 - tanh^2)/2
-            const float th = 2.f * a - 1.f;
-            return 0.5f * (1.f - th * th);
-        }
-        default: return 1.f;
-    }
-}
-
-__device__ __forceinline__ float block_sum(float v, float* red) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __syncthreads();
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    float s = 0.f;
-    for (int w = 0; w < nw; ++w) s += red[w];
-    return s;
-}
-
-__global__ __launch_bounds__(256) void act_backward_kernel(const float* __restrict__ dy, const float* __restrict__ aval,
-                                                           const float* __restrict__ pre, int act, int B, int C, int HW,
-                                                           float* __restrict__ dv, float* __restrict__ dbias,
-                                                           float* __restrict__ dbcast) {
-    __shared__ float red[8];
-    const int c = blockIdx.x;
-    float sb = 0.f;
-    for (int b = 0; b < B; ++b) {
-        const size_t base = ((size_t)b * C + c) * HW;
-        float sbc = 0.f;
-        for (int q = threadIdx.x; q < HW; q += blockDim.x) {
-            const float g = dy[base + q];
-            float d;
-            if (act == LDM_ACT_GELU) {   // needs the pre-activation v
-                const float v = pre[base + q];
-                const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752440f));
-                const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
-                d = g * (cdf + v * pdf);
-            } else {
-                d = g * act_grad(act, aval ? aval[base + q] : 0.f);
-            }
-            if (dv) dv[base + q] = d;
-            sb += d;
-            sbc += g;
-        }
-        if (dbcast) {
-            const float s = block_sum(sbc, red);
-            if (threadIdx.x == 0) dbcast[(size_t)b * C + c] = s;
-        }
-    }
-    if (dbias) {
-        const float s = block_sum(sb, red);
-        if (threadIdx.x == 0) dbias[c] = s;
-    }
-}
-
-// ================================================================================================
-// train-mode BatchNorm2d backward (+ activation): y = act(xhat*w + b), xhat = (x - mean)*invstd
-//   g = dy * act'(y);  dw = sum g*xhat;  db = sum g;  dx = w*invstd*(g - db/N - xhat*dw/N)
-// ================================================================================================
-__global__ __launch_bounds__(256) void bn_backward_kernel(const float* __restrict__ dy, const float* __restrict__ y,
-                                                          const float* __restrict__ x, const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, const float* __restrict__ w,
-                                                          int act, int B, int C, int HW, float* __restrict__ dx,
-                                                          float* __restrict__ dw, float* __restrict__ db) {
-    __shared__ float red[8];
-    const int c = blockIdx.x;
-    const float mu = mean[c], is = invstd[c];
-    float sg = 0.f, sgx = 0.f;
-    for (int b = 0; b < B; ++b) {
-        const size_t base = ((size_t)b * C + c) * HW;
-        for (int q = threadIdx.x; q < HW; q += blockDim.x) {
-            const float g = dy[base + q] * act_grad(act, y[base + q]);
-            const float xh = (x[base + q] - mu) * is;
-            sg += g;
-            sgx += g * xh;
-        }
-    }
-    sg = block_sum(sg, red);
-    sgx = block_sum(sgx, red);
-    const float N = (float)B * (float)HW;
-    const float k = (w ? w[c] : 1.f) * is;
-    if (dx) {
-        for (int b = 0; b < B; ++b) {
-            const size_t base = ((size_t)b * C + c) * HW;
-            for (int q = threadIdx.x; q < HW; q += blockDim.x) {
-                const float g = dy[base + q] * act_grad(act, y[base + q]);
-                const float xh = (x[base + q] - mu) * is;
-                dx[base + q] = k * ((g - sg / N) - xh * (sgx / N));
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        if (dw) dw[c] = sgx;
-        if (db) db[c] = sg;
-    }
-}
-
-// ================================================================================================
 // cross-attention backward, one block per (b, head); recomputes P from q, k:
 //   dV = dO P ; dP = dO^T V ; dS = P*(dP - rowsum(dP*P)) ; dq = scale*(K dS^T) ; dK = qs dS
 // q [B,E,L], kv [B,2E,S] (K then V), dout [B,E,L] -> dq [B,E,L], dkv [B,2E,S].
@@ -438,27 +332,6 @@ extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, 
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)a.partial, S, MN,
                        dw, accumulate);
     LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
-    return 0;
-}
-
-extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
-                                int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, void* stream) {
-    LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
-    LDM_REQUIRE(act != LDM_ACT_GELU || pre_act, "act_backward: GELU needs the pre-activation");
-    LDM_REQUIRE(act == LDM_ACT_NONE || act == LDM_ACT_GELU || act_out, "act_backward: needs the activation output");
-    hipLaunchKernelGGL(act_backward_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, act_out, pre_act, act, B, C,
-                       HW, dv, dbias, dbcast);
-    LDM_CHECK_LAUNCH("act_backward_kernel");
-    return 0;
-}
-
-extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
-                                      const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
-                                      int32_t HW, float* dx, float* dweight, float* dbias, void* stream) {
-    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
-    hipLaunchKernelGGL(bn_backward_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y, x, save_mean, save_invstd,
-                       weight, act, B, C, HW, dx, dweight, dbias);
-    LDM_CHECK_LAUNCH("bn_backward_kernel");
     return 0;
 }
 

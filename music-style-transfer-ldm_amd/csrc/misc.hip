@@ -522,64 +522,7 @@ __global__ __launch_bounds__(256) void ddim_step_kernel(float* __restrict__ x, c
     if (eps_log) eps_log[i] = e;
 }
 
-// ------------------------------------------------------------------------------------------------
-// train-mode BatchNorm2d: one block per channel; fp64 statistics like aten's CPU kernel
-// (batch_norm_cpu_collect_stats: accscalar_t = double), then x*alpha+beta and activation.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double block_sum_double(double v, double* red) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __syncthreads();
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    double s = 0.0;
-    for (int w = 0; w < nw; ++w) s += red[w];
-    return s;
-}
-
-__global__ __launch_bounds__(1024) void batchnorm_train_kernel(float* __restrict__ x, int B, int C, int HW,
-                                                                const float* __restrict__ weight,
-                                                                const float* __restrict__ bias,
-                                                                float* __restrict__ rmean, float* __restrict__ rvar,
-                                                                float momentum, float eps, int act,
-                                                                float* __restrict__ save_mean,
-                                                                float* __restrict__ save_invstd) {
-    __shared__ double red[16];
-    const int c = blockIdx.x;
-    const int64_t n = (int64_t)B * HW;
-    double s = 0.0;
-    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
-        s += (double)x[((size_t)b * C + c) * HW + p];
-    }
-    const double mean = block_sum_double(s, red) / (double)n;
-    double q = 0.0;
-    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
-        const double dv = (double)x[((size_t)b * C + c) * HW + p] - mean;
-        q += dv * dv;
-    }
-    const double var_sum = block_sum_double(q, red);
-    const float mean_f = (float)mean;
-    const float invstd = (float)(1.0 / sqrt(var_sum / (double)n + (double)eps));
-    const float alpha = invstd * (weight ? weight[c] : 1.0f);
-    const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
-    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-        const int b = (int)(e / HW), p = (int)(e - (int64_t)b * HW);
-        float* px = x + ((size_t)b * C + c) * HW + p;
-        const float v = *px * alpha + beta;
-        *px = apply_act(v, act);
-    }
-    if (threadIdx.x == 0) {
-        if (rmean) rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
-        if (rvar) {
-            const double unbiased = n > 1 ? var_sum / (double)(n - 1) : var_sum;
-            rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
-        }
-        if (save_mean) save_mean[c] = mean_f;
-        if (save_invstd) save_invstd[c] = invstd;
-    }
-}
+// (train-mode BatchNorm2d lives in reduce.hip)
 
 __global__ __launch_bounds__(256) void activation_kernel(const float* x, float* y, int64_t n, int act) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -804,16 +747,6 @@ extern "C" int ldm_ddim_step(float* x, const float* eps, const float* coef, floa
     hipLaunchKernelGGL(ddim_step_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, eps, coef, eta,
                        x0_log, eps_log, n);
     LDM_CHECK_LAUNCH("ddim_step_kernel");
-    return 0;
-}
-
-extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
-                                   float* running_mean, float* running_var, float momentum, float eps, int32_t act,
-                                   float* save_mean, float* save_invstd, void* stream) {
-    LDM_REQUIRE(x && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
-    hipLaunchKernelGGL(batchnorm_train_kernel, dim3(C), dim3(1024), 0, (hipStream_t)stream, x, B, C, HW, weight, bias,
-                       running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
-    LDM_CHECK_LAUNCH("batchnorm_train_kernel");
     return 0;
 }
 

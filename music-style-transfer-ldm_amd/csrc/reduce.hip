@@ -1,0 +1,471 @@
+// Per-channel reductions of the train path, sliced for the whole chip:
+//   * train-mode BatchNorm2d forward (batch stats -> normalise + act + running stats),
+//   * its backward (sum g, sum g*xhat -> dx),
+//   * the fused-epilogue activation backward (dv, dbias[c], dbcast[b,c]).
+// Reference semantics: nn.BatchNorm2d / the conv epilogues of model.py:10-49 (VAE) and
+// model.py:163-231 (UNet) under .train(); the backward follows torch's native_batch_norm_backward.
+//
+// Layout: NCHW fp32.  A channel's B*HW elements are cut into P contiguous slices of the flattened
+// (b, hw) index (slice length a multiple of 4, float4 loads when HW % 4 == 0), one 256-thread block
+// per (slice, channel), so a C=64..128 layer launches >= 1024 blocks instead of C.  Every reduction
+// has a fixed partition and a fixed order (thread stride -> wave shuffle tree -> waves in order ->
+// slices in order), so results are bitwise reproducible run to run.  BatchNorm statistics are fp64
+// (sum x, sum x^2) so the per-rank sums can be all-reduced for SyncBatchNorm between the two stages
+// (ldm_batchnorm_stats -> all-reduce -> ldm_batchnorm_apply; likewise the backward).
+#include "common.h"
+
+namespace ldm {
+namespace {
+
+constexpr int kThreads = 256;
+
+// slices per channel for a reduction over n = B*HW elements across C channels
+inline int bn_slices(int64_t n, int C) {
+    int64_t p = (1024 + C - 1) / C;                 // >= 1024 blocks in total
+    const int64_t by_len = (n + 2047) / 2048;       // but >= ~2048 elements per slice
+    if (p > by_len) p = by_len;
+    if (p < 1) p = 1;
+    if (p > 256) p = 256;
+    return (int)p;
+}
+inline int64_t slice_len(int64_t n, int P) { return ((n + P - 1) / P + 3) & ~(int64_t)3; }
+
+// slices per (b,c) plane for the activation backward
+inline int act_slices(int B, int C, int HW) {
+    int64_t q = (2048 + (int64_t)B * C - 1) / ((int64_t)B * C);
+    const int64_t by_len = (HW + 1023) / 1024;
+    if (q > by_len) q = by_len;
+    if (q < 1) q = 1;
+    return (int)q;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    T s = 0;
+    for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+    return s;
+}
+
+__device__ __forceinline__ float act_grad(int act, float a) {
+    switch (act) {
+        case LDM_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+        case LDM_ACT_TANH: return 1.f - a * a;
+        case LDM_ACT_TANH_HALF: {   // a = (tanh(v)+1)/2 -> da/dv = (1 - tanh^2)/2
+            const float th = 2.f * a - 1.f;
+            return 0.5f * (1.f - th * th);
+        }
+        default: return 1.f;
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void ld(const float* p, float (&v)[W]) {
+    if constexpr (W == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+        v[0] = *p;
+    }
+}
+template <int W>
+__device__ __forceinline__ void st(float* p, const float (&v)[W]) {
+    if constexpr (W == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        *p = v[0];
+    }
+}
+
+// Visit channel c's elements with flattened (b, hw) index in [e0, e1): f(offset) for W consecutive
+// elements of one plane.  Plane-by-plane, so no per-element division.
+template <int W, class F>
+__device__ __forceinline__ void slice_for(int64_t e0, int64_t e1, int C, int c, int HW, F&& f) {
+    if (e0 >= e1) return;
+    int b = (int)(e0 / HW);
+    int p = (int)(e0 - (int64_t)b * HW);
+    int64_t e = e0;
+    while (e < e1) {
+        const int64_t left = e1 - e;
+        const int n = (int)((int64_t)(HW - p) < left ? (int64_t)(HW - p) : left);
+        const size_t base = ((size_t)b * C + c) * HW + p;
+        for (int i = threadIdx.x * W; i < n; i += kThreads * W) f(base + i);
+        e += n;
+        ++b;
+        p = 0;
+    }
+}
+
+// ---- BatchNorm forward ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const float* __restrict__ x, int C, int HW,
+                                                                    int64_t n, int64_t S,
+                                                                    double* __restrict__ part) {
+    __shared__ double red[kThreads / 64];
+    const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
+    const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    double s = 0.0, q = 0.0;
+    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
+        float v[W];
+        ld<W>(x + o, v);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            s += (double)v[j];
+            q += (double)v[j] * (double)v[j];
+        }
+    });
+    s = block_sum(s, red);
+    q = block_sum(q, red);
+    if (threadIdx.x == 0) {
+        part[((size_t)c * P + k) * 2 + 0] = s;
+        part[((size_t)c * P + k) * 2 + 1] = q;
+    }
+}
+
+// stats[2c+j] = sum_k part[c][k][j] (slices in order); optional float copies out0/out1
+__global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double* __restrict__ part, int C, int P,
+                                                                   double* __restrict__ stats,
+                                                                   float* __restrict__ out0,
+                                                                   float* __restrict__ out1) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < P; ++k) {
+        a += part[((size_t)c * P + k) * 2 + 0];
+        b += part[((size_t)c * P + k) * 2 + 1];
+    }
+    stats[2 * c] = a;
+    stats[2 * c + 1] = b;
+    if (out0) out0[c] = (float)a;
+    if (out1) out1[c] = (float)b;
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(float* __restrict__ x, int C, int HW, int64_t n, int64_t S,
+                                                            const double* __restrict__ stats, double count,
+                                                            const float* __restrict__ weight,
+                                                            const float* __restrict__ bias, float* __restrict__ rmean,
+                                                            float* __restrict__ rvar, float momentum, float eps,
+                                                            int act, float* __restrict__ save_mean,
+                                                            float* __restrict__ save_invstd) {
+    const int k = blockIdx.x, c = blockIdx.y;
+    const double mean = stats[2 * c] / count;
+    double var_sum = stats[2 * c + 1] - mean * stats[2 * c];   // sum (x - mean)^2
+    if (var_sum < 0.0) var_sum = 0.0;
+    const float mean_f = (float)mean;
+    const float invstd = (float)(1.0 / sqrt(var_sum / count + (double)eps));
+    const float alpha = invstd * (weight ? weight[c] : 1.0f);
+    const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
+    const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
+        float v[W];
+        ld<W>(x + o, v);
+#pragma unroll
+        for (int j = 0; j < W; ++j) v[j] = apply_act(v[j] * alpha + beta, act);
+        st<W>(x + o, v);
+    });
+    if (k == 0 && threadIdx.x == 0) {
+        if (rmean) rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+        if (rvar) {
+            const double unbiased = count > 1.0 ? var_sum / (count - 1.0) : var_sum;
+            rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
+        }
+        if (save_mean) save_mean[c] = mean_f;
+        if (save_invstd) save_invstd[c] = invstd;
+    }
+}
+
+// ---- BatchNorm backward: g = dy*act'(y); sums (sum g, sum g*xhat); dx = w*invstd*(g - sg/N - xhat*sgx/N)
+template <int W>
+__global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const float* __restrict__ dy,
+                                                                  const float* __restrict__ y,
+                                                                  const float* __restrict__ x,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ invstd, int act, int C,
+                                                                  int HW, int64_t n, int64_t S,
+                                                                  double* __restrict__ part) {
+    __shared__ double red[kThreads / 64];
+    const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
+    const float mu = mean[c], is = invstd[c];
+    const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    float sg = 0.f, sgx = 0.f;
+    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
+        float g[W], yv[W], xv[W];
+        ld<W>(dy + o, g);
+        ld<W>(y + o, yv);
+        ld<W>(x + o, xv);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const float gj = g[j] * act_grad(act, yv[j]);
+            sg += gj;
+            sgx += gj * ((xv[j] - mu) * is);
+        }
+    });
+    const double a = block_sum((double)sg, red);
+    const double b = block_sum((double)sgx, red);
+    if (threadIdx.x == 0) {
+        part[((size_t)c * P + k) * 2 + 0] = a;
+        part[((size_t)c * P + k) * 2 + 1] = b;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __restrict__ dy,
+                                                                const float* __restrict__ y,
+                                                                const float* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ w, int act, int C, int HW,
+                                                                int64_t n, int64_t S, const double* __restrict__ sums,
+                                                                double count, float* __restrict__ dx) {
+    const int k = blockIdx.x, c = blockIdx.y;
+    const float mu = mean[c], is = invstd[c];
+    const float sgN = (float)(sums[2 * c] / count), sgxN = (float)(sums[2 * c + 1] / count);
+    const float kk = (w ? w[c] : 1.f) * is;
+    const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
+        float g[W], yv[W], xv[W], d[W];
+        ld<W>(dy + o, g);
+        ld<W>(y + o, yv);
+        ld<W>(x + o, xv);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const float gj = g[j] * act_grad(act, yv[j]);
+            d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
+        }
+        st<W>(dx + o, d);
+    });
+}
+
+// ---- fused-epilogue activation backward: dv = dy*act'(v); partial sums of dv and dy per (b,c,slice)
+template <int W>
+__global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
+                                                           const float* __restrict__ aval,
+                                                           const float* __restrict__ pre, int act, int C, int HW,
+                                                           int64_t S, float* dv,
+                                                           float* __restrict__ part) {
+    __shared__ float red[kThreads / 64];
+    const int k = blockIdx.x, plane = blockIdx.y, Q = gridDim.x;
+    const int b = plane / C, c = plane - b * C;
+    const int64_t e0 = (int64_t)b * HW + (int64_t)k * S;
+    const int64_t pe = (int64_t)b * HW + HW;
+    const int64_t e1 = e0 + S < pe ? e0 + S : pe;
+    float sd = 0.f, sg = 0.f;
+    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
+        float g[W], d[W];
+        ld<W>(dy + o, g);
+        if (act == LDM_ACT_GELU) {
+            float v[W];
+            ld<W>(pre + o, v);
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                const float cdf = 0.5f * (1.0f + erff(v[j] * 0.70710678118654752440f));
+                const float pdf = 0.39894228040143267794f * expf(-0.5f * v[j] * v[j]);
+                d[j] = g[j] * (cdf + v[j] * pdf);
+            }
+        } else if (aval) {
+            float a[W];
+            ld<W>(aval + o, a);
+#pragma unroll
+            for (int j = 0; j < W; ++j) d[j] = g[j] * act_grad(act, a[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) d[j] = g[j];
+        }
+        if (dv) st<W>(dv + o, d);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            sd += d[j];
+            sg += g[j];
+        }
+    });
+    if (part) {
+        sd = block_sum(sd, red);
+        sg = block_sum(sg, red);
+        if (threadIdx.x == 0) {
+            part[((size_t)plane * Q + k) * 2 + 0] = sd;
+            part[((size_t)plane * Q + k) * 2 + 1] = sg;
+        }
+    }
+}
+
+// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy   (fixed order)
+__global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float* __restrict__ part, int B, int C,
+                                                                    int Q, float* __restrict__ dbias,
+                                                                    float* __restrict__ dbcast) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float sb = 0.f;
+    for (int b = 0; b < B; ++b) {
+        const size_t pl = (size_t)b * C + c;
+        float sd = 0.f, sg = 0.f;
+        for (int k = 0; k < Q; ++k) {
+            sd += part[(pl * Q + k) * 2 + 0];
+            sg += part[(pl * Q + k) * 2 + 1];
+        }
+        sb += sd;
+        if (dbcast) dbcast[pl] = sg;
+    }
+    if (dbias) dbias[c] = sb;
+}
+
+bool vec_ok(int HW, const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr) {
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    return HW % 4 == 0 && al(a) && al(b) && al(c) && al(d);
+}
+
+}  // namespace
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW) {
+    if (B <= 0 || C <= 0 || HW <= 0) return 0;
+    const int64_t n = (int64_t)B * HW;
+    const int64_t bn = 2 * ((int64_t)C * bn_slices(n, C) * 2 + 2 * (int64_t)C);   // doubles -> floats
+    const int64_t ac = (int64_t)B * C * act_slices(B, C, HW) * 2;
+    return bn > ac ? bn : ac;
+}
+
+extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
+                                   void* stream) {
+    LDM_REQUIRE(x && stats && workspace && B > 0 && C > 0 && HW > 0, "batchnorm_stats: bad argument");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    double* part = reinterpret_cast<double*>(workspace);
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "batchnorm_stats: workspace must be 8-byte aligned");
+    const dim3 grid(P, C);
+    if (vec_ok(HW, x))
+        hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
+    else
+        hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
+    LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
+    hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       (hipStream_t)stream, part, C, P, stats, nullptr, nullptr);
+    LDM_CHECK_LAUNCH("slices_finalize_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
+                                   const float* weight, const float* bias, float* running_mean, float* running_var,
+                                   float momentum, float eps, int32_t act, float* save_mean, float* save_invstd,
+                                   void* stream) {
+    LDM_REQUIRE(x && stats && B > 0 && C > 0 && HW > 0 && count > 0.0, "batchnorm_apply: bad argument");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    const dim3 grid(P, C);
+    if (vec_ok(HW, x))
+        hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, stats,
+                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
+    else
+        hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, stats,
+                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
+    LDM_CHECK_LAUNCH("bn_apply_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
+                                   float* running_mean, float* running_var, float momentum, float eps, int32_t act,
+                                   float* save_mean, float* save_invstd, float* workspace, void* stream) {
+    LDM_REQUIRE(x && workspace && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
+    const int64_t n = (int64_t)B * HW;
+    double* stats = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
+    int rc = ldm_batchnorm_stats(x, B, C, HW, stats, workspace, stream);
+    if (rc) return rc;
+    return ldm_batchnorm_apply(x, B, C, HW, stats, (double)n, weight, bias, running_mean, running_var, momentum, eps,
+                               act, save_mean, save_invstd, stream);
+}
+
+extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
+                                             const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
+                                             double* sums, float* dweight, float* dbias, float* workspace,
+                                             void* stream) {
+    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && sums && workspace && B > 0 && C > 0 && HW > 0,
+                "bn_backward_reduce: bad argument");
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward_reduce: workspace must be 8-byte aligned");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    double* part = reinterpret_cast<double*>(workspace);
+    const dim3 grid(P, C);
+    if (vec_ok(HW, dy, y, x))
+        hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, act, C, HW, n, S, part);
+    else
+        hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, act, C, HW, n, S, part);
+    LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
+    // local sums: db = sum g, dw = sum g*xhat (SyncBatchNorm keeps the parameter grads local)
+    hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       (hipStream_t)stream, part, C, P, sums, dbias, dweight);
+    LDM_CHECK_LAUNCH("slices_finalize_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
+                                            const float* save_invstd, const float* weight, int32_t act, int32_t B,
+                                            int32_t C, int32_t HW, const double* sums, double count, float* dx,
+                                            void* stream) {
+    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && sums && dx && B > 0 && C > 0 && HW > 0 && count > 0.0,
+                "bn_backward_apply: bad argument");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    const dim3 grid(P, C);
+    if (vec_ok(HW, dy, y, x, dx))
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, weight, act, C, HW, n, S, sums, count, dx);
+    else
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, weight, act, C, HW, n, S, sums, count, dx);
+    LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
+    return 0;
+}
+
+extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
+                                      const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
+                                      int32_t HW, float* dx, float* dweight, float* dbias, float* workspace,
+                                      void* stream) {
+    LDM_REQUIRE(workspace && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
+    const int64_t n = (int64_t)B * HW;
+    double* sums = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
+    int rc = ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, act, B, C, HW, sums, dweight, dbias,
+                                           workspace, stream);
+    if (rc || !dx) return rc;
+    return ldm_batchnorm_backward_apply(dy, y, x, save_mean, save_invstd, weight, act, B, C, HW, sums, (double)n, dx,
+                                        stream);
+}
+
+extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
+                                int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
+                                void* stream) {
+    LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
+    LDM_REQUIRE(act != LDM_ACT_GELU || pre_act, "act_backward: GELU needs the pre-activation");
+    LDM_REQUIRE(act == LDM_ACT_NONE || act == LDM_ACT_GELU || act_out, "act_backward: needs the activation output");
+    const bool sums = dbias || dbcast;
+    LDM_REQUIRE(!sums || workspace, "act_backward: bias / bcast sums need the workspace");
+    const int Q = act_slices(B, C, HW);
+    const int64_t S = ((HW + Q - 1) / Q + 3) & ~3;
+    const dim3 grid(Q, B * C);
+    const float* aval = act == LDM_ACT_NONE || act == LDM_ACT_GELU ? nullptr : act_out;
+    float* part = sums ? workspace : nullptr;
+    if (vec_ok(HW, dy, aval, pre_act, dv))
+        hipLaunchKernelGGL(act_bwd_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, aval, pre_act, act, C,
+                           HW, S, dv, part);
+    else
+        hipLaunchKernelGGL(act_bwd_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, aval, pre_act, act, C,
+                           HW, S, dv, part);
+    LDM_CHECK_LAUNCH("act_bwd_kernel");
+    if (sums) {
+        hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                           (hipStream_t)stream, part, B, C, Q, dbias, dbcast);
+        LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
+    }
+    return 0;
+}

@@ -72,8 +72,12 @@ SIGNATURES = {
                                    ctypes.POINTER(Epilogue), c_fp, c_vp]),
     "ldm_conv_forward_ws": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp,
                                       ctypes.POINTER(Epilogue), c_fp, c_fp, c_vp]),
+    "ldm_reduce_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
-                                      c_int32, c_fp, c_fp, c_vp]),
+                                      c_int32, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_stats": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),
+    "ldm_batchnorm_apply": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, ctypes.c_double, c_fp, c_fp, c_fp, c_fp,
+                                      c_float, c_float, c_int32, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_eval": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_int32,
                                      c_vp]),
     "ldm_activation": (c_int32, [c_fp, c_fp, c_int64, c_int32, c_vp]),
@@ -102,9 +106,14 @@ SIGNATURES = {
     # backward / optimiser
     "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
-    "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
+                                   c_vp]),
     "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
-                                         c_fp, c_fp, c_fp, c_vp]),
+                                         c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward_reduce": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
+                                                c_vp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward_apply": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
+                                               c_vp, ctypes.c_double, c_fp, c_vp]),
     "ldm_attention_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          c_float, c_vp]),
     "ldm_unscale_check": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, c_fp, c_vp, c_vp]),

@@ -180,3 +180,15 @@ def broadcast_parameters(module, src=0, group=None):
         return
     for t in list(module.parameters()) + list(module.buffers()):
         tdist.broadcast(t.data, src=src, group=group)
+
+
+def convert_sync_batchnorm(module, group=True):
+    """SyncBatchNorm for the data-parallel train path (torch.nn.SyncBatchNorm.convert_sync_batchnorm
+    semantics, in place): every train-mode BatchNorm2d of `module` normalises with the batch statistics
+    of the whole process group (fp64 (sum x, sum x^2) and backward sums all-reduced between the two
+    stages of reduce.hip), so N ranks x B samples train like one process on N*B.  group=True means the
+    default group.  No effect in eval mode or single-process runs."""
+    for m in module.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.ldm_sync_group = group
+    return module

@@ -175,10 +175,12 @@ def batchnorm(x, bn_module, act="none"):
 
     def fwd_train(store, x_, w_, b_):
         y = ops.f32c(x_).clone()
-        sm, si = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps, act,
-                                      save=True)
+        sync = getattr(m, "ldm_sync_group", False)      # set by ldm_amd.dist.convert_sync_batchnorm
+        sm, si, count = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
+                                             act, save=True, sync=sync)
         store["saved"] = (x_, w_, b_, sm, si, y)
         store["act"] = act
+        store["sync"] = (sync, count)
         return y
 
     return hip_apply("batchnorm_train", fwd_train, x, m.weight, m.bias)
@@ -188,8 +190,10 @@ def batchnorm(x, bn_module, act="none"):
 def _bn_train_backward(ctx, gy):
     x, w, b, sm, si, y = ctx.saved_tensors
     nx, nw, nb = ctx.needs_input_grad[3:6]
+    sync, count = ctx.store.get("sync", (False, None))
     dx, dw, db = ops.batchnorm_backward(gy, y, x, sm, si, w, ctx.store["act"], need_dx=nx,
-                                        need_w=nw and w is not None, need_b=nb and b is not None)
+                                        need_w=nw and w is not None, need_b=nb and b is not None,
+                                        sync=sync, count=count)
     return dx, dw, db
 
 

@@ -261,20 +261,66 @@ def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=Fa
     dbc = torch.empty((B, C), device=dy.device, dtype=torch.float32) if need_bcast else None
     if act == "none" and not need_bias and not need_bcast:
         return dv, None, None
+    ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
     L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(pre_act), L.ACT[act], B, C, HW,
-           _p(dv) if act != "none" else None, _p(db), _p(dbc), stream_handle())
+           _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), stream_handle())
     return dv, db, dbc
 
 
-def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True):
+def reduce_workspace(B, C, HW, device):
+    """Scratch for the sliced per-channel reductions (reduce.hip)."""
+    return scratch("reduce", L.load().ldm_reduce_workspace_floats(B, C, HW), device)
+
+
+def _sync_group(group):
+    """The process group a SyncBatchNorm-marked module reduces over, or None (single process)."""
+    import torch.distributed as dist
+    if group is False or group is None or not dist.is_available() or not dist.is_initialized():
+        return None
+    g = None if group is True else group
+    return g if dist.get_world_size(g) > 1 else None
+
+
+def _allreduce_sum(t, group):
+    import torch.distributed as dist
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+
+def _global_count(n, group, device):
+    import torch.distributed as dist
+    c = torch.tensor([float(n)], device=device, dtype=torch.float64)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM, group=group)
+    return float(c.item())
+
+
+def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True,
+                       sync=False, count=None):
+    """Train-mode BN backward.  sync: SyncBatchNorm over the default group (True) or a given group, with
+    `count` = the global number of elements per channel saved by the forward."""
     dy = f32c(dy)
     B, C = dy.shape[0], dy.shape[1]
     HW = dy.numel() // max(1, B * C)
     dx = torch.empty_like(dy) if need_dx else None
     dw = torch.empty(C, device=dy.device, dtype=torch.float32) if need_w else None
     db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_b else None
-    L.call("ldm_batchnorm_backward", dy.data_ptr(), y.data_ptr(), f32c(x).data_ptr(), save_mean.data_ptr(),
-           save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db), stream_handle())
+    ws = reduce_workspace(B, C, HW, dy.device)
+    pg = _sync_group(sync)
+    if pg is None:
+        L.call("ldm_batchnorm_backward", dy.data_ptr(), y.data_ptr(), f32c(x).data_ptr(), save_mean.data_ptr(),
+               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db), ws.data_ptr(),
+               stream_handle())
+        return dx, dw, db
+    # SyncBatchNorm: local sums -> all-reduce -> dx with the global count (parameter grads stay local)
+    sums = torch.empty(2 * C, device=dy.device, dtype=torch.float64)
+    x = f32c(x)
+    L.call("ldm_batchnorm_backward_reduce", dy.data_ptr(), y.data_ptr(), x.data_ptr(), save_mean.data_ptr(),
+           save_invstd.data_ptr(), L.ACT[act], B, C, HW, sums.data_ptr(), _p(dw), _p(db), ws.data_ptr(),
+           stream_handle())
+    _allreduce_sum(sums, pg)
+    if dx is not None:
+        L.call("ldm_batchnorm_backward_apply", dy.data_ptr(), y.data_ptr(), x.data_ptr(), save_mean.data_ptr(),
+               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, sums.data_ptr(), float(count), dx.data_ptr(),
+               stream_handle())
     return dx, dw, db
 
 
@@ -290,7 +336,7 @@ def attention_backward(q, kv, dout, heads):
     return dq, dkv
 
 
-def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False):
+def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False, sync=False):
     """In-place train-mode BatchNorm2d (+activation); updates running stats like nn.BatchNorm2d."""
     require_device(x, weight, bias, running_mean, running_var)
     assert x.is_contiguous() and x.dtype == torch.float32
@@ -299,9 +345,24 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
     if save:
         sm = torch.empty(C, device=x.device, dtype=torch.float32)
         si = torch.empty(C, device=x.device, dtype=torch.float32)
-    L.call("ldm_batchnorm_train", x.data_ptr(), B, C, H * W, _p(weight), _p(bias), _p(running_mean),
-           _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si), stream_handle())
-    return (sm, si) if save else None
+    ws = reduce_workspace(B, C, H * W, x.device)
+    pg = _sync_group(sync)
+    if pg is None:
+        L.call("ldm_batchnorm_train", x.data_ptr(), B, C, H * W, _p(weight), _p(bias), _p(running_mean),
+               _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si), ws.data_ptr(),
+               stream_handle())
+        count = float(B * H * W)
+    else:
+        # SyncBatchNorm (torch.nn.SyncBatchNorm semantics): fp64 (sum x, sum x^2) all-reduced over the group,
+        # normalised with the global batch statistics; running stats use the global unbiased variance.
+        stats = torch.empty(2 * C, device=x.device, dtype=torch.float64)
+        L.call("ldm_batchnorm_stats", x.data_ptr(), B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
+        _allreduce_sum(stats, pg)
+        count = _global_count(B * H * W, pg, x.device)
+        L.call("ldm_batchnorm_apply", x.data_ptr(), B, C, H * W, stats.data_ptr(), count, _p(weight), _p(bias),
+               _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
+               stream_handle())
+    return (sm, si, count) if save else None
 
 
 def activation(x, act, inplace=False):

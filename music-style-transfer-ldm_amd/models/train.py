@@ -142,6 +142,7 @@ class LDMTrainer:
         self.reducer = None
         if hdist.world_size() > 1:
             hdist.broadcast_parameters(self.model)
+            hdist.convert_sync_batchnorm(self.model)      # global-batch BN statistics
             self.reducer = hdist.GradAllReduce(trainable_params)
             self.scaler.set_grad_divisor(hdist.world_size())
 
