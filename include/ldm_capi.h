@@ -106,8 +106,11 @@ int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float*
                         float* save_mean, float* save_invstd, float* workspace, void* stream);
 /* The same in two stages, for SyncBatchNorm (replaces torch.nn.SyncBatchNorm's batch_norm_stats /
  * batch_norm_gather_stats_with_counts / batch_norm_elemt for the data-parallel train path):
- * stats[2c] = sum x, stats[2c+1] = sum x^2 over this rank's batch (fp64) -> the caller all-reduces
- * stats over ranks -> apply with count = the global B*H*W. */
+ * stats[2c] = sum x, stats[2c+1] = sum x^2 over this rank's batch (fp64) and stats[2C] = this rank's
+ * B*H*W (stats holds 2C+1 doubles) -> the caller all-reduces all 2C+1 doubles over ranks (one collective;
+ * the count rides along) -> apply.  apply's count > 0 is used as given; count <= 0 reads the global count
+ * from stats[2C] on the device (no host synchronisation).  B may be 0 (an empty local shard joins the
+ * all-reduce with zero sums and still updates the running statistics). */
 int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
                         void* stream);
 int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
@@ -272,9 +275,9 @@ int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, cons
                            const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
                            int32_t HW, float* dx, float* dweight, float* dbias, float* workspace, void* stream);
 /* The same in two stages for SyncBatchNorm: sums[2c] = sum g, sums[2c+1] = sum g*xhat over this rank
- * (g = dy*act'(y)); dbias / dweight get these local sums (parameter grads stay local, as in
- * torch.nn.SyncBatchNorm; the DP gradient all-reduce averages them) -> the caller all-reduces sums ->
- * apply with count = the global B*H*W. */
+ * (g = dy*act'(y)) and sums[2C] = this rank's B*H*W (sums holds 2C+1 doubles); dbias / dweight get the
+ * local sums (parameter grads stay local, as in torch.nn.SyncBatchNorm; the DP gradient all-reduce
+ * averages them) -> the caller all-reduces all 2C+1 doubles -> apply (count <= 0: read sums[2C]). */
 int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
                                   const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
                                   double* sums, float* dweight, float* dbias, float* workspace, void* stream);

@@ -126,12 +126,15 @@ __global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const float*
     }
 }
 
-// stats[2c+j] = sum_k part[c][k][j] (slices in order); optional float copies out0/out1
+// stats[2c+j] = sum_k part[c][k][j] (slices in order); optional float copies out0/out1.  stats[2C] =
+// the element count per channel on this rank (n): all-reduced together with the sums, it becomes the
+// global count that the apply stages read on the device (no separate collective, no host sync).
 __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double* __restrict__ part, int C, int P,
                                                                    double* __restrict__ stats,
                                                                    float* __restrict__ out0,
-                                                                   float* __restrict__ out1) {
+                                                                   float* __restrict__ out1, double n) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0) stats[2 * C] = n;
     if (c >= C) return;
     double a = 0.0, b = 0.0;
     for (int k = 0; k < P; ++k) {
@@ -146,13 +149,14 @@ __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double*
 
 template <int W>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(float* __restrict__ x, int C, int HW, int64_t n, int64_t S,
-                                                            const double* __restrict__ stats, double count,
+                                                            const double* __restrict__ stats, double count_arg,
                                                             const float* __restrict__ weight,
                                                             const float* __restrict__ bias, float* __restrict__ rmean,
                                                             float* __restrict__ rvar, float momentum, float eps,
                                                             int act, float* __restrict__ save_mean,
                                                             float* __restrict__ save_invstd) {
     const int k = blockIdx.x, c = blockIdx.y;
+    const double count = count_arg > 0.0 ? count_arg : stats[2 * C];   // <= 0: the all-reduced count
     const double mean = stats[2 * c] / count;
     double var_sum = stats[2 * c + 1] - mean * stats[2 * c];   // sum (x - mean)^2
     if (var_sum < 0.0) var_sum = 0.0;
@@ -221,8 +225,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __r
                                                                 const float* __restrict__ invstd,
                                                                 const float* __restrict__ w, int act, int C, int HW,
                                                                 int64_t n, int64_t S, const double* __restrict__ sums,
-                                                                double count, float* __restrict__ dx) {
+                                                                double count_arg, float* __restrict__ dx) {
     const int k = blockIdx.x, c = blockIdx.y;
+    const double count = count_arg > 0.0 ? count_arg : sums[2 * C];
     const float mu = mean[c], is = invstd[c];
     const float sgN = (float)(sums[2 * c] / count), sgxN = (float)(sums[2 * c + 1] / count);
     const float kk = (w ? w[c] : 1.f) * is;
@@ -324,16 +329,17 @@ bool vec_ok(int HW, const void* a, const void* b = nullptr, const void* c = null
 using namespace ldm;
 
 extern "C" int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW) {
-    if (B <= 0 || C <= 0 || HW <= 0) return 0;
+    if (B < 0 || C <= 0 || HW <= 0) return 0;
+    if (B == 0) B = 1;   // an empty local shard (SyncBatchNorm) still runs the finalize stage
     const int64_t n = (int64_t)B * HW;
-    const int64_t bn = 2 * ((int64_t)C * bn_slices(n, C) * 2 + 2 * (int64_t)C);   // doubles -> floats
+    const int64_t bn = 2 * ((int64_t)C * bn_slices(n, C) * 2 + 2 * (int64_t)C + 2);   // doubles -> floats
     const int64_t ac = (int64_t)B * C * act_slices(B, C, HW) * 2;
     return bn > ac ? bn : ac;
 }
 
 extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
                                    void* stream) {
-    LDM_REQUIRE(x && stats && workspace && B > 0 && C > 0 && HW > 0, "batchnorm_stats: bad argument");
+    LDM_REQUIRE(stats && workspace && B >= 0 && C > 0 && HW > 0 && (x || B == 0), "batchnorm_stats: bad argument");
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
@@ -346,7 +352,7 @@ extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t
         hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
     LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
     hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       (hipStream_t)stream, part, C, P, stats, nullptr, nullptr);
+                       (hipStream_t)stream, part, C, P, stats, nullptr, nullptr, (double)n);
     LDM_CHECK_LAUNCH("slices_finalize_kernel");
     return 0;
 }
@@ -355,7 +361,7 @@ extern "C" int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, c
                                    const float* weight, const float* bias, float* running_mean, float* running_var,
                                    float momentum, float eps, int32_t act, float* save_mean, float* save_invstd,
                                    void* stream) {
-    LDM_REQUIRE(x && stats && B > 0 && C > 0 && HW > 0 && count > 0.0, "batchnorm_apply: bad argument");
+    LDM_REQUIRE(stats && B >= 0 && C > 0 && HW > 0 && (x || B == 0), "batchnorm_apply: bad argument");
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
@@ -386,7 +392,7 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
                                              const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
                                              double* sums, float* dweight, float* dbias, float* workspace,
                                              void* stream) {
-    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && sums && workspace && B > 0 && C > 0 && HW > 0,
+    LDM_REQUIRE(save_mean && save_invstd && sums && workspace && B >= 0 && C > 0 && HW > 0 && ((dy && y && x) || B == 0),
                 "bn_backward_reduce: bad argument");
     LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward_reduce: workspace must be 8-byte aligned");
     const int64_t n = (int64_t)B * HW;
@@ -403,7 +409,7 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
     LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
     // local sums: db = sum g, dw = sum g*xhat (SyncBatchNorm keeps the parameter grads local)
     hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       (hipStream_t)stream, part, C, P, sums, dbias, dweight);
+                       (hipStream_t)stream, part, C, P, sums, dbias, dweight, (double)n);
     LDM_CHECK_LAUNCH("slices_finalize_kernel");
     return 0;
 }
@@ -412,8 +418,9 @@ extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, con
                                             const float* save_invstd, const float* weight, int32_t act, int32_t B,
                                             int32_t C, int32_t HW, const double* sums, double count, float* dx,
                                             void* stream) {
-    LDM_REQUIRE(dy && y && x && save_mean && save_invstd && sums && dx && B > 0 && C > 0 && HW > 0 && count > 0.0,
+    LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 && ((dy && y && x && dx) || B == 0),
                 "bn_backward_apply: bad argument");
+    if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);

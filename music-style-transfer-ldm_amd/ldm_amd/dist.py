@@ -12,6 +12,8 @@ SURVEY.md §8(e):
     producing the gradients of earlier layers (overlap), and the 1/world averaging is folded into
     the GradScaler's unscale kernel (no extra pass over the gradients).
 """
+import contextlib
+
 import torch
 import torch.distributed as tdist
 
@@ -68,15 +70,24 @@ def gather_batch(x, n_total):
 def sharded_style_sample(model, z_T, style_spec, timesteps=100, eta=0.0):
     """style_ddim_sample_wrapper over a batch split across ranks: z_T [B,...] is the FULL starting
     noise (identical on every rank, e.g. from a seeded CPU generator as model.py:394 does), each rank
-    samples and decodes its shard, the decoded spectrograms are all-gathered.  Bit-identical to the
-    single-GPU result (the path is per-sample)."""
+    samples and decodes its shard, the decoded spectrograms are all-gathered.
+
+    The style encoder, UNet and sampler are per-sample, so each shard's latents equal the single-GPU
+    ones.  The decoder's BatchNorm layers couple the batch when the decoder is in train mode (the
+    reference samples that way, model.py:344-347 / tests.py:803-810): they are synchronised over the
+    group here, so the decoded batch equals the single-GPU result up to fp32 summation order.  A rank
+    whose shard is empty (B < world size) still joins those collectives."""
     B = z_T.shape[0]
     z = shard_batch(z_T).to(style_spec.device)
     s = shard_batch(style_spec)
     with torch.no_grad():
-        emb = model.style_encoder(s)
-        x, _ = model.style_conditioned_ddim_sample(z, emb, timesteps, eta)
-        dec = model.decoder(x, rescale=True)
+        if z.shape[0]:
+            emb = model.style_encoder(s)
+            x, _ = model.style_conditioned_ddim_sample(z, emb, timesteps, eta)
+        else:
+            x = z.float()
+        with batchnorm_sync(True):
+            dec = model.decoder(x, rescale=True)
     return gather_batch(dec.contiguous(), B)
 
 
@@ -184,11 +195,26 @@ def broadcast_parameters(module, src=0, group=None):
 
 def convert_sync_batchnorm(module, group=True):
     """SyncBatchNorm for the data-parallel train path (torch.nn.SyncBatchNorm.convert_sync_batchnorm
-    semantics, in place): every train-mode BatchNorm2d of `module` normalises with the batch statistics
-    of the whole process group (fp64 (sum x, sum x^2) and backward sums all-reduced between the two
-    stages of reduce.hip), so N ranks x B samples train like one process on N*B.  group=True means the
-    default group.  No effect in eval mode or single-process runs."""
+    semantics, in place): every BatchNorm2d of `module` that runs in training mode normalises with the
+    batch statistics of the whole process group (fp64 (sum x, sum x^2, count) and the backward sums
+    all-reduced between the two stages of reduce.hip, one collective each), so N ranks x B samples train
+    like one process on N*B.  group=True means the default group; group=False turns it off again.  No
+    effect in eval mode or single-process runs.  For rank-local use of a converted model (e.g. sampling
+    on rank 0 only) wrap the calls in ``batchnorm_sync(False)``: every rank must otherwise make the same
+    train-mode BatchNorm calls, in the same order, or the collectives wait for each other."""
     for m in module.modules():
         if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
             m.ldm_sync_group = group
     return module
+
+
+@contextlib.contextmanager
+def batchnorm_sync(group=True):
+    """Within the block, every train-mode BatchNorm uses `group` (True = default group, a ProcessGroup,
+    or False = local statistics), whatever convert_sync_batchnorm set on the module."""
+    from . import functional as HF
+    HF._SYNC_OVERRIDE.append(group)
+    try:
+        yield
+    finally:
+        HF._SYNC_OVERRIDE.pop()

@@ -153,6 +153,17 @@ def _activation_backward(ctx, gy):
     return (dv.reshape(x.shape),)
 
 
+_SYNC_OVERRIDE = []   # stack of group overrides pushed by ldm_amd.dist.batchnorm_sync
+
+
+def sync_group_for(m):
+    """SyncBatchNorm group of module m: the innermost batchnorm_sync(...) override, else the module's mark
+    (convert_sync_batchnorm), else False (local statistics)."""
+    if _SYNC_OVERRIDE:
+        return _SYNC_OVERRIDE[-1]
+    return getattr(m, "ldm_sync_group", False)
+
+
 def batchnorm(x, bn_module, act="none"):
     """nn.BatchNorm2d semantics (train: batch stats + running update; eval: running stats) + act."""
     m = bn_module
@@ -173,14 +184,18 @@ def batchnorm(x, bn_module, act="none"):
     rm = m.running_mean if (m.training and m.track_running_stats) else None
     rv = m.running_var if (m.training and m.track_running_stats) else None
 
+    # SyncBatchNorm only for a module in training mode (torch.nn.SyncBatchNorm semantics: eval-mode use of
+    # batch statistics, track_running_stats=False, stays local); the group comes from
+    # ldm_amd.dist.convert_sync_batchnorm or an enclosing ldm_amd.dist.batchnorm_sync(...) block.
+    sync = sync_group_for(m) if m.training else False
+
     def fwd_train(store, x_, w_, b_):
         y = ops.f32c(x_).clone()
-        sync = getattr(m, "ldm_sync_group", False)      # set by ldm_amd.dist.convert_sync_batchnorm
-        sm, si, count = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
-                                             act, save=True, sync=sync)
+        sm, si = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
+                                      act, save=True, sync=sync)
         store["saved"] = (x_, w_, b_, sm, si, y)
         store["act"] = act
-        store["sync"] = (sync, count)
+        store["sync"] = sync
         return y
 
     return hip_apply("batchnorm_train", fwd_train, x, m.weight, m.bias)
@@ -190,10 +205,9 @@ def batchnorm(x, bn_module, act="none"):
 def _bn_train_backward(ctx, gy):
     x, w, b, sm, si, y = ctx.saved_tensors
     nx, nw, nb = ctx.needs_input_grad[3:6]
-    sync, count = ctx.store.get("sync", (False, None))
     dx, dw, db = ops.batchnorm_backward(gy, y, x, sm, si, w, ctx.store["act"], need_dx=nx,
                                         need_w=nw and w is not None, need_b=nb and b is not None,
-                                        sync=sync, count=count)
+                                        sync=ctx.store.get("sync", False))
     return dx, dw, db
 
 

@@ -152,6 +152,9 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     desc = make_desc(B, Cin, H, W, Cout, kh, kw, stride, padding, output_padding, transposed)
     if desc.Hout <= 0 or desc.Wout <= 0:
         raise RuntimeError("conv: non-positive output size")
+    if B == 0:   # an empty batch shard (data-parallel sampling with B < world size): nothing to launch
+        return out if out is not None else torch.empty((0, Cout, desc.Hout, desc.Wout), device=x.device,
+                                                       dtype=torch.float32)
     plan = plan or get_plan(desc)
     wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
     y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
@@ -272,13 +275,21 @@ def reduce_workspace(B, C, HW, device):
     return scratch("reduce", L.load().ldm_reduce_workspace_floats(B, C, HW), device)
 
 
+class _Sync:
+    """A resolved SyncBatchNorm target: `pg` is the process group (None = the default group)."""
+
+    def __init__(self, pg):
+        self.pg = pg
+
+
 def _sync_group(group):
-    """The process group a SyncBatchNorm-marked module reduces over, or None (single process)."""
+    """The group a SyncBatchNorm-marked module reduces over as a _Sync, or None when the statistics stay
+    local (sync off, no process group, or a group of one rank).  group=True means the default group."""
     import torch.distributed as dist
     if group is False or group is None or not dist.is_available() or not dist.is_initialized():
         return None
     g = None if group is True else group
-    return g if dist.get_world_size(g) > 1 else None
+    return _Sync(g) if dist.get_world_size(g) > 1 else None
 
 
 def _allreduce_sum(t, group):
@@ -286,20 +297,14 @@ def _allreduce_sum(t, group):
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
-def _global_count(n, group, device):
-    import torch.distributed as dist
-    c = torch.tensor([float(n)], device=device, dtype=torch.float64)
-    dist.all_reduce(c, op=dist.ReduceOp.SUM, group=group)
-    return float(c.item())
-
-
 def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True,
-                       sync=False, count=None):
-    """Train-mode BN backward.  sync: SyncBatchNorm over the default group (True) or a given group, with
-    `count` = the global number of elements per channel saved by the forward."""
+                       sync=False):
+    """Train-mode BN backward.  sync: SyncBatchNorm over the default group (True) or a given group.  The
+    per-rank sums and the per-rank element count travel in ONE fp64 all-reduce of 2C+1 values; the apply
+    stage reads the global count on the device (reduce.hip), so there is no host synchronisation."""
     dy = f32c(dy)
     B, C = dy.shape[0], dy.shape[1]
-    HW = dy.numel() // max(1, B * C)
+    HW = max(1, math.prod(dy.shape[2:]))
     dx = torch.empty_like(dy) if need_dx else None
     dw = torch.empty(C, device=dy.device, dtype=torch.float32) if need_w else None
     db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_b else None
@@ -310,16 +315,17 @@ def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=Tr
                save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db), ws.data_ptr(),
                stream_handle())
         return dx, dw, db
-    # SyncBatchNorm: local sums -> all-reduce -> dx with the global count (parameter grads stay local)
-    sums = torch.empty(2 * C, device=dy.device, dtype=torch.float64)
+    # SyncBatchNorm: local sums (+ local count) -> all-reduce -> dx with the global count (parameter
+    # grads stay local, as in torch.nn.SyncBatchNorm)
+    sums = torch.empty(2 * C + 1, device=dy.device, dtype=torch.float64)
     x = f32c(x)
-    L.call("ldm_batchnorm_backward_reduce", dy.data_ptr(), y.data_ptr(), x.data_ptr(), save_mean.data_ptr(),
-           save_invstd.data_ptr(), L.ACT[act], B, C, HW, sums.data_ptr(), _p(dw), _p(db), ws.data_ptr(),
-           stream_handle())
-    _allreduce_sum(sums, pg)
-    if dx is not None:
+    L.call("ldm_batchnorm_backward_reduce", _p(dy if B else None), _p(y if B else None), _p(x if B else None),
+           save_mean.data_ptr(), save_invstd.data_ptr(), L.ACT[act], B, C, HW, sums.data_ptr(), _p(dw), _p(db),
+           ws.data_ptr(), stream_handle())
+    _allreduce_sum(sums, pg.pg)
+    if dx is not None and B:
         L.call("ldm_batchnorm_backward_apply", dy.data_ptr(), y.data_ptr(), x.data_ptr(), save_mean.data_ptr(),
-               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, sums.data_ptr(), float(count), dx.data_ptr(),
+               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, sums.data_ptr(), -1.0, dx.data_ptr(),
                stream_handle())
     return dx, dw, db
 
@@ -351,18 +357,19 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
         L.call("ldm_batchnorm_train", x.data_ptr(), B, C, H * W, _p(weight), _p(bias), _p(running_mean),
                _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si), ws.data_ptr(),
                stream_handle())
-        count = float(B * H * W)
     else:
-        # SyncBatchNorm (torch.nn.SyncBatchNorm semantics): fp64 (sum x, sum x^2) all-reduced over the group,
-        # normalised with the global batch statistics; running stats use the global unbiased variance.
-        stats = torch.empty(2 * C, device=x.device, dtype=torch.float64)
-        L.call("ldm_batchnorm_stats", x.data_ptr(), B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
-        _allreduce_sum(stats, pg)
-        count = _global_count(B * H * W, pg, x.device)
-        L.call("ldm_batchnorm_apply", x.data_ptr(), B, C, H * W, stats.data_ptr(), count, _p(weight), _p(bias),
+        # SyncBatchNorm (torch.nn.SyncBatchNorm semantics): fp64 (sum x, sum x^2, count) all-reduced over the
+        # group in one collective, normalised with the global batch statistics (the global count is read on
+        # the device); running stats use the global unbiased variance.  An empty local shard (B == 0) still
+        # joins the collective with zero sums and updates its running statistics like every other rank.
+        stats = torch.empty(2 * C + 1, device=x.device, dtype=torch.float64)
+        xp = x.data_ptr() if B else None
+        L.call("ldm_batchnorm_stats", xp, B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
+        _allreduce_sum(stats, pg.pg)
+        L.call("ldm_batchnorm_apply", xp, B, C, H * W, stats.data_ptr(), -1.0, _p(weight), _p(bias),
                _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
                stream_handle())
-    return (sm, si, count) if save else None
+    return (sm, si) if save else None
 
 
 def activation(x, act, inplace=False):

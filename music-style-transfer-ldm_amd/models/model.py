@@ -405,13 +405,16 @@ class LDM(nn.Module):
         times = torch.linspace(self.num_timesteps - 1, 0, timesteps).long()    # (model.py:420)
         return self._reverse(z_t, style_embedding, times, eta)
 
-    def content_style_transfer_wrapper(self, content_spec, style_spec, num_timesteps=250, eta=0.0):
+    def content_style_transfer_wrapper(self, content_spec, style_spec, num_timesteps=250, eta=0.0, noise=None):
+        """Encode content, q_sample it at T'-1, run the T'-step content/style loop, decode (reference
+        model.py:468-501).  `noise` (optional, [B, latent, H/8, W/8]) injects the q_sample epsilon that
+        the reference draws with randn_like (parity tests); by default it is drawn on the device."""
         content_spec = content_spec.float()
         style_spec = style_spec.float()
         z_0 = self.encoder(content_spec)
         t = torch.full((content_spec.shape[0],), num_timesteps - 1, dtype=torch.long)
         self.noise_scheduler._check_t(t)                                        # IndexError like model.py:107
-        z_t, noise = self.noise_scheduler(z_0, t.to(content_spec.device))
+        z_t, noise = self.noise_scheduler(z_0, t.to(content_spec.device), noise=noise)
         style_embedding = self.style_encoder(style_spec)
         sampled, _ = self.content_style_ddim_sample(z_t, style_embedding, num_timesteps, eta)
         decoded = self.decoder(sampled, rescale=True)

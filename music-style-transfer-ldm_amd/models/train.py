@@ -56,6 +56,21 @@ def _prepare_loaders(cfg):
 
 
 # ------------------------------------------------------------------------------------------------
+def autoencoder_step(encoder, decoder, optimizer, spectrogram, feature_extractor, reducer=None):
+    """One inner iteration of train_autoencoder (reference train.py:69-82): encode -> decode ->
+    compression_loss -> zero_grad -> backward (-> data-parallel gradient all-reduce) -> AdamW step.
+    Returns the loss tensor (the caller's .item() is the reference's host sync)."""
+    latent = encoder(spectrogram)
+    reconstructed = decoder(latent)
+    loss = compression_loss(spectrogram, reconstructed, latent, feature_extractor)
+    optimizer.zero_grad()
+    loss.backward()
+    if reducer is not None:
+        reducer.finish()
+    optimizer.step()
+    return loss
+
+
 def train_autoencoder(config, train_loader=None, test_loader=None, device=None):
     """VAE pre-training (reference train.py:28-138): encoder+decoder, AdamW, ReduceLROnPlateau,
     compression_loss with the configured feature extractor, best-val checkpointing."""
@@ -85,15 +100,8 @@ def train_autoencoder(config, train_loader=None, test_loader=None, device=None):
         decoder.train()
         for spectrogram in train_loader:
             spectrogram = spectrogram[0].to(device)
-            latent = encoder(spectrogram)
-            reconstructed = decoder(latent)
-            loss = compression_loss(spectrogram, reconstructed, latent, feature_extractor)
+            loss = autoencoder_step(encoder, decoder, optimizer, spectrogram, feature_extractor, reducer)
             running += loss.item()
-            optimizer.zero_grad()
-            loss.backward()
-            if reducer is not None:
-                reducer.finish()
-            optimizer.step()
         avg_train = running / max(1, len(train_loader))
         train_losses.append(avg_train)
 

@@ -1,6 +1,7 @@
 """Generate golden vectors by running the REFERENCE implementation on CPU (build container only).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py          # ref_goldens.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r2     # ref_goldens_r2.npz
 
 Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
 stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
@@ -201,5 +202,75 @@ def main():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
 
 
+def round2():
+    """Round-2 fixtures -> tests/golden/ref_goldens_r2.npz (the round-1 file is left untouched).
+
+    (8) content_style_transfer_wrapper end to end (model.py:468-501) at T'=100, eta=1 (config 5's
+        "100-step DDPM"), B=1, 128x128 content/style: the wrapper draws its q_sample noise with
+        torch.randn_like on the CPU generator right after torch.manual_seed(21) (nothing before it
+        consumes RNG), so the same epsilon is regenerated here and stored for injection.
+    (9) one train_autoencoder step (train.py:59-82): encoder + decoder in train mode (batch-statistics
+        BN in both, gradients through the whole encoder), loss = compression_loss with the LPIPS term
+        left out (weights are remote; loss.py:10) = MSE(recon, x) + 0.01 KL(latent), AdamW(lr=5e-4)."""
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+    with torch.no_grad():
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.eval()
+        content = torch.from_numpy(recipe.uniform01((1, 1, 128, 128), 720))
+        style = torch.from_numpy(recipe.uniform01((1, 1, 128, 128), 721))
+        torch.manual_seed(21)
+        decoded, z_t_decoded = ldm.content_style_transfer_wrapper(content, style, num_timesteps=100, eta=1.0)
+        torch.manual_seed(21)
+        eps = torch.randn((1, 32, 16, 16))
+        # self-check: the wrapper's z_t is q_sample(encoder(content), T'-1, eps)
+        z0 = ldm.encoder(content)
+        ab = ldm.noise_scheduler.alpha_bar_t[99]
+        zt = torch.sqrt(ab) * z0 + torch.sqrt(1 - ab) * eps
+        assert torch.allclose((ldm.decoder(zt)), z_t_decoded, atol=0, rtol=0)
+        G["cst100_eps"] = np32(eps)
+        G["cst100_decoded"] = np32(decoded)
+        G["cst100_zt_decoded"] = np32(z_t_decoded)
+
+    enc = M.SpectrogramEncoder(32)
+    dec = M.SpectrogramDecoder(32)
+    recipe.fill_module(enc, seed=730)
+    recipe.fill_module(dec, seed=731)
+    enc.train()
+    dec.train()
+    opt = torch.optim.AdamW(list(enc.parameters()) + list(dec.parameters()), lr=5e-4)
+    spec = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 732))
+    latent = enc(spec)
+    rec = dec(latent)
+    loss = torch.nn.MSELoss()(rec, spec) + 0.01 * L.kl_regularization_loss(latent)
+    opt.zero_grad()
+    loss.backward()
+    G["ae_latent"] = np32(latent)
+    G["ae_recon"] = np32(rec)
+    G["ae_loss"] = np32(loss)
+    named = dict([("encoder." + k, v) for k, v in enc.named_parameters()] +
+                 [("decoder." + k, v) for k, v in dec.named_parameters()])
+    for k in AE_KEYS:
+        G["ae_grad_" + k] = np32(named[k].grad)
+    opt.step()
+    for k in AE_KEYS:
+        G["ae_adamw1_" + k] = np32(named[k])
+    G["ae_enc_rm4"] = np32(enc.encoder[4].running_mean)
+    G["ae_dec_rv1"] = np32(dec.decoder[1].running_var)
+    path = os.path.join(HERE, "ref_goldens_r2.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
+AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.encoder.4.bias", "encoder.encoder.6.bias",
+           "encoder.encoder.7.weight", "decoder.decoder.0.weight", "decoder.decoder.1.bias", "decoder.decoder.4.weight",
+           "decoder.decoder.6.weight", "decoder.decoder.6.bias")
+
+
 if __name__ == "__main__":
-    main()
+    if "--r2" in sys.argv:
+        round2()
+    else:
+        main()

@@ -81,6 +81,47 @@ def _worker_grads(rank, world, port, q):
         tdist.destroy_process_group()
 
 
+def _worker_ldm_params(rank, world, port, q):
+    """GradAllReduce over the real LDM trainable-parameter list (UNet + StyleEncoder + Decoder, 9.77 M
+    params in ~25 MB buckets, encoder frozen as LDMTrainer sees it), then the 1/world divisor that
+    GradScaler.set_grad_divisor folds into its unscale: the result must be the mean of the ranks' grads."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "music-style-transfer-ldm_amd"))
+    import models.model as M
+    from ldm_amd import dist as D
+    _init(rank, world, port)
+    try:
+        torch.manual_seed(0)
+        ldm = M.LDM(32, pretrained_path="")
+        for p in ldm.encoder.parameters():
+            p.requires_grad_(False)
+        params = [p for p in ldm.parameters() if p.requires_grad]
+        red = D.GradAllReduce(params)
+        scale = 65536.0
+        ok = True
+        for step in range(2):
+            for p in params:
+                p.grad = None
+            # per-rank gradient G_r(p) = scale * rand(seed(step, rank, i)), delivered through autograd so the
+            # post-accumulate-grad hooks fire in backward order
+            loss = 0.0
+            for i, p in enumerate(params):
+                g = torch.Generator().manual_seed(1000 * step + 100 * rank + i)
+                loss = loss + (p * (torch.rand(p.shape, generator=g) * scale)).sum()
+            loss.backward()
+            red.finish()
+            inv = 1.0 / (scale * world)          # GradScaler.unscale_ with set_grad_divisor(world)
+            for i, p in enumerate(params):
+                exp = sum(torch.rand(p.shape, generator=torch.Generator().manual_seed(1000 * step + 100 * r + i))
+                          for r in range(world)) / world
+                ok &= bool(torch.allclose(p.grad * inv, exp, rtol=1e-6, atol=1e-6))
+        n = sum(p.numel() for p in params)
+        q.put((rank, ok, (len(red.buckets), n)))
+    finally:
+        tdist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -119,6 +160,14 @@ def test_bucketed_grad_allreduce_world2():
     res = _run(_worker_grads)
     assert all(r[1] for r in res), res
     assert res[0][2] > 1   # several buckets
+
+
+def test_grad_allreduce_ldm_parameter_list_world2():
+    res = _run(_worker_ldm_params)
+    assert all(r[1] for r in res), res
+    nb, n = res[0][2]
+    assert n == 6_841_504 + 2_729_984 + 198_209                                     # UNet + style + decoder
+    assert nb >= 2                                                                     # 39 MB in ~25 MB buckets
 
 
 if __name__ == "__main__":

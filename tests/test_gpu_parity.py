@@ -258,6 +258,18 @@ def test_split_chains_match_single_chain(M, cuda, split):
         assert rel_err(npy(b), npy(a)) < 1e-5
 
 
+def test_content_style_transfer_wrapper(ldm, goldens2, cuda):
+    """The config-5 entry point end to end (model.py:468-501): encode, q_sample at T'-1 with the
+    reference's epsilon (injected), 99-step eta=1 loop, (decoder+1)/2, and the undecorated decoder(z_t)."""
+    content = T(recipe.uniform01((1, 1, 128, 128), 720), cuda)
+    style = T(recipe.uniform01((1, 1, 128, 128), 721), cuda)
+    eps = T(goldens2["cst100_eps"], cuda)
+    with torch.no_grad():
+        decoded, ztd = ldm.content_style_transfer_wrapper(content, style, num_timesteps=100, eta=1.0, noise=eps)
+    assert rel_err(npy(decoded), goldens2["cst100_decoded"]) < TOL
+    assert rel_err(npy(ztd), goldens2["cst100_zt_decoded"]) < TOL
+
+
 def test_index_error_like_reference(ldm, cuda):
     style = T(recipe.uniform01((1, 1, 128, 128), 701), cuda)
     with pytest.raises(IndexError):

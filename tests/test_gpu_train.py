@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as tF
 
 import recipe
-from conftest import rel_err
+from conftest import adam_step_err, rel_err
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
@@ -298,3 +298,112 @@ def test_trainer_step_runs_and_decreases_loss(cuda):
     noise = torch.randn(2, 32, 16, 16, device=cuda)
     losses = [tr.train_step(content, style, t=t, noise=noise)["total_loss"] for _ in range(5)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+
+
+# ---- train_autoencoder ------------------------------------------------------------
+def test_autoencoder_step_matches_reference(goldens2, cuda):
+    """models.train.autoencoder_step (the inner iteration of train_autoencoder, reference train.py:69-82)
+    on the HIP path: train-mode BN in encoder and decoder, gradients through the whole encoder, fused
+    AdamW — against the reference's own step (tests/golden/make_goldens.py --r2, LPIPS term left out)."""
+    import models.model as M
+    import models.train as TR
+    from conftest import AE_KEYS
+    from ldm_amd import optim as hoptim
+    enc, dec = M.SpectrogramEncoder(32), M.SpectrogramDecoder(32)
+    recipe.fill_module(enc, seed=730)
+    recipe.fill_module(dec, seed=731)
+    enc, dec = enc.to(cuda), dec.to(cuda)
+    enc.train()
+    dec.train()
+    opt = hoptim.AdamW(list(enc.parameters()) + list(dec.parameters()), lr=5e-4)
+    spec = T(recipe.uniform01((2, 1, 128, 128), 732), cuda)
+    named = dict([("encoder." + k, v) for k, v in enc.named_parameters()] +
+                 [("decoder." + k, v) for k, v in dec.named_parameters()])
+    w0 = {k: npy(v) for k, v in named.items()}
+    loss = TR.autoencoder_step(enc, dec, opt, spec, None)
+    assert rel_err(npy(loss), goldens2["ae_loss"]) < TOL
+    # float64 restatement of the same step (oracle, fixture-pinned in test_oracle_golden.py).  The
+    # reference's own fp32 encoder gradients sit up to 6e-4 (relative to max) from float64: the train-mode
+    # BN backward subtracts the channel means of 32k-element sums.  So each gradient is held to
+    # max(1e-4, 3 x the reference's own fp32 error) against float64, and the conv biases that feed a
+    # train-mode BN (mathematically zero gradient) to 1e-4 of the largest weight gradient.
+    from oracle import ldm_torch_cpu as TC
+    sd64 = {k: torch.from_numpy(v).double().requires_grad_("running" not in k) for k, v in w0.items()}
+    for mod, pre in ((enc, "encoder."), (dec, "decoder.")):
+        rs = M.SpectrogramEncoder(32) if pre == "encoder." else M.SpectrogramDecoder(32)
+        recipe.fill_module(rs, seed=730 if pre == "encoder." else 731)
+        for k, v in rs.state_dict().items():
+            if "running" in k:
+                sd64[pre + k] = v.double()
+    x64 = spec.double().cpu()
+    lat = TC.encoder(sd64, x64, True, state={})
+    rec = TC.decoder(sd64, lat, True, state={})
+    (tF.mse_loss(rec, x64) + 0.01 * TC.kl_loss(lat)).backward()
+    gmax = max(np.abs(sd64[k].grad.numpy()).max() for k in ("encoder.encoder.0.weight", "encoder.encoder.3.weight"))
+    for k in AE_KEYS + ("encoder.encoder.0.bias", "encoder.encoder.3.bias"):
+        g64 = sd64[k].grad.numpy()
+        if k in ("encoder.encoder.0.bias", "encoder.encoder.3.bias", "encoder.encoder.6.bias"):
+            assert np.abs(npy(named[k].grad)).max() <= 1e-4 * gmax, k
+            continue
+        tol = max(TOL, 3 * rel_err(goldens2["ae_grad_" + k], g64))
+        assert rel_err(npy(named[k].grad), g64) < tol, (k, tol)
+    # AdamW's first step moves every element by ~lr * sign(g): elements with gradients inside the fp32
+    # noise may move the other way (conftest.adam_step_err); the pre-BN encoder bias has no signal at all
+    for k in AE_KEYS:
+        if k == "encoder.encoder.6.bias":
+            continue
+        assert adam_step_err(npy(named[k]), goldens2["ae_adamw1_" + k], goldens2["ae_grad_" + k], 5e-4,
+                             rel=2e-3) < 1e-5, k
+    assert rel_err(npy(enc.encoder[4].running_mean), goldens2["ae_enc_rm4"]) < TOL
+    assert rel_err(npy(dec.decoder[1].running_var), goldens2["ae_dec_rv1"]) < TOL
+
+
+def test_trainer_epochs_reporting_plateau_checkpoints(cuda, tmp_path, monkeypatch):
+    """LDMTrainer.train / train_epoch driver semantics (reference train.py:210-293): epoch averages times
+    config['training_iteration_noise'] (= 50, the reference's reporting multiplier), ReduceLROnPlateau fed
+    the epoch loss, ldm_{epoch}.pth written every 100 epochs (epoch 0 here) and loadable weights-only."""
+    import models.model as M
+    import models.train as TR
+    from models.config import config
+    monkeypatch.chdir(tmp_path)
+    torch.manual_seed(0)
+    ldm = M.LDM(32, pretrained_path="").to(cuda)
+    ldm.feature_loss_net = _ZeroFeat()
+    for p in ldm.encoder.parameters():
+        p.requires_grad_(False)
+    g = torch.Generator().manual_seed(5)
+    batches = [((torch.rand(2, 1, 128, 128, generator=g), torch.zeros(2)),
+                (torch.rand(2, 1, 128, 128, generator=g), torch.zeros(2))) for _ in range(3)]
+    tr = TR.LDMTrainer(ldm, batches, cuda, lr=1e-3)
+    tr.scheduler.patience = 0                    # let the plateau rule fire within 3 epochs
+    seen = []
+    step = tr.train_step
+
+    def spy(c, s, t=None, noise=None):
+        out = step(c, s, t, noise)
+        seen.append(out)
+        return out
+
+    tr.train_step = spy
+    losses, comp, den, sty = tr.train(3)
+    k = config["training_iteration_noise"]
+    assert k == 50 and len(losses) == 3 and len(seen) == 9
+    for e in range(3):
+        ep = seen[3 * e: 3 * e + 3]
+        assert losses[e] == pytest.approx(sum(o["total_loss"] for o in ep) / 3 * k, rel=1e-6)
+        assert den[e] == pytest.approx(sum(o["denoisinsg_loss"] for o in ep) / 3 * k, rel=1e-6)
+        assert comp[e] == pytest.approx(sum(o["compression_loss"] for o in ep) / 3 * k, rel=1e-6)
+    assert ldm.training
+    # plateau: the LR halves whenever the epoch loss did not improve (patience 0)
+    lr_expect = 1e-3
+    best = float("inf")
+    for e in range(3):
+        if losses[e] < best * (1 - 1e-4):
+            best = losses[e]
+        else:
+            lr_expect *= 0.5
+    assert tr.optimizer.param_groups[0]["lr"] == pytest.approx(lr_expect)
+    ck = tmp_path / "models" / "pretrained" / "ldm_0.pth"
+    assert ck.exists() and not (tmp_path / "models" / "pretrained" / "ldm_1.pth").exists()
+    sd = torch.load(str(ck), map_location="cpu", weights_only=True)
+    assert set(sd) == set(ldm.state_dict())

@@ -176,3 +176,50 @@ def test_train_step_gradients(ldm_sd, goldens):
         g = sd[k].grad
         g = g[:256] if g.dim() == 2 and g.shape[0] > 256 else g
         assert rel_err(g.numpy(), goldens["grad_" + k]) < 1e-4, k
+
+
+# ---- round-2 fixtures ------------------------------------------------------------------------------------
+def test_content_style_transfer_wrapper(ldm_sd, goldens2):
+    """content_style_transfer_wrapper (model.py:468-501) at T'=100, eta=1 with the recorded epsilon."""
+    ab = TC.schedule(200)[2]
+    content = torch.from_numpy(recipe.uniform01((1, 1, 128, 128), 720))
+    style = torch.from_numpy(recipe.uniform01((1, 1, 128, 128), 721))
+    eps = torch.from_numpy(goldens2["cst100_eps"])
+    with torch.no_grad():
+        z0 = TC.encoder(ldm_sd, content)
+        zt = TC.q_sample(ab, z0, torch.tensor([99]), eps)
+        emb = TC.style_encoder(ldm_sd, style)
+        x = TC.reverse_loop(ldm_sd, ab, zt, emb["s5"], emb["s6"], TC.content_times(100), 1.0)
+        dec = (TC.decoder(ldm_sd, x) + 1) / 2
+        ztd = TC.decoder(ldm_sd, zt)
+    assert rel_err(dec.numpy(), goldens2["cst100_decoded"]) < 1e-5
+    assert rel_err(ztd.numpy(), goldens2["cst100_zt_decoded"]) < 2e-6
+
+
+def test_autoencoder_step(M, goldens2):
+    """One train_autoencoder step (train.py:59-82) restated: train-mode BN in encoder and decoder,
+    MSE + 0.01 KL (LPIPS term out of scope), torch AdamW(lr=5e-4)."""
+    from conftest import AE_KEYS
+    sde = {"encoder." + k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k)
+           for k, v in sd_for(lambda: M.SpectrogramEncoder(32), 730).items()}
+    sdd = {"decoder." + k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k)
+           for k, v in sd_for(lambda: M.SpectrogramDecoder(32), 731).items()}
+    sd = {**sde, **sdd}
+    spec = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 732))
+    state = {}
+    lat = TC.encoder(sd, spec, True, state=state)
+    rec = TC.decoder(sd, lat, True, state=state)
+    loss = torch.nn.functional.mse_loss(rec, spec) + 0.01 * TC.kl_loss(lat)
+    loss.backward()
+    assert rel_err(lat.detach().numpy(), goldens2["ae_latent"]) < 2e-6
+    assert rel_err(rec.detach().numpy(), goldens2["ae_recon"]) < 2e-6
+    assert rel_err(loss.detach().numpy(), goldens2["ae_loss"]) < 2e-6
+    for k in AE_KEYS:
+        assert rel_err(sd[k].grad.numpy(), goldens2["ae_grad_" + k]) < 1e-4, k
+    params = [v for k, v in sd.items() if v.requires_grad]
+    opt = torch.optim.AdamW(params, lr=5e-4)
+    opt.step()
+    for k in AE_KEYS:
+        assert rel_err(sd[k].detach().numpy(), goldens2["ae_adamw1_" + k]) < 1e-6, k
+    assert rel_err(state["encoder.encoder.4.running_mean"].numpy(), goldens2["ae_enc_rm4"]) < 2e-6
+    assert rel_err(state["decoder.decoder.1.running_var"].numpy(), goldens2["ae_dec_rv1"]) < 2e-6
