@@ -221,6 +221,12 @@ typedef struct ldm_unet_weights {
     const float* fold_w[2];
     const float* fold_pb[2];
     int32_t use_fold;
+    /* Step kernels of the reverse loop (uconv.hip; used when use_step != 0 together with use_fold, for
+     * latent C = 32 and num_filters = 64): the nine convs packed by ldm_step_pack_weight (enc4 /
+     * bottleneck: their folded weights), and the folded position biases transposed to [Hout*Wout][Cout]. */
+    const float* step_w[9];
+    const float* step_pb[2];
+    int32_t use_step;
 } ldm_unet_weights;
 
 typedef struct ldm_unet_shape {
@@ -254,6 +260,17 @@ int64_t ldm_ddim_workspace_floats(const ldm_unet_shape* s, const ldm_unet_weight
 int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x, const float* s5,
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
                     float* x0_logs, float* eps_logs, int64_t log_step_stride, float* workspace, void* stream);
+
+/* ---- step kernels (uconv.hip): fixed-structure implicit GEMMs of the nine UNet convs -------------------
+ * Packed size (floats) of layer `layer` (0..8 = enc1..dec1) and its packing from the torch weight layout
+ * (conv [Cout][Cin][3][3], transposed conv [Cin][Cout][3][3]).  ldm_step_conv runs one layer on NHWC
+ * activations (latent [B,H,W] with H, W multiples of 8): y = act(conv(x) + bias) (+ bcast[b][c] for
+ * enc2) (+ skip for dec4..dec2); bias is [Cout], or [Hout*Wout][Cout] for the folded enc4 / bottleneck.
+ * dec1 only runs fused with the DDIM update inside ldm_ddim_sample. */
+int64_t ldm_step_packed_floats(int32_t layer);
+int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream);
+int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                  const float* bias, const float* bcast, const float* skip, float* y, void* stream);
 
 /* ---- train step backward (LDMTrainer.train_step, train.py:163-208: scaler.scale(loss).backward()) ---
  * Data gradients of a conv are the forward kernel on the dual descriptor (conv <-> transposed conv);

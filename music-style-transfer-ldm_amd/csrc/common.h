@@ -128,6 +128,23 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
 int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
                         int32_t S, float scale, float* kf, float* bf, hipStream_t st);
 
+// uconv.hip: the step kernels of the reverse loop (NHWC activations, see ldm_capi.h)
+struct StepConv {
+    const float* x;
+    const float* w;
+    float* y;
+    const float* bias;    // [Cout] or, for enc4 / bottleneck, the folded position bias [Hout*Wout][Cout]
+    const float* bcast;   // enc2: t_emb [B][128]
+    const float* skip;    // dec4..dec2
+    const float* coef;    // dec1: DDIM coefficients of the step
+    float eta;
+    float* xs;            // dec1: sampler state (NHWC), updated in place
+    float* x0_log;        // dec1: NCHW logs (or NULL)
+    float* eps_log;
+};
+int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
+int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
+
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.
 __device__ __forceinline__ float ddim_update(float xv, float e, const float* coef, float eta, float& x0) {

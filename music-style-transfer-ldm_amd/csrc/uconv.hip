@@ -1,0 +1,533 @@
+// Step kernels of the reverse loop: the nine convolutions of UNet.forward (model.py:178-194, :205-229)
+// as fixed-structure implicit GEMMs for gfx950, used by ldm_ddim_sample when use_step != 0.
+//
+// Why a second conv family next to conv.hip: at the sampling batch (B = 8 on a 16x64 latent) every layer
+// is a 0.3-0.6 GFLOP GEMM whose output is only 64K-512K values, so a launch is ~256 blocks that each own
+// one output tile and split K over their waves.  conv.hip's general kernel (runtime tap tables, phase
+// tables, K cursors, split-K hand-off) spends most of such a launch on dependent operand rounds and
+// address arithmetic.  Here the channel counts, the tap structure and the per-wave K range are template
+// constants, so:
+//   * the K order is channel-chunk major, tap minor (chunk c = cc*9 + tap): a wave's chunk range is a
+//     whole number of channel chunks times the 9 taps, every chunk's tap is a compile-time constant, and
+//     the per-lane input offset of each tap is computed once — the K loop is loads + MFMAs only;
+//   * every operand load of a stage is issued before the first MFMA of that stage (one memory round trip
+//     per stage; most layers are a single stage, so the whole K range is in flight at once);
+//   * activations are NHWC: a lane's 4 channels of a 16-channel chunk are one 16-byte load, and the
+//     16x16 accumulator rows of a lane (4 consecutive output channels) are one 16-byte store.
+// The stride-2 transposed convolutions (dec4..dec2) run over the INPUT grid with 4 accumulator sets, one
+// per output parity: tap (ky, kx) of ConvTranspose2d(k3, s2, p1, op1) reads input (qy + [ky==0],
+// qx + [kx==0]) and feeds output (2qy + [ky!=1], 2qx + [kx!=1]) — every block carries the same 9-tap K,
+// so the four parities need no separate (unequal) launches.
+//
+// MFMA: v_mfma_f32_16x16x4_f32 (exact fp32, = an fmaf chain, cdna_hip_programming.md §3).  Lane l holds
+// A[row = l & 15][k] and B[k][col = l & 15] for its lane group lg = l >> 4; within a 16-channel chunk,
+// MFMA step j uses k-local channel 4*lg + j.  D: row 4*lg + r, col l & 15.
+// Summation order differs from torch's (K blocked over waves, fixed order), well inside 1e-4.
+#include <type_traits>
+#include <utility>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace ldm {
+namespace uc {
+
+enum : int { EPI_RELU = 1, EPI_BCAST = 2, EPI_SKIP = 4, EPI_POSB = 8, EPI_DDIM = 16 };
+
+struct UArgs {
+    const float* x;       // NHWC [B, Hin, Win, CIN]
+    const float* w;       // packed [9*CIN/16][COUT][16]
+    float* y;             // NHWC [B, Hout, Wout, COUT] (unused with EPI_DDIM)
+    const float* bias;    // [COUT], or with EPI_POSB [Hout*Wout][COUT]
+    const float* bcast;   // [B][COUT]
+    const float* skip;    // NHWC like y
+    const float* coef;    // EPI_DDIM: [4] {sqrt(ab_t), sqrt(1-ab_t), sqrt(ab_n), sqrt(1-ab_n)}
+    float* xs;            // EPI_DDIM: sampler state x, NHWC, updated in place
+    float* x0_log;        // EPI_DDIM: pred_x0 log, NCHW [B, COUT, Hout, Wout] (or NULL)
+    float* eps_log;       // EPI_DDIM: noise_pred log, NCHW (or NULL)
+    float eta;
+    int32_t B, Hin, Win, Hout, Wout;
+    int32_t Hq, Wq, Nq;   // column grid: output pixels (conv) or input pixels (transposed)
+    int32_t nMt, nNt, order;
+    FastDiv fd_hw, fd_w, fd_mt, fd_nt;
+};
+
+// (ky, kx) of tap t and the conv input offset / the transposed conv's output parity
+__host__ __device__ constexpr int tky(int t) { return t / 3; }
+__host__ __device__ constexpr int tkx(int t) { return t % 3; }
+__host__ __device__ constexpr int tphase(int t) { return (tky(t) != 1 ? 2 : 0) + (tkx(t) != 1 ? 1 : 0); }
+
+// Diagnostic builds only (never shipped; tools/step_diag.sh): UCONV_DIAG bit 0 = no MFMAs, bit 1 = no
+// operand loads, bit 2 = per-block timestamps of wave 0 (entry and exit in 100 MHz wall ticks, the
+// phases between in shader clocks) into g_uconv_stamps, read back with ldm_debug_uconv_stamps.
+#ifndef UCONV_DIAG
+#define UCONV_DIAG 0
+#endif
+#if (UCONV_DIAG & 4)
+__device__ unsigned long long g_uconv_stamps[4096][5];
+#define UCONV_STAMP(k)                                                                                 \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < 4096u)                                                    \
+            g_uconv_stamps[blockIdx.x][k] = ((k) == 0 || (k) == 4) ? __builtin_amdgcn_s_memrealtime() \
+                                                                   : __builtin_amdgcn_s_memtime();    \
+    } while (0)
+#else
+#define UCONV_STAMP(k) \
+    do {               \
+    } while (0)
+#endif
+
+// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
+__global__ __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu((WN * WK + 3) / 4, (WN * WK + 3) / 4)))
+void uconv_kernel(UArgs a) {
+    constexpr int NPH = MODE == 2 ? 4 : 1;
+    constexpr int NST = NCH / S;
+    constexpr int CPC = 9;                        // chunks per channel chunk (the 9 taps)
+    static_assert(NCH % S == 0 && NCH % CPC == 0, "stage / chunk structure");
+    static_assert(CIN % 16 == 0 && COUT % (16 * TM) == 0, "channel tiling");
+    static_assert((9 * CIN / 16) == NCH * WK, "the block's waves cover K exactly once");
+    // a lone accumulator chain of 16x16x4 (40-cycle dependent latency, 32-cycle issue) alternates two
+    constexpr int NACC2 = (NPH * TM * TN == 1) ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    UCONV_STAMP(0);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wn = wave % WN, wk = wave / WN;
+    const int col = lane & 15, lg = lane >> 4;
+
+    // block -> (M tile, N tile)
+    int mt, nt;
+    {
+        const int bid = blockIdx.x;
+        const int q1 = a.fd_mt.div(bid), q2 = a.fd_nt.div(bid);
+        mt = a.order == 0 ? bid - q1 * a.nMt : q2;
+        nt = a.order == 0 ? q1 : bid - q2 * a.nNt;
+    }
+    const int m0 = mt * (16 * TM);
+    const int nbase = nt * (16 * TN * WN) + wn * (16 * TN);
+
+    // per column: (b, qy, qx) and the per-tap input byte offsets (kOOB: padding / outside the image)
+    constexpr int kOOB = 0x7ffffff0;
+    int vt[9][TN];
+    int cb[TN], cqy[TN], cqx[TN];
+    bool cval[TN];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+        const int n = nbase + 16 * ni + col;
+        const bool nv = n < a.Nq;
+        const int nn = nv ? n : 0;
+        const int b = a.fd_hw.div(nn);
+        const int r = nn - b * (a.Hq * a.Wq);
+        const int qy = a.fd_w.div(r);
+        const int qx = r - qy * a.Wq;
+        cb[ni] = b;
+        cqy[ni] = qy;
+        cqx[ni] = qx;
+        cval[ni] = nv;
+        const int iy0 = MODE == 0 ? qy - 1 : (MODE == 1 ? 2 * qy - 1 : qy);
+        const int ix0 = MODE == 0 ? qx - 1 : (MODE == 1 ? 2 * qx - 1 : qx);
+        const int base = ((b * a.Hin + iy0) * a.Win + ix0) * (CIN * 4) + lg * 16;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ky = tky(t), kx = tkx(t);
+            const int dy = MODE == 2 ? (ky == 0 ? 1 : 0) : ky;
+            const int dx = MODE == 2 ? (kx == 0 ? 1 : 0) : kx;
+            const bool ok = nv && (unsigned)(iy0 + dy) < (unsigned)a.Hin && (unsigned)(ix0 + dx) < (unsigned)a.Win;
+            vt[t][ni] = ok ? base + (dy * a.Win + dx) * (CIN * 4) : kOOB;
+        }
+    }
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.x), (short)0, uni(a.B * a.Hin * a.Win * CIN * 4), 0x00020000);
+    constexpr int WBYTES = 9 * CIN * COUT * 4;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, WBYTES, 0x00020000);
+    const int va = (m0 + col) * 64 + lg * 16;                 // A: row m0+col, k-local 4*lg .. +3
+    const int sa0 = uni(wk * NCH * COUT * 64);                 // first chunk of this wave
+    const int sb0 = uni(wk * (NCH / CPC) * 64);                // its first channel chunk (16 ch x 4 B)
+
+    floatx4 acc[NACC2][NPH][TM][TN];
+#pragma unroll
+    for (int u = 0; u < NACC2; ++u)
+#pragma unroll
+        for (int p = 0; p < NPH; ++p)
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) acc[u][p][mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    floatx4 fa[NST > 1 ? 2 : 1][S][TM], fb[NST > 1 ? 2 : 1][S][TN];
+    auto load_stage = [&](auto stc) {
+        constexpr int st = decltype(stc)::value;
+        constexpr int bf = NST > 1 ? (st & 1) : 0;
+        static_for<0, S>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int c = st * S + i;                 // chunk within this wave's range
+            constexpr int t = c % CPC, cc = c / CPC;
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+                fa[bf][i][mi] = (UCONV_DIAG & 2) ? floatx4{(float)(va + c), 0.f, 1.f, 2.f}
+                                                 : __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                                   wr, va, sa0 + c * COUT * 64 + mi * 1024, 0));
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                fb[bf][i][ni] = (UCONV_DIAG & 2) ? floatx4{(float)vt[t][ni], 1.f, 2.f, 3.f}
+                                                 : __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                                   xr, vt[t][ni], sb0 + cc * 64, 0));
+            __builtin_amdgcn_sched_barrier(0);        // chunks issue in consumption order
+        });
+    };
+    auto compute_stage = [&](auto stc) {
+        constexpr int st = decltype(stc)::value;
+        constexpr int bf = NST > 1 ? (st & 1) : 0;
+        static_for<0, S>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int c = st * S + i;
+            constexpr int p = MODE == 2 ? tphase(c % CPC) : 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const int u = NACC2 == 2 ? (j & 1) : 0;
+                        if constexpr ((UCONV_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
+                            if (j == 0) acc[u][p][mi][ni][0] = acc[u][p][mi][ni][0] + fa[bf][i][mi][j] * fb[bf][i][ni][j];
+                        } else {
+                            acc[u][p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                fa[bf][i][mi][j], fb[bf][i][ni][j], acc[u][p][mi][ni], 0, 0, 0);
+                        }
+                    }
+        });
+    };
+    // Epilogue operands of the fragments this thread finishes — fragment f = k*WK + wk for k < NMY (all
+    // of them when WK == 1) — loaded right after the last operand stage is issued: they arrive while the
+    // MFMAs run and never hold up an operand wait.  Branch-free (a fragment index past NFR is clamped
+    // and its result dropped), so the waitcnt pass sees one straight-line load sequence.
+    constexpr int NFR = NPH * TM * TN;   // accumulator fragments per wave
+    constexpr int NMY = (NFR + WK - 1) / WK;
+    static_assert(TN <= 2, "column selects below assume TN <= 2");
+    auto frag = [&](int k) { return WK == 1 ? k : k * WK + wk; };
+    // (a bitwise blend of two scalars: a ?: over array elements gets folded into a dynamically indexed
+    // array, which lives in scratch memory)
+    auto colsel = [&](const auto& arr, int ni) -> int {
+        const int v0 = (int)arr[0], v1 = (int)arr[TN - 1];
+        return TN == 1 ? v0 : (v0 ^ ((v0 ^ v1) & -(int)(ni != 0)));
+    };
+    struct Out {
+        int b, oy, ox, pix, m;
+        bool ok;
+    };
+    auto out_of = [&](int f) {
+        const int fc = f < NFR ? f : NFR - 1;
+        const int p = fc / (TM * TN), mi = (fc / TN) % TM, ni = fc % TN;
+        Out o;
+        o.b = colsel(cb, ni);
+        o.oy = MODE == 2 ? 2 * colsel(cqy, ni) + (p >> 1) : colsel(cqy, ni);
+        o.ox = MODE == 2 ? 2 * colsel(cqx, ni) + (p & 1) : colsel(cqx, ni);
+        o.pix = (o.b * a.Hout + o.oy) * a.Wout + o.ox;
+        o.m = m0 + 16 * mi + 4 * lg;
+        o.ok = f < NFR && colsel(cval, ni) != 0;
+        return o;
+    };
+    floatx4 pre_b[NMY], pre_c[NMY], pre_s[NMY];
+    auto epi_prefetch = [&]() {
+        static_for<0, NMY>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const Out o = out_of(frag(k));
+            pre_b[k] = (EPI & EPI_POSB)
+                           ? *reinterpret_cast<const floatx4*>(a.bias + (size_t)(o.oy * a.Wout + o.ox) * COUT + o.m)
+                           : *reinterpret_cast<const floatx4*>(a.bias + o.m);
+            if constexpr ((EPI & EPI_BCAST) != 0) pre_c[k] = *reinterpret_cast<const floatx4*>(a.bcast + (size_t)o.b * COUT + o.m);
+            if constexpr ((EPI & EPI_SKIP) != 0) pre_s[k] = *reinterpret_cast<const floatx4*>(a.skip + (size_t)o.pix * COUT + o.m);
+            if constexpr ((EPI & EPI_DDIM) != 0) pre_s[k] = *reinterpret_cast<const floatx4*>(a.xs + (size_t)o.pix * COUT + o.m);
+        });
+    };
+
+    // scheduling fences keep each stage's loads ahead of the MFMAs that consume the previous stage (the
+    // default scheduler would interleave them to save registers and expose one latency per chunk); the
+    // waitcnt pass then waits progressively, chunk by chunk, in issue order
+    UCONV_STAMP(1);
+    load_stage(std::integral_constant<int, 0>{});
+    if constexpr (NST == 1) epi_prefetch();
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, NST>([&](auto stc) {
+        constexpr int st = decltype(stc)::value;
+        if constexpr (st + 1 < NST) {
+            load_stage(std::integral_constant<int, st + 1>{});
+            if constexpr (st + 2 == NST) epi_prefetch();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute_stage(stc);
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (NACC2 == 2) {
+#pragma unroll
+        for (int p = 0; p < NPH; ++p)
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) acc[0][p][mi][ni] = acc[0][p][mi][ni] + acc[1][p][mi][ni];
+    }
+
+    UCONV_STAMP(2);
+    // ---- in-block K reduction (fixed order) and the fused epilogue ------------------------------------
+    floatx4* red = reinterpret_cast<floatx4*>(smem);
+    if constexpr (WK > 1) {
+        static_for<0, NFR>([&](auto fc) {
+            constexpr int f = decltype(fc)::value;
+            constexpr int p = f / (TM * TN), mi = (f / TN) % TM, ni = f % TN;
+            red[((wk * WN + wn) * NFR + f) * 64 + lane] = acc[0][p][mi][ni];
+        });
+        __syncthreads();
+    }
+    UCONV_STAMP(3);
+    static_for<0, NMY>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int f = frag(k);
+        floatx4 v;
+        if constexpr (WK > 1) {
+            const int fc = f < NFR ? f : NFR - 1;
+            v = red[((0 * WN + wn) * NFR + fc) * 64 + lane];
+#pragma unroll
+            for (int k2 = 1; k2 < WK; ++k2) v = v + red[((k2 * WN + wn) * NFR + fc) * 64 + lane];
+        } else {
+            constexpr int p = k / (TM * TN), mi = (k / TN) % TM, ni = k % TN;
+            v = acc[0][p][mi][ni];
+        }
+        const Out ot = out_of(f);
+        if (!ot.ok) return;
+        const floatx4 bias = pre_b[k];
+        floatx4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float sv = v[r] + bias[r];
+            if (EPI & EPI_RELU) sv = sv < 0.f ? 0.f : sv;
+            o[r] = sv;
+        }
+        if constexpr ((EPI & EPI_BCAST) != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = o[r] + pre_c[k][r];
+        }
+        if constexpr ((EPI & EPI_SKIP) != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = o[r] + pre_s[k][r];
+        }
+        if constexpr ((EPI & EPI_DDIM) != 0) {
+            // noise_pred = o; the reverse update of model.py:442-458 (ddim_update, one rounding per op)
+            const floatx4 xv = pre_s[k];
+            floatx4 xn;
+            const size_t hw = (size_t)a.Hout * a.Wout;
+            const size_t lbase = ((size_t)ot.b * COUT + ot.m) * hw + (size_t)ot.oy * a.Wout + ot.ox;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x0;
+                xn[r] = ddim_update(xv[r], o[r], a.coef, a.eta, x0);
+                if (a.x0_log) a.x0_log[lbase + r * hw] = x0;
+                if (a.eps_log) a.eps_log[lbase + r * hw] = o[r];
+            }
+            *reinterpret_cast<floatx4*>(a.xs + (size_t)ot.pix * COUT + ot.m) = xn;
+        } else {
+            *reinterpret_cast<floatx4*>(a.y + (size_t)ot.pix * COUT + ot.m) = o;
+        }
+    });
+    UCONV_STAMP(4);
+}
+
+// packed[c][m][16], c = cc*9 + t, element e = 4*lg + j  ->  input channel cc*16 + e, tap t = ky*3 + kx.
+// conv: w [COUT][CIN][3][3]; transposed conv: w [CIN][COUT][3][3] (torch layouts).
+__global__ __launch_bounds__(256) void uconv_pack_kernel(const float* __restrict__ w, float* __restrict__ out,
+                                                         int CIN, int COUT, int transposed) {
+    const int64_t total = (int64_t)9 * CIN * COUT;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int e = (int)(idx % 16);
+    const int m = (int)((idx / 16) % COUT);
+    const int c = (int)(idx / (16 * (int64_t)COUT));
+    const int cc = c / 9, t = c % 9;
+    const int ci = cc * 16 + e;
+    out[idx] = transposed ? w[((int64_t)ci * COUT + m) * 9 + t] : w[((int64_t)m * CIN + ci) * 9 + t];
+}
+
+// NCHW <-> NHWC for the sampler state (once before / after the loop)
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x, float* __restrict__ y, int C,
+                                                           int HW, int64_t n) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over y (NHWC)
+    if (idx >= n) return;
+    const int c = (int)(idx % C);
+    const int64_t r = idx / C;
+    const int p = (int)(r % HW);
+    const int64_t b = r / HW;
+    y[idx] = x[(b * C + c) * HW + p];
+}
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float* __restrict__ x, float* __restrict__ y, int C,
+                                                           int HW, int64_t n) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over y (NCHW)
+    if (idx >= n) return;
+    const int p = (int)(idx % HW);
+    const int64_t r = idx / HW;
+    const int c = (int)(r % C);
+    const int64_t b = r / C;
+    y[idx] = x[(b * HW + p) * C + c];
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Layer table: the instance each of the nine layers runs (the batch only changes the grid).
+// Chosen so that at the sampling batch (B = 8, 16x64 latent) a launch is 256 equal blocks (dec4: 128),
+// one wave per SIMD (bottleneck / dec4: two) and 144 MFMAs per wave.
+// ------------------------------------------------------------------------------------------------------
+struct LayerGeo {
+    int mode, cin, cout, tm, tn, wn, wk;
+};
+
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
+static int launch(const UArgs& a, hipStream_t st) {
+    constexpr int NPH = MODE == 2 ? 4 : 1;
+    const int blocks = a.nMt * a.nNt;
+    const size_t lds = WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0;
+    auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI>;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * WN * WK), lds, st, a);
+    LDM_CHECK_LAUNCH("uconv_kernel");
+    return 0;
+}
+
+constexpr LayerGeo kGeo[9] = {
+    {0, 32, 64, 2, 1, 4, 1},     // enc1        conv3x3 s1
+    {1, 64, 128, 2, 2, 1, 4},    // enc2        conv3x3 s2 (+ t_emb)
+    {1, 128, 256, 2, 1, 1, 4},   // enc3        conv3x3 s2
+    {1, 256, 512, 1, 1, 1, 4},   // enc4        conv3x3 s2 (folded with CA2's out-projection)
+    {0, 512, 512, 1, 1, 1, 8},   // bottleneck  conv3x3 s1 (folded with CA1's out-projection)
+    {2, 512, 256, 1, 1, 1, 8},   // dec4        convT k3 s2 (+ skip z3)
+    {2, 256, 128, 1, 1, 1, 4},   // dec3        convT (+ skip z2)
+    {2, 128, 64, 1, 2, 1, 4},    // dec2        convT (+ skip z1)
+    {0, 64, 32, 2, 2, 1, 4},     // dec1        conv3x3 s1 (+ fused DDIM update)
+};
+
+}  // namespace uc
+
+// Packed floats of layer `layer`'s step weights (9*Cin*Cout).
+int64_t step_packed_floats(int layer) {
+    if (layer < 0 || layer > 8) return -1;
+    return (int64_t)9 * uc::kGeo[layer].cin * uc::kGeo[layer].cout;
+}
+
+int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st) {
+    using namespace uc;
+    LDM_REQUIRE(layer >= 0 && layer <= 8, "step conv: layer index");
+    LDM_REQUIRE(B > 0 && H % 8 == 0 && W % 8 == 0, "step conv: latent H, W must be multiples of 8");
+    const LayerGeo& g = kGeo[layer];
+    // spatial size of each layer's input (model.py:178-194)
+    static const int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
+    const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
+    UArgs a{};
+    a.x = s.x;
+    a.w = s.w;
+    a.y = s.y;
+    a.bias = s.bias;
+    a.bcast = s.bcast;
+    a.skip = s.skip;
+    a.coef = s.coef;
+    a.xs = s.xs;
+    a.x0_log = s.x0_log;
+    a.eps_log = s.eps_log;
+    a.eta = s.eta;
+    a.B = B;
+    a.Hin = Hin;
+    a.Win = Win;
+    if (g.mode == 0) {
+        a.Hout = Hin, a.Wout = Win, a.Hq = Hin, a.Wq = Win;
+    } else if (g.mode == 1) {
+        a.Hout = Hin / 2, a.Wout = Win / 2, a.Hq = a.Hout, a.Wq = a.Wout;
+    } else {
+        a.Hout = 2 * Hin, a.Wout = 2 * Win, a.Hq = Hin, a.Wq = Win;
+    }
+    a.Nq = B * a.Hq * a.Wq;
+    const int bm = 16 * g.tm, bn = 16 * g.tn * g.wn;
+    a.nMt = g.cout / bm;
+    a.nNt = (a.Nq + bn - 1) / bn;
+    // weight-heavy layers keep one M tile's blocks together (N tile fastest would spread a weight slab
+    // over every XCD's L2); activation-heavy ones walk M fastest
+    const int64_t wbytes = (int64_t)9 * g.cin * g.cout * 4, xbytes = (int64_t)B * Hin * Win * g.cin * 4;
+    a.order = wbytes > xbytes ? 0 : 1;
+    a.fd_hw = FastDiv::make(a.Hq * a.Wq);
+    a.fd_w = FastDiv::make(a.Wq);
+    a.fd_mt = FastDiv::make(a.nMt);
+    a.fd_nt = FastDiv::make(a.nNt);
+    LDM_REQUIRE((int64_t)B * Hin * Win * g.cin * 4 < 0x7ff00000LL && (int64_t)B * a.Hout * a.Wout * g.cout * 4 < 0x7ff00000LL,
+                "step conv: tensor too large for 32-bit buffer offsets");
+    LDM_REQUIRE(s.x && s.w && s.bias, "step conv: null operand");
+    switch (layer) {
+        case 0: LDM_REQUIRE(s.y, "enc1: y"); return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, st);
+        case 1: LDM_REQUIRE(s.y && s.bcast, "enc2: y, t_emb");
+            return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, st);
+        case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, st);
+        case 3: LDM_REQUIRE(s.y, "enc4: y"); return launch<1, 256, 512, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_POSB>(a, st);
+        case 4: LDM_REQUIRE(s.y, "bottleneck: y"); return launch<0, 512, 512, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_POSB>(a, st);
+        case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
+            return launch<2, 512, 256, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_SKIP>(a, st);
+        case 6: LDM_REQUIRE(s.y && s.skip, "dec3: y, skip");
+            return launch<2, 256, 128, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_SKIP>(a, st);
+        case 7: LDM_REQUIRE(s.y && s.skip, "dec2: y, skip");
+            return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP>(a, st);
+        default: LDM_REQUIRE(s.xs && s.coef, "dec1: sampler state, coefficients");
+            return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, st);
+    }
+}
+
+int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st) {
+    const int64_t n = (int64_t)B * C * HW;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (to_nhwc)
+        hipLaunchKernelGGL(uc::nchw_to_nhwc_kernel, dim3(blocks), dim3(256), 0, st, x, y, C, HW, n);
+    else
+        hipLaunchKernelGGL(uc::nhwc_to_nchw_kernel, dim3(blocks), dim3(256), 0, st, x, y, C, HW, n);
+    LDM_CHECK_LAUNCH("layout transpose");
+    return 0;
+}
+
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" int64_t ldm_step_packed_floats(int32_t layer) { return step_packed_floats(layer); }
+
+#if (UCONV_DIAG & 4)
+extern "C" int ldm_debug_uconv_stamps(unsigned long long* host, int nblocks) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(uc::g_uconv_stamps), sizeof(unsigned long long) * 5 * nblocks, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
+
+extern "C" int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream) {
+    LDM_REQUIRE(layer >= 0 && layer <= 8 && w && packed, "step pack: bad argument");
+    const uc::LayerGeo& g = uc::kGeo[layer];
+    const int64_t total = step_packed_floats(layer);
+    hipLaunchKernelGGL(uc::uconv_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       w, packed, g.cin, g.cout, g.mode == 2 ? 1 : 0);
+    LDM_CHECK_LAUNCH("uconv_pack_kernel");
+    return 0;
+}
+
+extern "C" int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                             const float* bias, const float* bcast, const float* skip, float* y, void* stream) {
+    StepConv s{};
+    s.x = x;
+    s.w = packed;
+    s.bias = bias;
+    s.bcast = bcast;
+    s.skip = skip;
+    s.y = y;
+    LDM_REQUIRE(layer != 8, "ldm_step_conv: dec1 runs fused with the DDIM update (ldm_ddim_sample)");
+    return step_conv(layer, B, H, W, s, (hipStream_t)stream);
+}

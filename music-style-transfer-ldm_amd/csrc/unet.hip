@@ -94,6 +94,7 @@ static int layer_desc(const ldm_unet_shape& s, int layer, ldm_conv_desc& d) {
 struct UNetWs {
     float *convws, *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
     float *kf2, *bf2, *kf1, *bf1;   // folded keys of both cross-attentions (reverse loop, use_fold)
+    float* xs;                      // the sampler state in NHWC (reverse loop with the step kernels)
     int64_t total;
 };
 
@@ -144,6 +145,7 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.bf2 = take(B * 4 * L2);
     w.kf1 = take(B * 4 * 512 * L1);
     w.bf1 = take(B * 4 * L1);
+    w.xs = take(B * (int64_t)s.C * HW);
     w.total = off;
     return w;
 }
@@ -260,6 +262,45 @@ static int unet_forward_folded(const ldm_unet_shape& s, const ldm_unet_weights& 
     return 0;
 }
 
+// The same folded step on the step kernels (uconv.hip): x and every activation NHWC, 11 launches, the
+// DDIM update fused into dec1.  z (the sampler state) is ws.xs.
+static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w, const UNetWs& ws, hipStream_t st,
+                             const float* temb, const DdimFuse& fuse) {
+    const int HW = s.H * s.W;
+    const int L2 = HW / 16, L1 = HW / 64;
+    auto sc = [&](int layer, const float* x, const float* bias, float* y, const float* bcast = nullptr,
+                  const float* skip = nullptr) {
+        StepConv c{};
+        c.x = x;
+        c.w = w.step_w[layer];
+        c.y = y;
+        c.bias = bias;
+        c.bcast = bcast;
+        c.skip = skip;
+        return step_conv(layer, s.B, s.H, s.W, c, st);
+    };
+    LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
+    LDM_TRY(sc(1, ws.z1, w.conv_b[1], ws.z2, temb));
+    LDM_TRY(sc(2, ws.z2, w.conv_b[2], ws.z3));
+    LDM_TRY(attention_folded(ws.z3, ws.kv2, ws.kf2, ws.bf2, ws.a2, s.B, 256, 4, L2, L2, st));
+    LDM_TRY(sc(3, ws.a2, w.step_pb[0], ws.z4));
+    LDM_TRY(attention_folded(ws.z4, ws.kv1, ws.kf1, ws.bf1, ws.a1, s.B, 512, 4, L1, L1, st));
+    LDM_TRY(sc(4, ws.a1, w.step_pb[1], ws.zb));
+    LDM_TRY(sc(5, ws.zb, w.conv_b[5], ws.d4, nullptr, ws.z3));
+    LDM_TRY(sc(6, ws.d4, w.conv_b[6], ws.d3, nullptr, ws.z2));
+    LDM_TRY(sc(7, ws.d3, w.conv_b[7], ws.d2, nullptr, ws.z1));
+    StepConv c{};
+    c.x = ws.d2;
+    c.w = w.step_w[8];
+    c.bias = w.conv_b[8];
+    c.coef = fuse.coef;
+    c.eta = fuse.eta;
+    c.xs = ws.xs;
+    c.x0_log = fuse.x0_log;
+    c.eps_log = fuse.eps_log;
+    return step_conv(8, s.B, s.H, s.W, c, st);
+}
+
 }  // namespace ldm
 
 using namespace ldm;
@@ -323,6 +364,18 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
                                     (float)std::sqrt(1.0 / 64.0), ws.kf2, ws.bf2, st));
         LDM_TRY(attention_fold_keys(ws.kv1, w->ca_wq_raw[1], w->ca_bq[1], s->B, 512, 4, HW / 64,
                                     (float)std::sqrt(1.0 / 128.0), ws.kf1, ws.bf1, st));
+        if (w->use_step) {
+            LDM_REQUIRE(s->C == 32 && s->nf == 64, "ddim_sample: the step kernels are built for latent 32 / 64 filters");
+            for (int l = 0; l < 9; ++l) LDM_REQUIRE(w->step_w[l], "ddim_sample: use_step needs the step weights");
+            LDM_REQUIRE(w->step_pb[0] && w->step_pb[1], "ddim_sample: use_step needs the folded biases");
+            LDM_TRY(step_layout(x, ws.xs, s->B, s->C, HW, true, st));
+            for (int i = 0; i < nsteps; ++i) {
+                DdimFuse fuse{coef_table + 4 * (size_t)i, eta, ws.xs, x0_logs ? x0_logs + (size_t)i * n : nullptr,
+                              eps_logs ? eps_logs + (size_t)i * n : nullptr};
+                LDM_TRY(unet_step_kernels(*s, *w, ws, st, temb_all + (size_t)i * s->B * 128, fuse));
+            }
+            return step_layout(ws.xs, x, s->B, s->C, HW, false, st);
+        }
         for (int i = 0; i < nsteps; ++i) {
             DdimFuse fuse{coef_table + 4 * (size_t)i, eta, x, x0_logs ? x0_logs + (size_t)i * n : nullptr,
                           eps_logs ? eps_logs + (size_t)i * n : nullptr};

@@ -54,7 +54,8 @@ class UNetWeights(ctypes.Structure):
                 ("ca_wkv", c_fp * 2), ("ca_bkv", c_fp * 2), ("ca_plan_kv", ConvPlan * 2),
                 ("ca_wo", c_fp * 2), ("ca_bo", c_fp * 2), ("ca_plan_o", ConvPlan * 2),
                 ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp),
-                ("ca_wq_raw", c_fp * 2), ("fold_w", c_fp * 2), ("fold_pb", c_fp * 2), ("use_fold", c_int32)]
+                ("ca_wq_raw", c_fp * 2), ("fold_w", c_fp * 2), ("fold_pb", c_fp * 2), ("use_fold", c_int32),
+                ("step_w", c_fp * 9), ("step_pb", c_fp * 2), ("use_step", c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
@@ -73,6 +74,9 @@ SIGNATURES = {
     "ldm_conv_forward_ws": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), c_fp, c_fp,
                                       ctypes.POINTER(Epilogue), c_fp, c_fp, c_vp]),
     "ldm_reduce_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_step_packed_floats": (c_int64, [c_int32]),
+    "ldm_step_pack_weight": (c_int32, [c_int32, c_fp, c_fp, c_vp]),
+    "ldm_step_conv": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
                                       c_int32, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_stats": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),

@@ -20,11 +20,14 @@ _CONV_NAMES = ("enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "de
 class UNetEngine:
     """Runs `unet` (a models.model.UNet: reference parameter names / shapes) through libldm_amd."""
 
-    def __init__(self, unet, fold=None):
+    def __init__(self, unet, fold=None, step=None):
         self.unet = unet
         # Re-associated cross-attentions in the reverse loop (ldm_capi.h use_fold); LDM_AMD_FOLD=0 turns
         # it off (A/B timing, parity of the literal form).
         self.fold = (os.environ.get("LDM_AMD_FOLD", "1") != "0") if fold is None else bool(fold)
+        # Step kernels (uconv.hip) for the folded reverse loop; LDM_AMD_STEP=0 keeps conv.hip's general
+        # kernel (A/B timing).  Built for the LDM's latent 32 / 64 filters.
+        self.step = (os.environ.get("LDM_AMD_STEP", "1") != "0") if step is None else bool(step)
         self._bound = {}      # shape key -> (key of param versions, UNetWeights, keepalive)
         self._ws = {}         # (shape key, device) -> workspace tensor
         self._graphs = {}
@@ -55,7 +58,7 @@ class UNetEngine:
             if not p.is_contiguous():
                 raise RuntimeError("UNet parameters must be contiguous")
         vkey = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params) + \
-            tuple(sorted(ops._PLAN_OVERRIDE.items())) + (self.fold,)
+            tuple(sorted(ops._PLAN_OVERRIDE.items())) + (self.fold, self.step)
         hit = self._bound.get(skey)
         if hit is not None and hit[0] == vkey:
             return hit[1]
@@ -104,6 +107,7 @@ class UNetEngine:
             w.ca_bq[j] = ipb.data_ptr()
             w.ca_bkv[j] = ipb.data_ptr() + E * 4
             w.ca_bo[j] = a.out_proj.bias.data_ptr()
+        folded = {}
         if self.fold:
             # enc4 o out_proj(CA2) and bottleneck o out_proj(CA1), packed with those layers' plans
             for j, (layer, conv, ca) in enumerate(((3, u.enc4, u.cross_attention2), (4, u.bottleneck, u.cross_attention1))):
@@ -119,7 +123,22 @@ class UNetEngine:
                 w.fold_w[j] = buf.data_ptr()
                 w.fold_pb[j] = pb.data_ptr()
                 w.ca_wq_raw[j] = a.in_proj_weight.data_ptr()
+                folded[layer] = (wf, pb)
             w.use_fold = 1
+            if self.step and shape.C == 32 and shape.nf == 64:
+                lib = L.load()
+                for i, n in enumerate(_CONV_NAMES):
+                    src = folded[i][0] if i in folded else getattr(u, n).weight.detach()
+                    src = ops.f32c(src)
+                    buf = torch.empty(int(lib.ldm_step_packed_floats(i)), device=src.device, dtype=torch.float32)
+                    L.call("ldm_step_pack_weight", i, src.data_ptr(), buf.data_ptr(), ops.stream_handle())
+                    keep += [src, buf]
+                    w.step_w[i] = buf.data_ptr()
+                for j, layer in enumerate((3, 4)):
+                    pbt = folded[layer][1].permute(1, 2, 0).contiguous()     # [Hout, Wout, Cout]
+                    keep.append(pbt)
+                    w.step_pb[j] = pbt.data_ptr()
+                w.use_step = 1
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)
