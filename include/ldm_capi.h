@@ -221,9 +221,11 @@ typedef struct ldm_unet_weights {
     const float* fold_w[2];
     const float* fold_pb[2];
     int32_t use_fold;
-    /* Step kernels of the reverse loop (uconv.hip; used when use_step != 0 together with use_fold, for
-     * latent C = 32 and num_filters = 64): the nine convs packed by ldm_step_pack_weight (enc4 /
-     * bottleneck: their folded weights), and the folded position biases transposed to [Hout*Wout][Cout]. */
+    /* Step kernels of the reverse loop (used when use_step != 0 together with use_fold, for latent C = 32
+     * and num_filters = 64): the nine convs packed by ldm_step_pack_weight (enc4 / bottleneck: their
+     * folded weights), and the folded position biases transposed to [Hout*Wout][Cout].  use_step 1: the
+     * register-direct kernels (uconv.hip, any latent with H, W multiples of 8); 2: the LDS-staged kernels
+     * (ustep.hip) where they apply (latent 16 x 64, B a multiple of 4), else as 1. */
     const float* step_w[9];
     const float* step_pb[2];
     int32_t use_step;
@@ -271,6 +273,13 @@ int64_t ldm_step_packed_floats(int32_t layer);
 int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream);
 int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                   const float* bias, const float* bcast, const float* skip, float* y, void* stream);
+/* The LDS-staged variant (ustep.hip) of the same layers at the canonical latent H = 16, W = 64 with B a
+ * multiple of 4 (else -1).  The deep layers split K across blocks: they need a zero-filled workspace of
+ * ldm_ustep_workspace_floats(layer, B) floats (0: none), which they leave zero-filled; layers running one
+ * after another on a stream may share one.  Same packed weights and epilogue as ldm_step_conv. */
+int64_t ldm_ustep_workspace_floats(int32_t layer, int32_t B);
+int ldm_ustep_conv(int32_t layer, int32_t B, const float* x, const float* packed, const float* bias,
+                   const float* bcast, const float* skip, float* y, float* workspace, void* stream);
 
 /* ---- train step backward (LDMTrainer.train_step, train.py:163-208: scaler.scale(loss).backward()) ---
  * Data gradients of a conv are the forward kernel on the dual descriptor (conv <-> transposed conv);

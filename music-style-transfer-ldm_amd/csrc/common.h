@@ -144,6 +144,10 @@ struct StepConv {
 };
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
+// ustep.hip: the LDS-staged step kernels at the canonical latent (16 x 64, batch a multiple of 4)
+bool ustep_supported(int B, int H, int W);
+int64_t ustep_workspace_floats(int layer, int B, int64_t* cnt_floats = nullptr);
+int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.

@@ -95,6 +95,7 @@ struct UNetWs {
     float *convws, *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
     float *kf2, *bf2, *kf1, *bf1;   // folded keys of both cross-attentions (reverse loop, use_fold)
     float* xs;                      // the sampler state in NHWC (reverse loop with the step kernels)
+    float* ustep;                   // split-K counters + slabs of the LDS-staged step kernels (zero-filled)
     int64_t total;
 };
 
@@ -108,6 +109,21 @@ static int64_t conv_ws_floats(const ldm_unet_weights* w) {
         m = m > w->ca_plan_q[j].ws_floats ? m : w->ca_plan_q[j].ws_floats;
         m = m > w->ca_plan_kv[j].ws_floats ? m : w->ca_plan_kv[j].ws_floats;
         m = m > w->ca_plan_o[j].ws_floats ? m : w->ca_plan_o[j].ws_floats;
+    }
+    return m;
+}
+
+// The LDS-staged step kernels (ustep.hip) run when use_step == 2 at their canonical shape.
+static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
+    return w && w->use_fold && w->use_step == 2 && s.C == 32 && s.nf == 64 && ustep_supported(s.B, s.H, s.W);
+}
+
+static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* w) {
+    if (!use_ustep(s, w)) return 0;
+    int64_t m = 0;
+    for (int l = 0; l < 9; ++l) {
+        const int64_t f = ustep_workspace_floats(l, s.B);
+        m = m > f ? m : f;
     }
     return m;
 }
@@ -146,6 +162,7 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.kf1 = take(B * 4 * 512 * L1);
     w.bf1 = take(B * 4 * L1);
     w.xs = take(B * (int64_t)s.C * HW);
+    w.ustep = take(ustep_ws_floats(s, wts));
     w.total = off;
     return w;
 }
@@ -267,6 +284,7 @@ static int unet_forward_folded(const ldm_unet_shape& s, const ldm_unet_weights& 
 static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w, const UNetWs& ws, hipStream_t st,
                              const float* temb, const DdimFuse& fuse) {
     const int HW = s.H * s.W;
+    const bool v3 = use_ustep(s, &w);
     const int L2 = HW / 16, L1 = HW / 64;
     auto sc = [&](int layer, const float* x, const float* bias, float* y, const float* bcast = nullptr,
                   const float* skip = nullptr) {
@@ -277,7 +295,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
         c.bias = bias;
         c.bcast = bcast;
         c.skip = skip;
-        return step_conv(layer, s.B, s.H, s.W, c, st);
+        return v3 ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
     };
     LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
     LDM_TRY(sc(1, ws.z1, w.conv_b[1], ws.z2, temb));
@@ -298,7 +316,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     c.xs = ws.xs;
     c.x0_log = fuse.x0_log;
     c.eps_log = fuse.eps_log;
-    return step_conv(8, s.B, s.H, s.W, c, st);
+    return v3 ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
 }
 
 }  // namespace ldm

@@ -77,6 +77,8 @@ SIGNATURES = {
     "ldm_step_packed_floats": (c_int64, [c_int32]),
     "ldm_step_pack_weight": (c_int32, [c_int32, c_fp, c_fp, c_vp]),
     "ldm_step_conv": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
+    "ldm_ustep_conv": (c_int32, [c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
                                       c_int32, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_stats": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),

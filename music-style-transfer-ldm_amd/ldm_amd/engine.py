@@ -25,9 +25,14 @@ class UNetEngine:
         # Re-associated cross-attentions in the reverse loop (ldm_capi.h use_fold); LDM_AMD_FOLD=0 turns
         # it off (A/B timing, parity of the literal form).
         self.fold = (os.environ.get("LDM_AMD_FOLD", "1") != "0") if fold is None else bool(fold)
-        # Step kernels (uconv.hip) for the folded reverse loop; LDM_AMD_STEP=0 keeps conv.hip's general
-        # kernel (A/B timing).  Built for the LDM's latent 32 / 64 filters.
-        self.step = (os.environ.get("LDM_AMD_STEP", "1") != "0") if step is None else bool(step)
+        # Step kernels for the folded reverse loop (ldm_capi.h use_step): 2 (default, or True) the LDS-staged
+        # kernels (ustep.hip) where they apply, else the register-direct ones (uconv.hip); 1 only the latter;
+        # 0 conv.hip's general kernel (LDM_AMD_STEP, A/B timing).  Built for the LDM's latent 32 / 64 filters.
+        if step is None:
+            step = int(os.environ.get("LDM_AMD_STEP", "2"))
+        self.step = 2 if step is True else (0 if step is False else int(step))
+        if self.step not in (0, 1, 2):
+            raise ValueError(f"step must be 0, 1 or 2, got {step!r}")
         self._bound = {}      # shape key -> (key of param versions, UNetWeights, keepalive)
         self._ws = {}         # (shape key, device) -> workspace tensor
         self._graphs = {}
@@ -138,7 +143,7 @@ class UNetEngine:
                     pbt = folded[layer][1].permute(1, 2, 0).contiguous()     # [Hout, Wout, Cout]
                     keep.append(pbt)
                     w.step_pb[j] = pbt.data_ptr()
-                w.use_step = 1
+                w.use_step = self.step
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)

@@ -28,9 +28,17 @@ def npy(t):
     return t.detach().double().cpu().numpy()
 
 
-@pytest.mark.parametrize("layer", range(8))
-@pytest.mark.parametrize("shape", [(8, 16, 64), (2, 16, 16), (3, 8, 24)])
-def test_step_layer_vs_float64(cuda, layer, shape):
+def _case(variant, layer, shape):
+    return variant, layer, shape
+
+
+@pytest.mark.parametrize("variant,layer,shape",
+                         [_case("uconv", l, s) for l in range(8) for s in [(8, 16, 64), (2, 16, 16), (3, 8, 24)]] +
+                         [_case("ustep", l, s) for l in range(8) for s in [(8, 16, 64), (4, 16, 64), (12, 16, 64)]])
+def test_step_layer_vs_float64(cuda, variant, layer, shape):
+    """uconv: ldm_step_conv (register-direct, any latent with H, W multiples of 8); ustep: ldm_ustep_conv
+    (LDS-staged, latent 16 x 64, B a multiple of 4), run twice on one workspace: bitwise-equal results
+    (the split-K sum is in slot order) and the counters left zero."""
     from ldm_amd import _lib as L
     B, H, W = shape
     Cin, Cout, mode = LAYERS[layer]
@@ -54,8 +62,24 @@ def test_step_layer_vs_float64(cuda, layer, shape):
     bd = bias.contiguous().to(cuda)
     bcd = bc.to(cuda) if bc is not None else None
     skd = sk.permute(0, 2, 3, 1).contiguous().to(cuda) if sk is not None else None
-    L.call("ldm_step_conv", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(),
-           None if bcd is None else bcd.data_ptr(), None if skd is None else skd.data_ptr(), y.data_ptr(), st)
+    bcp = None if bcd is None else bcd.data_ptr()
+    skp = None if skd is None else skd.data_ptr()
+    if variant == "uconv":
+        L.call("ldm_step_conv", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp,
+               y.data_ptr(), st)
+    else:
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B))
+        assert nws >= 0
+        ws = torch.zeros(max(nws, 1), device=cuda)
+        L.call("ldm_ustep_conv", layer, B, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp, y.data_ptr(),
+               ws.data_ptr() if nws else None, st)
+        y2 = torch.full_like(y, float("nan"))
+        L.call("ldm_ustep_conv", layer, B, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp, y2.data_ptr(),
+               ws.data_ptr() if nws else None, st)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+        if nws:   # the tile counters lead the workspace (a second run with stale ones would lose tiles)
+            assert int(ws[:64].view(torch.int32).abs().sum()) == 0
     torch.cuda.synchronize()
     x64, w64 = x.double(), w.double()
     if mode == 2:
@@ -72,10 +96,24 @@ def test_step_layer_vs_float64(cuda, layer, shape):
     assert rel_err(npy(got), ref.numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("shape,eta", [((8, 16, 64), 0.0), ((2, 16, 16), 1.0), ((3, 8, 24), 0.4), ((1, 16, 64), 0.0)])
+def test_ustep_rejects_other_shapes(cuda):
+    from ldm_amd import _lib as L
+    lib = L.load()
+    assert lib.ldm_ustep_workspace_floats(0, 6) == -1     # B not a multiple of 4
+    assert lib.ldm_ustep_workspace_floats(9, 8) == -1     # no such layer
+    assert lib.ldm_ustep_workspace_floats(0, 8) == 0      # enc1 does not split K
+    assert lib.ldm_ustep_workspace_floats(4, 8) > 0
+    x = torch.zeros(6 * 16 * 64 * 32, device=cuda)
+    assert lib.ldm_ustep_conv(0, 6, x.data_ptr(), x.data_ptr(), x.data_ptr(), None, None, x.data_ptr(), None,
+                              torch.cuda.current_stream().cuda_stream) != 0
+
+
+@pytest.mark.parametrize("shape,eta", [((8, 16, 64), 0.0), ((2, 16, 16), 1.0), ((3, 8, 24), 0.4), ((1, 16, 64), 0.0),
+                                       ((4, 16, 64), 0.7)])
 def test_step_loop_equals_general_loop(M, cuda, shape, eta):
-    """The reverse loop on the step kernels (NHWC state, fused dec1 update) == the same folded loop on
-    conv.hip's general kernel, final x and both logs."""
+    """The reverse loop on the step kernels (NHWC state, fused dec1 update; use_step 1 = uconv.hip,
+    2 = ustep.hip where it applies) == the same folded loop on conv.hip's general kernel, final x and
+    both logs."""
     from ldm_amd.engine import UNetEngine
     B, H, W = shape
     unet = M.UNet(32, 32, 64)
@@ -90,16 +128,17 @@ def test_step_loop_equals_general_loop(M, cuda, shape, eta):
     tt = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(cuda)
     outs = []
     with torch.no_grad():
-        for step in (False, True):
+        for step in (0, 1, 2):   # (2: the nine layers share one split-K workspace)
             eng = UNetEngine(unet, fold=True, step=step)
             x = x0.clone()
             lg = (torch.empty((5, B, 32, H, W), device=cuda), torch.empty((5, B, 32, H, W), device=cuda))
             eng.ddim_loop(x, s5, s6, tt, coefs, eta, *lg)
-            assert bool(eng.weights(eng.shape(B, 32, H, W)).use_step) == step
+            assert eng.weights(eng.shape(B, 32, H, W)).use_step == step
             outs.append((x, lg[0], lg[1]))
     torch.cuda.synchronize()
-    for a, b in zip(outs[0], outs[1]):
-        assert rel_err(npy(b), npy(a)) < 1e-5
+    for k in (1, 2):
+        for a, b in zip(outs[0], outs[k]):
+            assert rel_err(npy(b), npy(a)) < 1e-5
 
 
 @pytest.fixture(scope="module")

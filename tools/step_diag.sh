@@ -1,14 +1,20 @@
 #!/bin/bash
-# Diagnostic variants of the step kernels (csrc/uconv.hip, -DUCONV_DIAG=k) -> lib/libldm_amd_ucd<k>.so:
-#   1 no MFMAs, 2 no operand loads, 3 neither (fixed cost), 4 per-block timestamps (tools/step_times.py --stamps)
+# Diagnostic variants of the step kernels -> lib/libldm_amd_<file><k>.so (never shipped; delete after use):
+#   tools/step_diag.sh uconv|ustep k...   with k: 1 no MFMAs, 2 no operand loads, 3 neither (fixed cost),
+#   4 per-block timestamps (tools/step_times.py --stamps)
 set -e
 cd "$(dirname "$0")/../music-style-transfer-ldm_amd/csrc"
+f=$1; shift
+D=$(echo $f | tr a-z A-Z)_DIAG
 for k in "$@"; do
-  mkdir -p ../build/ucd$k
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -DUCONV_DIAG=$k -fno-gpu-rdc -x hip -c uconv.hip -o ../build/ucd$k/uconv.hip.o &
+  mkdir -p ../build/${f}d$k
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -D$D=$k -fno-gpu-rdc -x hip -c $f.hip -o ../build/${f}d$k/$f.hip.o &
 done
 wait
+others=""
+for s in capi.cpp conv.hip misc.hip unet.hip backward.hip reduce.hip uconv.hip ustep.hip; do
+  [ "$s" = "$f.hip" ] || others="$others ../build/$s.o"
+done
 for k in "$@"; do
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o ../lib/libldm_amd_ucd$k.so ../build/ucd$k/uconv.hip.o \
-    ../build/capi.cpp.o ../build/conv.hip.o ../build/misc.hip.o ../build/unet.hip.o ../build/backward.hip.o ../build/reduce.hip.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fno-gpu-rdc -o ../lib/libldm_amd_${f}d$k.so ../build/${f}d$k/$f.hip.o $others
 done

@@ -44,8 +44,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="8x16x64")
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs libldm_amd_ucd4.so)")
+    ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a USTEP_DIAG/UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
+    ap.add_argument("--variant", default="ustep", choices=["uconv", "ustep"])
     args = ap.parse_args()
     B, H, W = (int(v) for v in args.shape.split("x"))
     from ldm_amd import _lib as L
@@ -65,16 +66,44 @@ def main():
         sk = torch.randn(B, Hout, Wout, Cout, device=dev)
         y = torch.empty(B, Hout, Wout, Cout, device=dev)
 
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if args.variant == "ustep" else 0
+        ws = torch.zeros(max(nws, 1), device=dev)
+
         def run():
-            lib.ldm_step_conv(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(),
-                              bc.data_ptr() if layer == 1 else None, sk.data_ptr() if mode == 2 else None,
-                              y.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            bcp = bc.data_ptr() if layer == 1 else None
+            skp = sk.data_ptr() if mode == 2 else None
+            stp = torch.cuda.current_stream().cuda_stream
+            if args.variant == "ustep":
+                rc = lib.ldm_ustep_conv(layer, B, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
+                                        y.data_ptr(), ws.data_ptr() if nws else None, stp)
+            else:
+                rc = lib.ldm_step_conv(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
+                                       y.data_ptr(), stp)
+            assert rc == 0
 
         us = graph_us(run, args.reps)
         fl = 2.0 * B * Cout * Hout * Wout * Cin * (9 if mode < 2 else 2.25)
         tot += us
         extra = ""
-        if args.stamps:
+        if args.stamps and args.variant == "ustep":
+            import numpy as np
+            lib.ldm_debug_ustep_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            graph_us(run, 10)          # stamps of the last launch of a 10-launch graph chain (warm)
+            torch.cuda.synchronize()
+            buf = np.zeros((4096, 8), dtype=np.uint64)
+            assert lib.ldm_debug_ustep_stamps(buf.ctypes.data, 4096) == 0
+            nb = int((buf[:, 0] > 0).sum())
+            b = buf[:nb].astype(np.float64)
+            clk = 2.4e3   # shader cycles per us (s_memtime), nominal
+            ph = [np.median((b[:, k + 1] - b[:, k]) / clk) for k in range(1, 6)]
+            blk = (b[:, 7] - b[:, 0]) * 0.01
+            span = (b[:, 7].max() - b[:, 0].min()) * 0.01
+            st0 = (b[:, 0] - b[:, 0].min()) * 0.01
+            pct = np.percentile(st0, [10, 50, 90])
+            extra = (f" | blocks {nb} span {span:5.2f} start p10/50/90 {pct[0]:4.2f}/{pct[1]:4.2f}/{pct[2]:4.2f} "
+                     f"blk {np.median(blk):5.2f} (max {blk.max():5.2f}) | setup {ph[0]:4.2f} issue0 {ph[1]:4.2f} "
+                     f"wait0 {ph[2]:4.2f} mma {ph[3]:4.2f} red {ph[4]:4.2f} us")
+        elif args.stamps:
             import numpy as np
             lib.ldm_debug_uconv_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
             graph_us(run, 10)          # stamps of the last launch of a 10-launch graph chain (warm)
@@ -112,7 +141,7 @@ def main():
     tt = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(dev)
     with torch.no_grad():
         emb = ldm.style_encoder(style)
-        for step in (False, True):
+        for step in (0, 1, 2):
             eng = UNetEngine(ldm.unet, fold=True, step=step)
             gd = GraphedDDIM(eng, z, emb["s5"], emb["s6"], tt, coefs, 0.0, logs=True)
             for _ in range(3):
