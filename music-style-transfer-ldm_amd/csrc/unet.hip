@@ -118,10 +118,16 @@ static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
     return w && w->use_fold && w->use_step == 2 && s.C == 32 && s.nf == 64 && ustep_supported(s.B, s.H, s.W);
 }
 
+// Layers that run on ustep.hip under use_step 2: measured in the reverse loop (rocprofv3, B=8), the
+// LDS-staged form wins for enc1, dec4 and dec2 and loses where it has to split K across blocks or where the
+// register-direct form already streams well (profiles/r02/README.md).
+static bool ustep_layer(int l) { return l == 0 || l == 5 || l == 7; }
+
 static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* w) {
     if (!use_ustep(s, w)) return 0;
     int64_t m = 0;
     for (int l = 0; l < 9; ++l) {
+        if (!ustep_layer(l)) continue;
         const int64_t f = ustep_workspace_floats(l, s.B);
         m = m > f ? m : f;
     }
@@ -295,7 +301,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
         c.bias = bias;
         c.bcast = bcast;
         c.skip = skip;
-        return v3 ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
+        return v3 && ustep_layer(layer) ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
     };
     LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
     LDM_TRY(sc(1, ws.z1, w.conv_b[1], ws.z2, temb));
@@ -316,7 +322,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     c.xs = ws.xs;
     c.x0_log = fuse.x0_log;
     c.eps_log = fuse.eps_log;
-    return v3 ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
+    return v3 && ustep_layer(8) ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
 }
 
 }  // namespace ldm

@@ -58,6 +58,7 @@ struct G {
     static constexpr Cfg c = kCfg[L];
     static constexpr int MODE = c.mode, CIN = c.cin, COUT = c.cout, BM = c.bm, BN = c.bn, KS = c.ks, KC = c.kc;
     static constexpr int WM = c.wm, WN = c.wn, WK = c.wk, EPI = c.epi, NW = WM * WN * WK, NST = c.nst;
+    static constexpr int NWL = 4, NT = NW + NWL;      // + loader waves (one per SIMD): they issue every DMA
     static constexpr int Hin = kH / c.div, Win = kW / c.div;
     static constexpr int Hq = MODE == 1 ? Hin / 2 : Hin, Wq = MODE == 1 ? Win / 2 : Win;   // column grid
     static constexpr int Hout = MODE == 2 ? 2 * Hin : Hq, Wout = MODE == 2 ? 2 * Win : Wq;
@@ -79,9 +80,9 @@ struct G {
     static constexpr int KCS = KC / NST;               // channel chunks per stage
     static constexpr int CPW = KCS / WK;               // channel chunks per stage per wave
     static constexpr int NIT = CPW * 9;                // (chunk, tap) steps per stage per wave
-    // DMA instructions (1 KB each) per stage: A rows, B window; padded to a multiple of the wave count
+    // DMA instructions (1 KB each) per stage: A rows, B window; padded to a multiple of the loader waves
     static constexpr int GA = KCS * 9 * BM / 16, GB = KCS * WSLOTS / 16;
-    static constexpr int GS = (GA + GB + NW - 1) / NW * NW, GPW = GS / NW;
+    static constexpr int GS = (GA + GB + NWL - 1) / NWL * NWL, GPL = GS / NWL;
     static constexpr int LDS_A = KC * 9 * BM * 64, LDS_B = KC * WSLOTS * 64, LDS_DUMMY = 1024;
     static constexpr int LDS_RED = NW * NPH * TM * TN * 64 * 16;
     static constexpr int LDS = (LDS_A + LDS_B + LDS_DUMMY) > LDS_RED ? (LDS_A + LDS_B + LDS_DUMMY) : LDS_RED;
@@ -89,6 +90,7 @@ struct G {
     static_assert(COUT % BM == 0 && BM % (16 * WM) == 0 && BN % (16 * WN) == 0 && TM >= 1 && TN >= 1, "tile");
     static_assert(FULLROW ? (R % Hq == 0 || Hq % R == 0) : (Wq % BN == 0), "the tile is whole rows or samples");
     static_assert(LDS <= 160 * 1024, "LDS budget");
+    static_assert(NST * GPL <= 63, "a loader wave's DMAs must fit the vmcnt counter");
 };
 
 struct Args {
@@ -102,7 +104,7 @@ struct Args {
     float* xs;            // EPI_DDIM: sampler state (NHWC)
     float* x0_log;        // EPI_DDIM: NCHW logs or NULL
     float* eps_log;
-    float* slab;          // KS > 1: partial tiles [tile][KS][NW][NPH*TM*TN][64] float4
+    float* slab;          // KS > 1: partial tiles [tile][KS][WM*WN][NPH*TM*TN][64] float4
     int32_t* cnt;         // KS > 1: arrival counter per tile (zero between launches)
     float eta;
     int32_t B, nNt;
@@ -124,6 +126,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // Diagnostic builds only (never shipped; tools/step_diag.sh ustep): USTEP_DIAG bit 0 = no MFMAs, bit 1 = no
 // DMAs, bit 2 = per-block timestamps of thread 0 (entry / exit in 100 MHz wall ticks, phases in shader
 // clocks) into g_ustep_stamps, read back with ldm_debug_ustep_stamps.
+// Loader look-ahead: 1 = issue stage s+1, wait for stage s, release it; 2 = keep stages s+1 and s+2 in
+// flight while stage s is released (issue s+2 right after the release).
+#ifndef USTEP_LA
+#define USTEP_LA 2
+#endif
 #ifndef USTEP_DIAG
 #define USTEP_DIAG 0
 #endif
@@ -142,7 +149,7 @@ __device__ unsigned long long g_ustep_stamps[4096][8];
 #endif
 
 template <int L>
-__global__ __launch_bounds__(64 * G<L>::NW) __attribute__((amdgpu_waves_per_eu((G<L>::NW + 3) / 4, (G<L>::NW + 3) / 4)))
+__global__ __launch_bounds__(64 * G<L>::NT) __attribute__((amdgpu_waves_per_eu((G<L>::NT + 3) / 4, (G<L>::NT + 3) / 4)))
 void ustep_kernel(Args a) {
     using g = G<L>;
     constexpr int MODE = g::MODE, CIN = g::CIN, COUT = g::COUT, BM = g::BM, BN = g::BN, KS = g::KS, KC = g::KC;
@@ -150,7 +157,7 @@ void ustep_kernel(Args a) {
     constexpr int WMN = WM * WN, NST = g::NST, NIT = g::NIT;
     constexpr int Hin = g::Hin, Win = g::Win, Hq = g::Hq, Wq = g::Wq, Hout = g::Hout, Wout = g::Wout;
     constexpr int WR = g::WR, WC = g::WC, WE = g::WE, WPIX = g::WPIX, WSLOTS = g::WSLOTS;
-    constexpr int KCS = g::KCS, GA = g::GA, GB = g::GB, GPW = g::GPW;
+    constexpr int KCS = g::KCS, GA = g::GA, GB = g::GB, GPL = g::GPL, NWL = g::NWL;
     constexpr int NFR = NPH * TM * TN, NMY = (NFR + WK - 1) / WK;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     char* const lds = reinterpret_cast<char*>(smem);
@@ -160,7 +167,8 @@ void ustep_kernel(Args a) {
     USTEP_STAMP(1);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wn = wave % WN, wm = (wave / WN) % WM, wk = wave / WMN, wmn = wave % WMN;
+    const bool loader = wave >= NW;   // waves NW.. only issue DMAs; 0..NW-1 only multiply
+    const int wn = wave % WN, wm = (wave / WN) % WM, wk = (wave / WMN) % WK, wmn = wave % WMN;
     const int col = lane & 15, lg = lane >> 4;
 
     // block -> (M tile, N tile, K slice).  Blocks are dealt to the 8 XCDs round-robin (bid % 8; for speed
@@ -207,11 +215,11 @@ void ustep_kernel(Args a) {
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.x), (short)0, uni(a.B * Hin * Win * CIN * 4), 0x00020000);
 
-    // DMA instruction k (of GPW) of this wave for stage st
-    auto dma_one = [&](int st, auto kc_) {
+    // DMA instruction k (of GPL) of loader wave lw for stage st
+    auto dma_one = [&](int st, int lw, auto kc_) {
         if constexpr ((USTEP_DIAG & 2) != 0) return;
         constexpr int k = decltype(kc_)::value;
-        const int gi = k * NW + wave;   // wave-uniform
+        const int gi = k * NWL + lw;   // wave-uniform
         if (gi < GA) {
             constexpr int RB = BM / 16;
             const int cl = gi / RB, rb = gi - cl * RB;
@@ -284,13 +292,13 @@ void ustep_kernel(Args a) {
         o.ox = MODE == 2 ? 2 * colsel(cqx, ni) + (p & 1) : colsel(cqx, ni);
         o.pix = (o.b * Hout + o.oy) * Wout + o.ox;
         o.m = m0 + wm * (TM * 16) + 16 * mi + 4 * lg;
-        o.ok = f < NFR;
+        o.ok = f < NFR && !loader;
         return o;
     };
     auto frag = [&](int k) { return WK == 1 ? k : k * WK + wk; };
     floatx4 pre_b[NMY], pre_c[NMY], pre_s[NMY];
     USTEP_STAMP(2);
-    static_for<0, NMY>([&](auto kc_) {
+    if (!loader) static_for<0, NMY>([&](auto kc_) {
         constexpr int k = decltype(kc_)::value;
         const Out o = out_of(frag(k));
         pre_b[k] = (EPI & EPI_POSB) ? *reinterpret_cast<const floatx4*>(a.bias + (size_t)(o.oy * Wout + o.ox) * COUT + o.m)
@@ -299,10 +307,6 @@ void ustep_kernel(Args a) {
         if constexpr ((EPI & EPI_SKIP) != 0) pre_s[k] = *reinterpret_cast<const floatx4*>(a.skip + (size_t)o.pix * COUT + o.m);
         if constexpr ((EPI & EPI_DDIM) != 0) pre_s[k] = *reinterpret_cast<const floatx4*>(a.xs + (size_t)o.pix * COUT + o.m);
     });
-    // (the epilogue operands are the oldest loads: the first stage wait covers them)
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<0, GPW>([&](auto kc_) { dma_one(0, kc_); });
-    __builtin_amdgcn_sched_barrier(0);
     USTEP_STAMP(3);
 
     // ---- MFMAs from LDS ---------------------------------------------------------------------------------
@@ -335,43 +339,49 @@ void ustep_kernel(Args a) {
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) fb[ni] = *reinterpret_cast<const floatx4*>(lds + kc * (WSLOTS * 64) + boff[t][ni]);
     };
-    // Stage s: wait for its DMAs (everyone's: barrier), then multiply it while this wave issues stage s+1's
-    // DMAs, spread over the first half of the stage so that they land before it ends.
-    static_for<0, NST>([&](auto sc) {
-        constexpr int st = decltype(sc)::value;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if constexpr (st == 0) USTEP_STAMP(4);
-        floatx4 fa[2][TM], fb[2][TN];
-        load_frag(st, 0, fa[0], fb[0]);
-        static_for<0, NIT>([&](auto ic) {
-            constexpr int it = decltype(ic)::value, cur = it & 1;
-            constexpr int t = it % 9;
-            constexpr int p = MODE == 2 ? ((t / 3 != 1 ? 2 : 0) + (t % 3 != 1 ? 1 : 0)) : 0;
-            if constexpr (st + 1 < NST) {
-                constexpr int SPREAD = NIT / 2 > 0 ? NIT / 2 : 1;
-                static_for<0, GPW>([&](auto kc_) {
-                    constexpr int k = decltype(kc_)::value;
-                    if constexpr (k * SPREAD / GPW == it) dma_one(st + 1, kc_);
-                });
-            }
-            if constexpr (it + 1 < NIT) load_frag(st, it + 1, fa[cur ^ 1], fb[cur ^ 1]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < TN; ++ni) {
-                        if constexpr ((USTEP_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
-                            if (j == 0) acc[p][mi][ni][0] = acc[p][mi][ni][0] + fa[cur][mi][j] * fb[cur][ni][j];
-                        } else {
-                            acc[p][mi][ni] =
-                                __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][mi][j], fb[cur][ni][j], acc[p][mi][ni], 0, 0, 0);
-                        }
-                    }
-            __builtin_amdgcn_sched_barrier(0);
+    // The loader waves keep two stages of DMAs in flight and release stage s to the multiplying waves
+    // (barrier s) once their own DMAs of it landed (nothing is overwritten: every stage stays resident).
+    if (loader) {
+        const int lw = wave - NW;
+        auto issue = [&](auto sc) { static_for<0, GPL>([&](auto kc_) { dma_one(decltype(sc)::value, lw, kc_); }); };
+        issue(std::integral_constant<int, 0>{});
+        if constexpr (USTEP_LA == 2 && NST > 1) issue(std::integral_constant<int, 1>{});
+        static_for<0, NST>([&](auto sc) {
+            constexpr int st = decltype(sc)::value;
+            if constexpr (USTEP_LA == 1 && st + 1 < NST) issue(std::integral_constant<int, st + 1>{});
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(st + 1 < NST ? GPL : 0) : "memory");
+            __builtin_amdgcn_s_barrier();
+            if constexpr (USTEP_LA == 2 && st + 2 < NST) issue(std::integral_constant<int, st + 2>{});
         });
-    });
+    } else {
+        static_for<0, NST>([&](auto sc) {
+            constexpr int st = decltype(sc)::value;
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if constexpr (st == 0) USTEP_STAMP(4);
+            floatx4 fa[2][TM], fb[2][TN];
+            load_frag(st, 0, fa[0], fb[0]);
+            static_for<0, NIT>([&](auto ic) {
+                constexpr int it = decltype(ic)::value, cur = it & 1;
+                constexpr int t = it % 9;
+                constexpr int p = MODE == 2 ? ((t / 3 != 1 ? 2 : 0) + (t % 3 != 1 ? 1 : 0)) : 0;
+                if constexpr (it + 1 < NIT) load_frag(st, it + 1, fa[cur ^ 1], fb[cur ^ 1]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < TN; ++ni) {
+                            if constexpr ((USTEP_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
+                                if (j == 0) acc[p][mi][ni][0] = acc[p][mi][ni][0] + fa[cur][mi][j] * fb[cur][ni][j];
+                            } else {
+                                acc[p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][mi][j], fb[cur][ni][j],
+                                                                                      acc[p][mi][ni], 0, 0, 0);
+                            }
+                        }
+            });
+        });
+    }
     USTEP_STAMP(5);
 
     // ---- K reduction: waves (LDS), then blocks (sc1 slabs, last arriver) ------------------------------
@@ -382,7 +392,7 @@ void ustep_kernel(Args a) {
         static_for<0, NFR>([&](auto fc) {
             constexpr int f = decltype(fc)::value;
             constexpr int p = f / (TM * TN), mi = (f / TN) % TM, ni = f % TN;
-            red[((wk * WMN + wmn) * NFR + f) * 64 + lane] = acc[p][mi][ni];
+            if (!loader) red[((wk * WMN + wmn) * NFR + f) * 64 + lane] = acc[p][mi][ni];
         });
         __syncthreads();
         static_for<0, NMY>([&](auto kc_) {
@@ -408,7 +418,7 @@ void ustep_kernel(Args a) {
         static_for<0, NMY>([&](auto kc_) {
             constexpr int k = decltype(kc_)::value;
             const int f = frag(k);
-            if (f < NFR)   // write-through (sc1) partial tile
+            if (f < NFR && !loader)   // write-through (sc1) partial tile
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v[k]), sr,
                                                        slab_off(ks, f), 0, 16);
         });
@@ -557,7 +567,7 @@ int launch(const Args& a0, hipStream_t st) {
         LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, g::LDS));
         opted = true;
     }
-    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * g::NW), g::LDS, st, a);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * g::NT), g::LDS, st, a);
     LDM_CHECK_LAUNCH("ustep_kernel");
     return 0;
 }

@@ -47,13 +47,14 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a USTEP_DIAG/UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--variant", default="ustep", choices=["uconv", "ustep"])
+    ap.add_argument("--loop-only", default=None, help="comma list of use_step values: only time the loop")
     args = ap.parse_args()
     B, H, W = (int(v) for v in args.shape.split("x"))
     from ldm_amd import _lib as L
     dev = torch.device("cuda:0")
     lib = L.load()
     tot = 0.0
-    for layer, name in enumerate(NAMES):
+    for layer, name in enumerate(NAMES if args.loop_only is None else []):
         Cin, Cout, mode = LAYERS[layer]
         Hin, Win = H // DIV[layer], W // DIV[layer]
         Hout, Wout = (Hin, Win) if mode == 0 else ((Hin // 2, Win // 2) if mode == 1 else (2 * Hin, 2 * Win))
@@ -141,7 +142,7 @@ def main():
     tt = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(dev)
     with torch.no_grad():
         emb = ldm.style_encoder(style)
-        for step in (0, 1, 2):
+        for step in ((0, 1, 2) if args.loop_only is None else [int(v) for v in args.loop_only.split(",")]):
             eng = UNetEngine(ldm.unet, fold=True, step=step)
             gd = GraphedDDIM(eng, z, emb["s5"], emb["s6"], tt, coefs, 0.0, logs=True)
             for _ in range(3):
