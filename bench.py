@@ -42,10 +42,10 @@ def parse():
     ap.add_argument("--eta", type=float, default=None, help="0.0 for sample, 1.0 for transfer")
     ap.add_argument("--split", type=int, default=1,
                     help="run the per-GPU batch as this many sub-batch chains on separate streams (one graph)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic_step.json"),
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
     a = ap.parse_args()
     if a.batch is None:
@@ -94,96 +94,192 @@ def _graph_time_us(fn, reps):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
-def time_layers(engine, shape, dev, reps=50):
-    """Average launch duration of each UNet GEMM-shaped kernel, HIP events on the launching stream."""
-    import ctypes
+STEP_LAYERS = [  # (name, Cin, Cout, mode 0 conv s1 / 1 conv s2 / 2 convT s2, input scale divisor)
+    ("enc1", 32, 64, 0, 1), ("enc2", 64, 128, 1, 1), ("enc3", 128, 256, 1, 2), ("enc4", 256, 512, 1, 4),
+    ("bottleneck", 512, 512, 0, 8), ("dec4", 512, 256, 2, 8), ("dec3", 256, 128, 2, 4), ("dec2", 128, 64, 2, 2)]
+USTEP_LAYERS = (0, 5, 7)   # csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip
+
+
+def time_step_layers(engine, B, H, W, dev, reps=50):
+    """Average launch duration of each kernel of the reverse loop's UNet step, launched exactly as the loop
+    launches it (the engine's packed step weights and folded biases; ustep.hip for USTEP_LAYERS under
+    use_step 2, else uconv.hip), timed as a dependent chain of `reps` launches in one hipGraph with HIP
+    events on the launching stream.  dec1 runs fused with the DDIM update and is not timed alone."""
     from ldm_amd import _lib as L
-    from ldm_amd import ops
+    lib = L.load()
+    shape = engine.shape(B, 32, H, W)
     w = engine.weights(shape)
-    names = ["enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "dec2", "dec1",
-             "ca2.q", "ca2.kv", "ca2.out", "ca1.q", "ca1.kv", "ca1.out"]
-    plans = list(w.conv_plan) + [w.ca_plan_q[0], w.ca_plan_kv[0], w.ca_plan_o[0],
-                                 w.ca_plan_q[1], w.ca_plan_kv[1], w.ca_plan_o[1]]
-    wptr = list(w.conv_w) + [w.ca_wq[0], w.ca_wkv[0], w.ca_wo[0], w.ca_wq[1], w.ca_wkv[1], w.ca_wo[1]]
-    bptr = list(w.conv_b) + [w.ca_bq[0], w.ca_bkv[0], w.ca_bo[0], w.ca_bq[1], w.ca_bkv[1], w.ca_bo[1]]
     out = {}
-    st = torch.cuda.current_stream()
-    for i, name in enumerate(names):
-        d = L.ConvDesc()
-        L.call("ldm_unet_layer_desc", ctypes.byref(shape), i, ctypes.byref(d))
-        x = torch.randn(d.B, d.Cin, d.Hin, d.Win, device=dev)
-        y = torch.empty(d.B, d.Cout, d.Hout, d.Wout, device=dev)
-        ep = L.Epilogue()
-        ep.bias = bptr[i]
-        ep.act = 1 if i < 8 else 0
-        plan = plans[i]
-        ws = torch.zeros(max(1, int(plan.ws_floats)), device=dev)     # split-K counters + partials
-        args = (ctypes.byref(d), ctypes.byref(plan), x.data_ptr(), wptr[i], ctypes.byref(ep), y.data_ptr(),
-                ws.data_ptr())
-        lib = L.load()
-        L.check(lib.ldm_conv_forward_ws(*args, st.cuda_stream), name)
-        us = _graph_time_us(lambda: lib.ldm_conv_forward_ws(*args, torch.cuda.current_stream().cuda_stream), reps)
-        fl, by = layer_flops(d), layer_bytes(d)
+    for layer, (name, cin, cout, mode, div) in enumerate(STEP_LAYERS):
+        hin, win = H // div, W // div
+        hout, wout = (hin, win) if mode == 0 else ((hin // 2, win // 2) if mode == 1 else (2 * hin, 2 * win))
+        x = torch.randn(B, hin, win, cin, device=dev)
+        y = torch.empty(B, hout, wout, cout, device=dev)
+        bias = w.step_pb[layer - 3] if layer in (3, 4) else w.conv_b[layer]
+        bc = torch.randn(B, cout, device=dev) if layer == 1 else None
+        sk = torch.randn(B, hout, wout, cout, device=dev) if mode == 2 else None
+        v3 = int(w.use_step) == 2 and layer in USTEP_LAYERS and B % 4 == 0 and (H, W) == (16, 64)
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else 0
+        ws = torch.zeros(max(1, nws), device=dev)
+        args = (x.data_ptr(), w.step_w[layer], bias, None if bc is None else bc.data_ptr(),
+                None if sk is None else sk.data_ptr(), y.data_ptr())
+
+        def run():
+            stp = torch.cuda.current_stream().cuda_stream
+            if v3:
+                return lib.ldm_ustep_conv(layer, B, *args, ws.data_ptr() if nws else None, stp)
+            return lib.ldm_step_conv(layer, B, H, W, *args, stp)
+
+        L.check(run(), name)
+        us = _graph_time_us(run, reps)
+        taps = 9 if mode < 2 else 2.25
+        fl = 2.0 * B * cout * hout * wout * cin * taps
+        by = 4.0 * (cin * cout * 9 + B * cin * hin * win + B * cout * hout * wout)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "plan": list(plan.key())}
-    # attention cores
-    for name, E, Lt in (("attn2", 256, shape.H * shape.W // 16), ("attn1", 512, shape.H * shape.W // 64)):
-        q = torch.randn(shape.B, E, Lt, device=dev)
-        kv = torch.randn(shape.B, 2 * E, Lt, device=dev)
-        o = torch.empty_like(q)
-        scale = float((1.0 / (E // 4)) ** 0.5)
-        lib = L.load()
-        us = _graph_time_us(lambda: lib.ldm_attention_core(q.data_ptr(), kv.data_ptr(), o.data_ptr(), shape.B, E, 4,
-                                                           Lt, Lt, scale, torch.cuda.current_stream().cuda_stream),
-                            reps)
-        fl = 4.0 * shape.B * E * Lt * Lt
-        by = 4.0 * shape.B * 4 * E * Lt
-        out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by}
-        # the reverse loop's folded form: scores from the projection input z against scale*Wq^T K
-        z = torch.randn(shape.B, Lt, E, device=dev)
-        kf = torch.randn(shape.B, 4, Lt, E, device=dev)
-        bf = torch.randn(shape.B, 4, Lt, device=dev)
+                     "flops": fl, "bytes": by, "kernel": ("ustep_kernel<%d>" % layer) if v3 else "uconv_kernel"}
+    # the folded cross-attentions of the loop
+    for name, E, Lt in (("attn2_folded", 256, H * W // 16), ("attn1_folded", 512, H * W // 64)):
+        z = torch.randn(B, Lt, E, device=dev)
+        kv = torch.randn(B, 2 * E, Lt, device=dev)
+        kf = torch.randn(B, 4, Lt, E, device=dev)
+        bf = torch.randn(B, 4, Lt, device=dev)
+        o = torch.empty(B, Lt, E, device=dev)
         us = _graph_time_us(lambda: lib.ldm_attention_folded(z.data_ptr(), kv.data_ptr(), kf.data_ptr(), bf.data_ptr(),
-                                                             o.data_ptr(), shape.B, E, 4, Lt, Lt,
+                                                             o.data_ptr(), B, E, 4, Lt, Lt,
                                                              torch.cuda.current_stream().cuda_stream), reps)
-        fl = 2.0 * shape.B * 4 * Lt * Lt * E + 2.0 * shape.B * E * Lt * Lt
-        by = 4.0 * shape.B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
-        out[name + "f"] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                           "flops": fl, "bytes": by}
+        fl = 2.0 * B * 4 * Lt * Lt * E + 2.0 * B * E * Lt * Lt
+        by = 4.0 * B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
+        out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
+                     "flops": fl, "bytes": by, "kernel": "attention_mfma_kernel (folded)"}
     return out
 
 
-def cpu_baseline(ldm, batch, times, eta, seconds):
-    """The oracle's torch-CPU restatement of the reference loop (oracle/ldm_torch_cpu.py), fp32, on this
-    box's host cores, over a bounded number of denoising iterations of the same workload."""
-    from oracle import ldm_torch_cpu as TC
+def cpu_env():
+    """Host cores for the CPU baseline: every core of this process's affinity mask, capped by the CPU share
+    the box declares for one GPU (OMP_NUM_THREADS; the GPU box sets 16), and the CPU model name."""
     try:
-        ncores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncores = os.cpu_count() or 1
-    ncores = max(1, min(ncores, 16))   # the GPU box's CPU share per GPU (16)
-    torch.set_num_threads(ncores)
-    sd = {k: v.detach().float().cpu() for k, v in ldm.state_dict().items()}
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(aff, share) if share > 0 else aff)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"affinity_cores": aff, "threads": threads, "model": model}
+
+
+def _median_s(fn, warmups=3, runs=10):
+    """3 warm-up runs, then the median of >= 10 timed runs (seconds)."""
+    for _ in range(warmups):
+        fn()
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts
+
+
+def _cpu_model(ldm):
+    return {k: v.detach().float().cpu().clone() for k, v in ldm.state_dict().items()}
+
+
+def cpu_baseline(ldm, batch, times, eta):
+    """Configs 2 / 5 on the host: one denoising iteration (UNet forward + DDIM update) of the same workload
+    in the oracle's torch-CPU restatement of the reference loop (oracle/ldm_torch_cpu.py), fp32."""
+    from oracle import ldm_torch_cpu as TC
+    env = cpu_env()
+    torch.set_num_threads(env["threads"])
+    sd = _cpu_model(ldm)
     ab = TC.schedule(200)[2]
-    g = torch.Generator().manual_seed(5)
+    g = torch.Generator().manual_seed(1)
     style = torch.rand(batch, 1, 128, 512, generator=g)
-    x = torch.randn(batch, 32, 16, 64, generator=g)
+    torch.manual_seed(1234)
+    x = torch.randn(batch, 32, 16, 64)
     with torch.no_grad():
         emb = TC.style_encoder(sd, style)
         s5, s6 = emb["s5"], emb["s6"]
-        TC.reverse_loop(sd, ab, x, s5, s6, times[:2], eta)        # warm-up (1 iteration)
-        n, t0 = 0, time.perf_counter()
-        while True:
-            i = n % (len(times) - 1)
+        k = [0]
+
+        def one():   # one iteration, walking the schedule like the loop does
+            i = k[0] % (len(times) - 1)
             TC.reverse_loop(sd, ab, x, s5, s6, times[i:i + 2], eta)
-            n += 1
-            if time.perf_counter() - t0 >= seconds and n >= 3:
-                break
-        dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "steps/s", "cores": ncores, "kind": "port",
-            "sample": f"{n} DDIM iterations (UNet fwd + update, batch {batch}, [{batch},32,16,64] latents, fp32) "
-                      f"of the same 50-step schedule, torch-CPU restatement oracle/ldm_torch_cpu.py, {dt:.1f}s"}
+            k[0] += 1
+        med, ts = _median_s(one)
+    return {"value": round(1.0 / med, 3), "unit": "steps/s", "cores": env["threads"], "kind": "port",
+            "cpu_model": env["model"], "affinity_cores": env["affinity_cores"],
+            "sample": f"median of {len(ts)} single DDIM iterations after 3 warm-ups (UNet forward + update, batch "
+                      f"{batch}, [{batch},32,16,64] latents, eta={eta}, fp32), torch-CPU restatement "
+                      f"oracle/ldm_torch_cpu.py; runs {min(ts):.3f}-{max(ts):.3f} s"}
+
+
+def cpu_leg_forward(ldm):
+    """Config 1 on the host: LDM.forward (encode -> q_sample -> UNet -> predict_start -> decode) + the
+    diffusion / compression (MSE + KL) losses, batch 1, oracle/ldm_torch_cpu.py, fp32."""
+    from oracle import ldm_torch_cpu as TC
+    env = cpu_env()
+    torch.set_num_threads(env["threads"])
+    sd = _cpu_model(ldm)
+    ab = TC.schedule(200)[2]
+    g = torch.Generator().manual_seed(0)
+    content = torch.rand(1, 1, 128, 512, generator=g)
+    style = torch.rand(1, 1, 128, 512, generator=torch.Generator().manual_seed(1))
+    t = torch.randint(0, 200, (1,), generator=torch.Generator().manual_seed(7))
+    eps = torch.randn(1, 32, 16, 64, generator=torch.Generator().manual_seed(11))
+
+    def one():
+        with torch.no_grad():
+            o = TC.ldm_forward(sd, content, style, t, eps, ab)
+            loss = torch.mean((o["noise_pred"] - o["noise"]) ** 2) + torch.mean((o["reconstructed"] - content) ** 2) \
+                + TC.kl_loss(o["z_0"])
+        return float(loss)
+    med, ts = _median_s(one)
+    return {"value": round(1.0 / med, 3), "unit": "forward+loss/s", "cores": env["threads"], "kind": "port",
+            "cpu_model": env["model"],
+            "sample": f"config 1: median of {len(ts)} LDM.forward + loss at batch 1 after 3 warm-ups, "
+                      f"oracle/ldm_torch_cpu.py; {med * 1e3:.1f} ms each"}
+
+
+def cpu_leg_train(ldm, batch=8):
+    """Config 3 on the host: the train step's arithmetic (frozen VAE encode, style encode, q_sample, UNet,
+    decode, diffusion + compression losses, backward through the trained modules, Adam) in the oracle's
+    torch-CPU restatement under autograd, fp32, on a small batch (samples/s scales ~linearly)."""
+    from oracle import ldm_torch_cpu as TC
+    env = cpu_env()
+    torch.set_num_threads(env["threads"])
+    sd = _cpu_model(ldm)
+    trained = [k for k in sd if not k.startswith("encoder.") and sd[k].is_floating_point()
+               and "running_" not in k and "num_batches" not in k]
+    for k in trained:
+        sd[k].requires_grad_(True)
+    opt = torch.optim.Adam([sd[k] for k in trained], lr=1e-4)
+    ab = TC.schedule(200)[2]
+    g = torch.Generator().manual_seed(0)
+    content = torch.rand(batch, 1, 128, 512, generator=g)
+    style = torch.rand(batch, 1, 128, 512, generator=torch.Generator().manual_seed(1))
+    t = torch.randint(0, 200, (batch,), generator=torch.Generator().manual_seed(7))
+    eps = torch.randn(batch, 32, 16, 64, generator=torch.Generator().manual_seed(11))
+
+    def one():
+        opt.zero_grad()
+        o = TC.ldm_forward(sd, content, style, t, eps, ab, train_decoder=True)
+        loss = torch.mean((o["noise_pred"] - o["noise"]) ** 2) + torch.mean((o["reconstructed"] - content) ** 2) \
+            + TC.kl_loss(o["z_0"])
+        loss.backward()
+        opt.step()
+    med, ts = _median_s(one, warmups=3, runs=10)
+    return {"value": round(batch / med, 3), "unit": "samples/s", "cores": env["threads"], "kind": "port",
+            "cpu_model": env["model"],
+            "sample": f"config 3: median of {len(ts)} train steps at batch {batch} after 3 warm-ups (fwd + bwd + "
+                      f"Adam, fp32), oracle/ldm_torch_cpu.py under autograd; {med:.2f} s each"}
 
 
 TRAIN_GFLOP_PER_SAMPLE = 10.7   # SURVEY.md §8(d): frozen VAE enc fwd 0.698 + 3 x (style enc 1.642 + UNet 0.449 + dec 1.242)
@@ -266,6 +362,10 @@ def main():
 
     if args.workload == "train":
         result = run_train(args, world, rank, dev, M)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            torch.manual_seed(0)
+            result["cpu_baseline"] = cpu_leg_train(M.LDM(32, pretrained_path="").eval())
+            result["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
         if rank == 0:
             print(json.dumps(result), flush=True)
         if world > 1:
@@ -346,9 +446,8 @@ def main():
 
     if rank == 0 and not args.no_kernel_timing:
         with torch.no_grad():
-            kt = time_layers(eng, eng.shape(B, 32, 16, 64), dev)
-        convs = {k: v for k, v in kt.items() if "plan" in v}
-        dom = max(convs, key=lambda k: convs[k]["us"])
+            kt = time_step_layers(eng, B, 16, 64, dev)
+        dom = max(kt, key=lambda k: kt[k]["us"])      # the longest launch of the step (the bottleneck conv)
         dk = kt[dom]
         traffic = None
         if os.path.exists(args.pmc):
@@ -358,15 +457,17 @@ def main():
                 traffic = pmc.get("per_launch_bytes", {}).get(dom)
             except (OSError, ValueError):
                 traffic = None
-        result["roofline"] = {"kernel": f"conv_mfma ({dom})", "bound": "mfma",
+        result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
                               "achieved": dk["tflops"], "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(dk["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                               "flops_per_launch": dk["flops"], "avg_launch_us": dk["us"]}
         result["kernels"] = {k: {kk: vv for kk, vv in v.items() if kk not in ("flops", "bytes")} for k, v in kt.items()}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(ldm, B, times, args.eta, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(ldm, B, times, args.eta)
         result["gpu_over_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
+        if args.workload == "sample" and not args.no_cpu_legs:
+            result["cpu_legs"] = {"config1": cpu_leg_forward(ldm), "config3": cpu_leg_train(ldm)}
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -46,7 +46,9 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a USTEP_DIAG/UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
-    ap.add_argument("--variant", default="ustep", choices=["uconv", "ustep"])
+    ap.add_argument("--variant", default="hybrid", choices=["uconv", "ustep", "hybrid"],
+                    help="hybrid = what use_step 2 runs: ustep for enc1/dec4/dec2, uconv otherwise")
+    ap.add_argument("--layers", default=None, help="comma list of layer indices (default all)")
     ap.add_argument("--loop-only", default=None, help="comma list of use_step values: only time the loop")
     args = ap.parse_args()
     B, H, W = (int(v) for v in args.shape.split("x"))
@@ -54,7 +56,11 @@ def main():
     dev = torch.device("cuda:0")
     lib = L.load()
     tot = 0.0
+    sel = None if args.layers is None else {int(v) for v in args.layers.split(",")}
     for layer, name in enumerate(NAMES if args.loop_only is None else []):
+        if sel is not None and layer not in sel:
+            continue
+        v3 = args.variant == "ustep" or (args.variant == "hybrid" and layer in (0, 5, 7))
         Cin, Cout, mode = LAYERS[layer]
         Hin, Win = H // DIV[layer], W // DIV[layer]
         Hout, Wout = (Hin, Win) if mode == 0 else ((Hin // 2, Win // 2) if mode == 1 else (2 * Hin, 2 * Win))
@@ -67,14 +73,14 @@ def main():
         sk = torch.randn(B, Hout, Wout, Cout, device=dev)
         y = torch.empty(B, Hout, Wout, Cout, device=dev)
 
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if args.variant == "ustep" else 0
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else 0
         ws = torch.zeros(max(nws, 1), device=dev)
 
         def run():
             bcp = bc.data_ptr() if layer == 1 else None
             skp = sk.data_ptr() if mode == 2 else None
             stp = torch.cuda.current_stream().cuda_stream
-            if args.variant == "ustep":
+            if v3:
                 rc = lib.ldm_ustep_conv(layer, B, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
                                         y.data_ptr(), ws.data_ptr() if nws else None, stp)
             else:
@@ -86,7 +92,7 @@ def main():
         fl = 2.0 * B * Cout * Hout * Wout * Cin * (9 if mode < 2 else 2.25)
         tot += us
         extra = ""
-        if args.stamps and args.variant == "ustep":
+        if args.stamps and v3:
             import numpy as np
             lib.ldm_debug_ustep_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
             graph_us(run, 10)          # stamps of the last launch of a 10-launch graph chain (warm)
