@@ -305,6 +305,8 @@ static int wgrad_splits(const WgradArgs& a) {
 
 extern "C" int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d) {
     if (!d) return -1;
+    int64_t f2 = 0;
+    if (wgrad2_plan_ws(*d, f2)) return f2;
     WgradArgs a;
     int kk;
     if (wgrad_setup(*d, a, kk)) return -1;
@@ -321,14 +323,23 @@ extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, 
     if (rc) return rc;
     a.dense = d->transposed ? x : dy;
     a.gath = d->transposed ? dy : x;
+    hipStream_t st = (hipStream_t)stream;
+    const int MN = a.M * a.N;
+    int S2 = 0;
+    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, st);   // the tap-shared form (wgrad.hip) where it applies
+    if (rc > 0) return rc;
+    if (rc == 0) {
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)workspace, S2,
+                           MN, dw, accumulate);
+        LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
+        return 0;
+    }
     const int S = wgrad_splits(a);
     a.per_split = (a.nchunk + S - 1) / S;
     a.partial = workspace;
-    hipStream_t st = (hipStream_t)stream;
     dim3 grid((a.N + 15) / 16, (a.M + 15) / 16, S);
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(64), 0, st, a);
     LDM_CHECK_LAUNCH("wgrad_kernel");
-    const int MN = a.M * a.N;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)a.partial, S, MN,
                        dw, accumulate);
     LDM_CHECK_LAUNCH("wgrad_reduce_kernel");

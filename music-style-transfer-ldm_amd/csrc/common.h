@@ -149,6 +149,11 @@ bool ustep_supported(int B, int H, int W);
 int64_t ustep_workspace_floats(int layer, int B, int64_t* cnt_floats = nullptr);
 int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 
+// wgrad.hip: the tap-shared weight-gradient kernel (ldm_conv_backward_weight where it applies)
+bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats);
+int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits,
+               hipStream_t st);
+
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.
 __device__ __forceinline__ float ddim_update(float xv, float e, const float* coef, float eta, float& x0) {

@@ -64,6 +64,7 @@ struct ConvArgs {
     FastDiv fd_cpt;        // K chunk -> (tap, channel chunk)
     FastDiv fd_np, fd_inner;   // block -> (phase, tile), tile -> (outer, inner) of the XCD order
     FastDiv fd_nn, fd_nm;      // natural order: block -> (N-tile, M-tile, phase)
+    FastDiv fd_dwo, fd_dho, fd_dco;   // direct kernel: output index -> (b, co, oy, ox)
     PhaseTable pt;
     // Per-phase scalars of the MFMA kernel, indexed [phase] and read at static offsets (one batch of
     // scalar loads, then a select by phase: a load indexed by the runtime phase would be a second,
@@ -813,16 +814,30 @@ extern "C" int ldm_debug_stamps(unsigned long long* host, int nblocks) {
 // ------------------------------------------------------------------------------------------------
 // kind 0: direct VALU conv (Cin not a multiple of 8, or tiny Cout: VAE first/last layers)
 // ------------------------------------------------------------------------------------------------
+// One output per lane, 32-bit index arithmetic by multiply-high (the host guarantees < 2^31 outputs): the
+// 64-bit div/mod chains of a per-lane decomposition cost more than the arithmetic of these thin layers.
+// The phase table is indexed by a per-lane phase (the output parity of a transposed conv): it is copied
+// to LDS once per block, since a kernarg array indexed by a VGPR compiles to per-lane global loads.  The
+// taps' offsets and validity are resolved first, so that each channel's tap loads are independent (no
+// branch between them) and issue back to back.
 __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
-    const int64_t total = (int64_t)a.B * a.Cout * a.Hout * a.Wout;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int tab[kMaxPhase * kMaxTap * 3 + kMaxPhase];   // dy, dx, kk [phase][tap], ntap[phase]
+    for (int i = threadIdx.x; i < kMaxPhase * kMaxTap * 3 + kMaxPhase; i += blockDim.x) {
+        const int which = i / (kMaxPhase * kMaxTap), e = i - which * (kMaxPhase * kMaxTap);
+        const int ph = e / kMaxTap, t = e - ph * kMaxTap;
+        tab[i] = which == 0 ? a.pt.dy[ph][t] : which == 1 ? a.pt.dx[ph][t] : which == 2 ? a.pt.kk[ph][t]
+                                                                                      : a.pt.ntap[e < kMaxPhase ? e : 0];
+    }
+    __syncthreads();
+    const int total = a.B * a.Cout * a.Hout * a.Wout;
+    const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (idx >= total) return;
-    const int ox = (int)(idx % a.Wout);
-    int64_t rest = idx / a.Wout;
-    const int oy = (int)(rest % a.Hout);
-    rest /= a.Hout;
-    const int co = (int)(rest % a.Cout);
-    const int b = (int)(rest / a.Cout);
+    int rest = a.fd_dwo.div(idx);
+    const int ox = idx - rest * a.Wout;
+    int r2 = a.fd_dho.div(rest);
+    const int oy = rest - r2 * a.Hout;
+    const int b = a.fd_dco.div(r2);
+    const int co = r2 - b * a.Cout;
     int ph, qy, qx;
     if (a.pt.osy == 1) {
         ph = 0;
@@ -835,19 +850,69 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
     }
     const int HWin = a.Hin * a.Win;
     const float* xb = a.x + (size_t)b * a.Cin * HWin;
-    const size_t wci = a.transposed ? (size_t)a.Cout * a.KK : (size_t)a.KK;
+    const int wci = a.transposed ? a.Cout * a.KK : a.KK;
     const float* wb = a.w + (a.transposed ? (size_t)co * a.KK : (size_t)co * a.Cin * a.KK);
+    const int nt = tab[kMaxPhase * kMaxTap * 3 + ph];
+    int off[kMaxTap], wkk[kMaxTap];
+    bool ok[kMaxTap];
+#pragma unroll
+    for (int t = 0; t < kMaxTap; ++t) {
+        const int e = ph * kMaxTap + t;
+        const int iy = qy * a.pt.sy + tab[e];
+        const int ix = qx * a.pt.sy + tab[kMaxPhase * kMaxTap + e];
+        ok[t] = t < nt && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+        off[t] = ok[t] ? iy * a.Win + ix : 0;
+        wkk[t] = t < nt ? tab[2 * kMaxPhase * kMaxTap + e] : 0;
+    }
     float acc = 0.f;
-    const int nt = a.pt.ntap[ph];
-    for (int t = 0; t < nt; ++t) {
-        const int iy = qy * a.pt.sy + a.pt.dy[ph][t];
-        const int ix = qx * a.pt.sy + a.pt.dx[ph][t];
-        if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
-        const float* xp = xb + iy * a.Win + ix;
-        const float* wq = wb + a.pt.kk[ph][t];
-        for (int ci = 0; ci < a.Cin; ++ci) acc = fmaf(xp[(size_t)ci * HWin], wq[ci * wci], acc);
+    for (int ci = 0; ci < a.Cin; ++ci) {
+        const float* xp = xb + (size_t)ci * HWin;
+        const float* wq = wb + (size_t)ci * wci;
+        float xv[kMaxTap], wv[kMaxTap];
+#pragma unroll
+        for (int t = 0; t < kMaxTap; ++t) {
+            xv[t] = t < nt ? xp[off[t]] : 0.f;
+            wv[t] = t < nt ? wq[wkk[t]] : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < kMaxTap; ++t)
+            if (ok[t]) acc = fmaf(xv[t], wv[t], acc);
     }
     epilogue_store(a, co, b, oy, ox, acc);
+}
+
+// Single-input-channel conv (the VAE encoder's and the style encoder's first layers, 1 -> 64 on 128x512
+// mels): one lane per output pixel computes every output channel from one k x k window read, with the
+// Cout x k*k weights in LDS; the stores stay coalesced (consecutive lanes = consecutive ox per channel).
+__global__ __launch_bounds__(256) void conv_cin1_kernel(ConvArgs a) {
+    __shared__ float ws[64 * 16];
+    for (int i = threadIdx.x; i < a.Cout * a.KK; i += blockDim.x) ws[i] = a.w[i];   // [co][kh*kw]
+    __syncthreads();
+    const int total = a.B * a.Hout * a.Wout;
+    const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (idx >= total) return;
+    const int rest = a.fd_dwo.div(idx);
+    const int ox = idx - rest * a.Wout;
+    const int b = a.fd_dho.div(rest);
+    const int oy = rest - b * a.Hout;
+    const float* xb = a.x + (size_t)b * a.Hin * a.Win;
+    float xv[kMaxTap];
+    bool ok[kMaxTap];
+    const int nt = a.pt.ntap[0];
+#pragma unroll
+    for (int t = 0; t < kMaxTap; ++t) {
+        const int iy = oy * a.pt.sy + a.pt.dy[0][t];
+        const int ix = ox * a.pt.sy + a.pt.dx[0][t];
+        ok[t] = t < nt && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+        xv[t] = xb[ok[t] ? iy * a.Win + ix : 0];
+    }
+    for (int co = 0; co < a.Cout; ++co) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < kMaxTap; ++t)
+            if (ok[t]) acc = fmaf(xv[t], ws[co * a.KK + a.pt.kk[0][t]], acc);
+        epilogue_store(a, co, b, oy, ox, acc);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1150,6 +1215,16 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     if (p.kind == 0) {
         LDM_REQUIRE(d.layout == 0, "conv: the direct kernel supports NCHW tensors only");
         const int64_t total = (int64_t)d.B * d.Cout * d.Hout * d.Wout;
+        LDM_REQUIRE(total < 0x7fffffffLL, "conv: the direct kernel indexes outputs in 32 bits");
+        a.fd_dwo = FastDiv::make(d.Wout);
+        a.fd_dho = FastDiv::make(d.Hout);
+        a.fd_dco = FastDiv::make(d.Cout);
+        if (d.Cin == 1 && !d.transposed && d.Cout <= 64 && a.KK <= 16) {
+            const int64_t pix = (int64_t)d.B * d.Hout * d.Wout;
+            hipLaunchKernelGGL(conv_cin1_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, st, a);
+            LDM_CHECK_LAUNCH("conv_cin1_kernel");
+            return 0;
+        }
         hipLaunchKernelGGL(conv_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
         LDM_CHECK_LAUNCH("conv_direct_kernel");
         return 0;

@@ -1,0 +1,296 @@
+// Conv / transposed-conv weight gradient of the train step (LDMTrainer.train_step, train.py:163-208:
+// scaler.scale(loss).backward() through every trained conv) as a tap-shared implicit GEMM for gfx950.
+//
+//   dW[m][c][t] = sum_{b,q} Dense[b][m][q] * Gath[b][c][q*s + d_t],   d_t = (kh - pad, kw - pad)
+//   conv  (w [Cout][Cin][k][k]):  Dense = dY (m = co, q over Hout x Wout), Gath = X,  s = stride
+//   convT (w [Cin][Cout][k][k]):  Dense = X  (m = ci, q over Hin  x Win ), Gath = dY, s = stride
+//
+// One block owns a BM (m) x BC (c) tile for ALL k*k taps and walks a slice of K = (b, q) in chunks of 64
+// output positions (one 64-wide row segment, or 64/Wq whole rows).  Per chunk it DMAs into LDS (16 B per
+// lane, buffer_load ... lds) the Dense rows [BM][64] and the Gath window the chunk's taps touch,
+// [BC][WR][WCa] (borders and channels past C arrive as zeros: the window origin is aligned down to 4
+// floats, so a 16-B piece is either inside the image row or wholly outside it).  Every Dense fragment is
+// then read once per 16 positions and reused by all k*k taps, every window value by every tap that
+// covers it: the previous kernel (backward.hip) gathered 4 scalars per lane per tap from global memory.
+// Chunks are double-buffered: the DMAs of chunk i+1 are issued before chunk i is multiplied.
+// K is split over blocks (grid.z) into fixed ranges; wgrad_reduce_kernel sums the partials in split
+// order, so the result is bitwise reproducible.
+// MFMA v_mfma_f32_16x16x4_f32: lane l = (col l&15, group g = l>>4); for the 16 positions of step u the
+// lane supplies positions 16u + 4g + j at MFMA j (A as one float4 from LDS, B as 4 window values).
+#include <type_traits>
+#include <utility>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace ldm {
+namespace wg {
+
+struct Args {
+    const float* dense;   // [B][M][Hq*Wq]
+    const float* gath;    // [B][C][Hg][Wg]
+    float* partial;       // [S][M][C*T]
+    int32_t B, M, C, Hq, Wq, Hg, Wg, pad;
+    int32_t cols, rows;   // chunk = rows x cols output positions (cols = min(Wq, 64), rows = 64 / cols)
+    int32_t cps;          // chunks per sample
+    int32_t nchunk, per_split;
+    int32_t wr, wca, e;   // window rows, row pitch (floats, multiple of 4), column shift of the aligned origin
+    int32_t pitch_c;      // floats per channel in the window (wr * wca)
+};
+
+template <int B_, int E_, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B_ < E_) {
+        f(std::integral_constant<int, B_>{});
+        static_for<B_ + 1, E_>(f);
+    }
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+constexpr int kOOB = 0x7ffffff0;
+constexpr int kKQ = 64;   // output positions per chunk
+
+template <int S, int KK, int BM, int BC>
+struct Cfg {
+    static constexpr int T = KK * KK;
+    static constexpr int WCF = BC / 16, WMF = 4 / WCF, FM = BM / 16 / WMF;   // 4 waves: WMF x WCF, FM m-frags each
+    static_assert(WMF * WCF == 4 && FM >= 1 && FM * 16 * WMF == BM, "wave layout");
+    static constexpr int A_FLOATS = BM * kKQ;
+};
+
+// floats of one LDS buffer: A rows + the window rounded up to whole wave-instructions (64 pieces)
+__host__ __device__ inline int buf_floats(int a_floats, int bc, int pitch_c) {
+    return a_floats + (bc * pitch_c + 255) / 256 * 256;
+}
+
+template <int S, int KK, int BM, int BC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad_kernel(Args a) {
+    using g = Cfg<S, KK, BM, BC>;
+    constexpr int T = g::T, WCF = g::WCF, FM = g::FM, AF = g::A_FLOATS;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wc = wave % WCF, wm = wave / WCF;
+    const int col = lane & 15, lg = lane >> 4;
+    const int m0 = blockIdx.y * BM, c0 = blockIdx.x * BC;
+    const int HQ = a.Hq * a.Wq;
+    const int bufF = buf_floats(AF, BC, a.pitch_c);
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 4), 0x00020000);
+
+    // chunk -> (sample, first output row, first output column)
+    auto chunk_geo = [&](int ch, int& b, int& qy0, int& qx0) {
+        b = ch / a.cps;
+        const int r = ch - b * a.cps;
+        if (a.cols == a.Wq) {   // whole rows
+            qy0 = r * a.rows, qx0 = 0;
+        } else {                // 64-wide segments of one row
+            const int segs = a.Wq / kKQ;
+            qy0 = r / segs, qx0 = (r - qy0 * segs) * kKQ;
+        }
+    };
+    // DMA of chunk ch into buffer buf: A = BM rows x 64 positions (XOR-swizzled 16-B pieces), then the
+    // window [BC][wr][wca]; the work is dealt round-robin over all 256 lanes' 16-B pieces.
+    auto issue = [&](int ch, int buf) {
+        int b, qy0, qx0;
+        chunk_geo(ch, b, qy0, qx0);
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+        // A: BM*16 pieces = BM/4 wave-instructions
+        for (int gi = wave; gi < BM / 4; gi += 4) {
+            const int row = gi * 4 + (lane >> 4);
+            const int p = lane & 15;                       // destination piece
+            const int sp = p ^ (row & 15);                  // source piece
+            const int m = m0 + row;
+            const int ql = sp * 4;                          // chunk-local position of the piece
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const bool ok = m < a.M && qy < a.Hq;
+            const int voff = ok ? (((b * a.M + m) * HQ + qy * a.Wq + qx) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(base + gi * 1024), 16, voff, 0, 0, 0);
+        }
+        // window: BC * wr * wca / 4 pieces
+        const int wq4 = a.wca >> 2;
+        const int npiece = BC * a.wr * wq4;
+        const int row0 = qy0 * S - a.pad, colA = qx0 * S - a.pad - a.e;
+        for (int gi = wave; gi * 64 < npiece; gi += 4) {
+            const int pc = gi * 64 + lane;
+            const int cl = pc / (a.wr * wq4);
+            const int rem = pc - cl * (a.wr * wq4);
+            const int wrow = rem / wq4, wp = rem - wrow * wq4;
+            const int c = c0 + cl, iy = row0 + wrow, ix = colA + wp * 4;
+            const bool ok = pc < npiece && c < a.C && (unsigned)iy < (unsigned)a.Hg && (unsigned)ix < (unsigned)a.Wg;
+            const int voff = ok ? ((((b * a.C + c) * a.Hg + iy) * a.Wg + ix) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + AF * 4 + gi * 1024), 16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx4 acc[T][FM];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[t][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // per-lane LDS offsets inside a buffer: A row pieces, window column of position 16u + 4g (+ j*S)
+    int aoff[FM][4];
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int row = (wm * FM + f) * 16 + col;
+            aoff[f][u] = row * kKQ + (((4 * u + lg) ^ (row & 15)) << 2);
+        }
+    int boff[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        // positions past the chunk's rows (a small image zero-padded to 64) multiply zeros of A: point them
+        // at position 0 so that they read finite window values (0 * NaN from stale LDS would be NaN)
+        const int ql = (16 * u + 4 * lg < a.rows * a.cols) ? 16 * u + 4 * lg : 0;
+        const int rl = ql / a.cols, xl = ql - rl * a.cols;
+        boff[u] = AF + (wc * 16 + col) * a.pitch_c + rl * S * a.wca + a.e + xl * S;
+    }
+
+    if (ch_begin < ch_end) issue(ch_begin, 0);
+    for (int ch = ch_begin; ch < ch_end; ++ch) {
+        const int buf = (ch - ch_begin) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // chunk ch landed everywhere; every wave is done with the other buffer
+        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+        const float* sb = smem + buf * bufF;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            floatx4 fa[FM];
+#pragma unroll
+            for (int f = 0; f < FM; ++f) fa[f] = *reinterpret_cast<const floatx4*>(sb + aoff[f][u]);
+            static_for<0, T>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                constexpr int ky = t / KK, kx = t % KK;
+                const float* bp = sb + boff[u] + ky * a.wca + kx;
+                float bv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bv[j] = bp[j * S];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int f = 0; f < FM; ++f)
+                        acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[f][j], bv[j], acc[t][f], 0, 0, 0);
+            });
+        }
+    }
+
+    // partial tile: rows m = m0 + 16*(wm*FM+f) + 4g + r, column c = c0 + 16*wc + col, T taps contiguous
+    const int N = a.C * T;
+    const int c = c0 + wc * 16 + col;
+    if (c < a.C) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * N;
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + (wm * FM + f) * 16 + 4 * lg + r;
+                if (m < a.M) {
+                    float* o = out + (size_t)m * N + (size_t)c * T;
+#pragma unroll
+                    for (int t = 0; t < T; ++t) o[t] = acc[t][f][r];
+                }
+            }
+    }
+}
+
+struct Plan {
+    int S, KK, BM, BC, splits;
+    Args a;
+    int lds_bytes;
+};
+
+// Geometry and instance choice; false when this form does not apply (the caller keeps backward.hip's).
+bool plan(const ldm_conv_desc& d, Plan& p) {
+    if (d.kh != d.kw || (d.kh != 3 && d.kh != 4) || (d.stride != 1 && d.stride != 2) || d.pad < 0 || d.pad > 3)
+        return false;
+    Args a{};
+    a.B = d.B;
+    if (!d.transposed) {
+        a.M = d.Cout, a.C = d.Cin, a.Hq = d.Hout, a.Wq = d.Wout, a.Hg = d.Hin, a.Wg = d.Win;
+    } else {
+        a.M = d.Cin, a.C = d.Cout, a.Hq = d.Hin, a.Wq = d.Win, a.Hg = d.Hout, a.Wg = d.Wout;
+    }
+    a.pad = d.pad;
+    if (a.Wq % 4 || a.Wg % 4) return false;
+    if (a.Wq >= kKQ ? (a.Wq % kKQ != 0) : (kKQ % a.Wq != 0)) return false;
+    a.cols = a.Wq >= kKQ ? kKQ : a.Wq;
+    a.rows = kKQ / a.cols;
+    if (a.rows > a.Hq) a.rows = a.Hq;   // a small image: one chunk per sample, the rest zero-padded
+    a.cps = a.Wq >= kKQ ? a.Hq * (a.Wq / kKQ) : (a.Hq + a.rows - 1) / a.rows;
+    a.nchunk = a.B * a.cps;
+    const int KK = d.kh, S = d.stride;
+    a.e = ((a.pad % 4) == 0) ? 0 : 4 - (a.pad % 4);          // origin qx0*S - pad, qx0*S a multiple of 4
+    a.wr = (a.rows - 1) * S + KK;
+    const int wc = (a.cols - 1) * S + KK;
+    a.wca = (a.e + wc + 3) / 4 * 4;
+    a.pitch_c = a.wr * a.wca;
+    p.S = S, p.KK = KK;
+    p.BC = (a.C <= 16 || KK == 4) ? 16 : 32;
+    p.BM = (p.BC == 32 && a.M <= 32) ? 32 : 64;
+    p.lds_bytes = 2 * buf_floats(p.BM * kKQ, p.BC, a.pitch_c) * 4;
+    if (p.lds_bytes > 160 * 1024) return false;
+    const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + p.BC - 1) / p.BC);
+    int s = 1;
+    while (s < 256 && tiles * s < 512 && a.nchunk / (s * 2) >= 2) s *= 2;
+    p.splits = s;
+    a.per_split = (a.nchunk + s - 1) / s;
+    p.a = a;
+    return true;
+}
+
+template <int S, int KK, int BM, int BC>
+int launch(const Plan& p, hipStream_t st) {
+    auto kfn = wgrad_kernel<S, KK, BM, BC>;
+    static bool opted = false;
+    if (!opted) {
+        LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        opted = true;
+    }
+    dim3 grid((p.a.C + BC - 1) / BC, (p.a.M + BM - 1) / BM, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(256), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_kernel (tap-shared)");
+    return 0;
+}
+
+}  // namespace wg
+
+bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats) {
+    wg::Plan p;
+    if (!wg::plan(d, p)) return false;
+    ws_floats = (int64_t)p.splits * p.a.M * p.a.C * p.KK * p.KK;
+    return true;
+}
+
+// Runs the tap-shared kernel into `partial` ([splits][M][N]); returns the split count through `splits`,
+// or -1 when the form does not apply.
+int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits,
+               hipStream_t st) {
+    wg::Plan p;
+    if (!wg::plan(d, p)) return -1;
+    p.a.dense = dense;
+    p.a.gath = gath;
+    p.a.partial = partial;
+    splits = p.splits;
+    const int key = p.S * 1000 + p.KK * 100 + (p.BM == 64 ? 10 : 0) + (p.BC == 32 ? 1 : 0);
+    switch (key) {
+        case 1311: return wg::launch<1, 3, 64, 32>(p, st);
+        case 1301: return wg::launch<1, 3, 32, 32>(p, st);
+        case 1310: return wg::launch<1, 3, 64, 16>(p, st);
+        case 2311: return wg::launch<2, 3, 64, 32>(p, st);
+        case 2301: return wg::launch<2, 3, 32, 32>(p, st);
+        case 2310: return wg::launch<2, 3, 64, 16>(p, st);
+        case 2410: return wg::launch<2, 4, 64, 16>(p, st);
+        case 1410: return wg::launch<1, 4, 64, 16>(p, st);
+        default: return -1;
+    }
+}
+
+}  // namespace ldm

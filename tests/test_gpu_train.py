@@ -5,6 +5,7 @@ reference, §How-to-work); the whole train step against golden gradients / Adam 
 REFERENCE (tests/golden/make_goldens.py section 7).  Tolerance: max|g - g_ref| <= 1e-4 * max|g_ref|
 (north_star "within 1e-4 rel-fp32"); the optimiser update 1e-5 (elementwise, no reduction).
 """
+import ctypes
 import zlib
 
 import numpy as np
@@ -407,3 +408,51 @@ def test_trainer_epochs_reporting_plateau_checkpoints(cuda, tmp_path, monkeypatc
     assert ck.exists() and not (tmp_path / "models" / "pretrained" / "ldm_1.pth").exists()
     sd = torch.load(str(ck), map_location="cpu", weights_only=True)
     assert set(sd) == set(ldm.state_dict())
+
+
+# ---- tap-shared weight gradient (csrc/wgrad.hip) at the train step's shapes --------------------------
+# (B, Cin, Hin, Win, Cout, k, stride, pad, out_pad, transposed): one case per kernel instance / chunk form
+WGRAD_CASES = {
+    "style_enc2_k3s2_rowseg": (2, 64, 64, 256, 128, 3, 2, 1, 0, False),       # <2,3,64,32>, 64-wide segments
+    "unet_enc1_k3s1": (2, 32, 16, 64, 64, 3, 1, 1, 0, False),                 # <1,3,64,32>
+    "unet_dec1_k3s1_m32": (2, 64, 16, 64, 32, 3, 1, 1, 0, False),             # <1,3,32,32>
+    "unet_bottleneck_small_image": (2, 512, 2, 8, 512, 3, 1, 1, 0, False),    # one zero-padded chunk / sample
+    "unet_dec4_convT": (2, 512, 2, 8, 256, 3, 2, 1, 1, True),                 # <2,3,64,32> on the input grid
+    "unet_dec2_convT_rows": (2, 128, 8, 32, 64, 3, 2, 1, 1, True),            # 2 whole rows per chunk
+    "vae_dec0_convT_k4_m32": (2, 32, 16, 64, 128, 4, 2, 1, 0, True),          # <2,4,64,16>, M < BM
+    "vae_dec2_convT_k4_c1": (1, 64, 64, 256, 1, 4, 2, 1, 0, True),            # C = 1
+    "style_enc1_cin1": (1, 1, 128, 512, 64, 3, 2, 1, 0, False),               # <2,3,64,16>, C = 1
+    "style_enc6_k3s2": (2, 256, 4, 16, 512, 3, 2, 1, 0, False),
+    "k3s1_c8_b3": (3, 8, 16, 32, 24, 3, 1, 1, 0, False),                      # <1,3,64,16>, M, C ragged
+}
+
+
+@pytest.mark.parametrize("case", sorted(WGRAD_CASES))
+def test_wgrad_tap_shared(cuda, case):
+    """dW of ldm_conv_backward_weight against float64 torch autograd (1e-5 rel: fp32 MFMA sums over
+    K = B*Hq*Wq in split order), twice bitwise equal, and accumulate=1 adding onto dW."""
+    from ldm_amd import _lib as L, ops
+    B, Cin, H, W, Cout, k, s, p, op, tr = WGRAD_CASES[case]
+    seed = zlib.crc32(case.encode()) % 1000
+    x = _rand((B, Cin, H, W), seed)
+    wshape = (Cin, Cout, k, k) if tr else (Cout, Cin, k, k)
+    w = _rand(wshape, seed + 1, -0.2, 0.2)
+    xt = torch.from_numpy(x).double()
+    wt = torch.from_numpy(w).double().requires_grad_()
+    if tr:
+        v = tF.conv_transpose2d(xt, wt, None, stride=s, padding=p, output_padding=op)
+    else:
+        v = tF.conv2d(xt, wt, None, stride=s, padding=p)
+    dy = _rand(tuple(v.shape), seed + 5)
+    (v * torch.from_numpy(dy).double()).sum().backward()
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, s, p, op, tr)
+    assert int(L.load().ldm_conv_wgrad_workspace_floats(ctypes.byref(desc))) > 0
+    xg, dyg = T(x, cuda), T(dy, cuda)
+    dw1 = ops.conv_backward_weight(xg, dyg, desc)
+    dw2 = ops.conv_backward_weight(xg, dyg, desc)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2)
+    assert rel_err(npy(dw1), wt.grad.numpy()) < 1e-5
+    acc = torch.ones_like(dw1)
+    ops.conv_backward_weight(xg, dyg, desc, dw=acc, accumulate=True)
+    assert rel_err(npy(acc), wt.grad.numpy() + 1.0) < 1e-5
