@@ -24,6 +24,8 @@ import torch  # noqa: E402
 
 METRIC = "UNet denoising steps/sec on 1×128×512 mel-latents, 1/2/4/8 MI355X"
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_*_f32) = FP32 vector peak
+LOWP_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16 / F16 dense MFMA peak
+DT_CODE = {"fp32": 0, "fp16": 1, "bf16": 2}
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 UNET_GFLOP_PER_SAMPLE = 0.4494   # SURVEY.md §8(d), torch FlopCounterMode-verified
 
@@ -40,6 +42,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="latents per GPU (8 sample/transfer, 32 train)")
     ap.add_argument("--timesteps", type=int, default=None, help="50 for sample, T'=100 for transfer")
     ap.add_argument("--eta", type=float, default=None, help="0.0 for sample, 1.0 for transfer")
+    ap.add_argument("--dtype", choices=("fp32", "fp16", "bf16"), default=None,
+                    help="step-kernel operand precision (fp32 accumulation and sampler state): fp32 for sample "
+                         "(config 2), fp16 for transfer (config 5)")
     ap.add_argument("--split", type=int, default=1,
                     help="run the per-GPU batch as this many sub-batch chains on separate streams (one graph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -54,6 +59,8 @@ def parse():
         a.timesteps = 100 if a.workload == "transfer" else 50
     if a.eta is None:
         a.eta = 1.0 if a.workload == "transfer" else 0.0
+    if a.dtype is None:
+        a.dtype = {"transfer": "fp16", "train": "bf16"}.get(a.workload, "fp32")
     return a
 
 
@@ -118,7 +125,8 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         bias = w.step_pb[layer - 3] if layer in (3, 4) else w.conv_b[layer]
         bc = torch.randn(B, cout, device=dev) if layer == 1 else None
         sk = torch.randn(B, hout, wout, cout, device=dev) if mode == 2 else None
-        v3 = int(w.use_step) == 2 and layer in USTEP_LAYERS and B % 4 == 0 and (H, W) == (16, 64)
+        dt = int(w.step_dtype)
+        v3 = int(w.use_step) == 2 and dt == 0 and layer in USTEP_LAYERS and B % 4 == 0 and (H, W) == (16, 64)
         nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else 0
         ws = torch.zeros(max(1, nws), device=dev)
         args = (x.data_ptr(), w.step_w[layer], bias, None if bc is None else bc.data_ptr(),
@@ -128,7 +136,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
             stp = torch.cuda.current_stream().cuda_stream
             if v3:
                 return lib.ldm_ustep_conv(layer, B, *args, ws.data_ptr() if nws else None, stp)
-            return lib.ldm_step_conv(layer, B, H, W, *args, stp)
+            return lib.ldm_step_conv_dt(layer, B, H, W, *args, dt, stp)
 
         L.check(run(), name)
         us = _graph_time_us(run, reps)
@@ -136,7 +144,8 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         fl = 2.0 * B * cout * hout * wout * cin * taps
         by = 4.0 * (cin * cout * 9 + B * cin * hin * win + B * cout * hout * wout)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "kernel": ("ustep_kernel<%d>" % layer) if v3 else "uconv_kernel"}
+                     "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else "uconv_kernel")
+                     + ("" if dt == 0 else (" fp16 operands" if dt == 1 else " bf16 operands"))}
     # the folded cross-attentions of the loop
     for name, E, Lt in (("attn2_folded", 256, H * W // 16), ("attn1_folded", 512, H * W // 64)):
         z = torch.randn(B, Lt, E, device=dev)
@@ -298,6 +307,9 @@ def run_train(args, world, rank, dev, M):
         from ldm_amd import dist as hdist                      # same initial weights on every rank
         hdist.broadcast_parameters(ldm)
     trainer = LDMTrainer(ldm, None, dev, lr=1e-4)                 # LDMTrainer default (train.py:142)
+    trainer.autocast_dtype = {"fp32": None, "fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    if args.dtype == "fp32":
+        os.environ["LDM_AMD_DTYPE"] = "fp32"                      # autocast region present, fp32 operands
     ldm.train()
     B = args.batch
     g = torch.Generator().manual_seed(11 + rank)
@@ -327,18 +339,21 @@ def run_train(args, world, rank, dev, M):
     value = B * world * args.steps / elapsed
     flops = TRAIN_GFLOP_PER_SAMPLE * 1e9 * B
     achieved = flops / (ms_step * 1e-3) / 1e12
+    peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
     return {
         "metric": "LDM train samples/sec (encode -> UNet train step -> decode), 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32",
+        "vs_baseline": None,
+        "dtype": "fp32" if args.dtype == "fp32" else f"{args.dtype} (conv / weight-gradient operands inside the autocast "
+                                                     f"region; fp32 accumulation, BN, attention, optimizer)",
         "data": "synthetic (U[0,1) content/style mels; random-init weights; t ~ randint on device)",
-        "config": {"workload": f"configs 3/4: LDMTrainer.train_step, batch {B}/GPU, 1x128x512 mels, fp32 kernels "
-                               f"inside the reference's autocast region, Adam + GradScaler"
+        "config": {"workload": f"configs 3/4: LDMTrainer.train_step, batch {B}/GPU, 1x128x512 mels, "
+                               f"torch.autocast({args.dtype}) region of train.py:174, Adam + GradScaler"
                                + (f", RCCL bucketed grad all-reduce over {world} ranks" if world > 1 else ""),
                    "global_batch": B * world, "parallelism": f"dp{world}"},
         "roofline": {"kernel": "whole train step (composite)", "bound": "mfma", "achieved": round(achieved, 2),
-                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      "traffic": None, "flops_per_step": flops},
         "last_losses": {k: round(v, 6) for k, v in losses.items()},
     }
@@ -395,6 +410,7 @@ def main():
     with torch.no_grad():
         emb = ldm.style_encoder(style)
         eng = M.engine_for(ldm.unet)
+        eng.dtype = args.dtype
         gd = GraphedDDIM(eng, z_T, emb["s5"], emb["s6"], t_table, coefs, args.eta, logs=True, split=args.split)
         for _ in range(args.warmup):
             gd.replay()
@@ -424,14 +440,17 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (U[0,1) style mel, N(0,1) z_T; random-init weights)",
+        "vs_baseline": None,
+        "dtype": "fp32" if args.dtype == "fp32" else f"{args.dtype} (conv operands; fp32 accumulation, epilogue, "
+                                                     f"attention and sampler state)",
+        "data": "synthetic (U[0,1) style mel, N(0,1) z_T; random-init weights)",
         "config": {"workload": (f"config 2: {args.timesteps}-step DDIM reverse sample ({n_iter} UNet+update "
                                 f"iterations per step), batch {B}/GPU, 1x128x512 mel -> [{B},32,16,64] latents, "
                                 f"eta={args.eta}, hipGraph replay of {args.split} concurrent sub-batch chains")
                    if args.workload == "sample" else
                    (f"config 5: content/style transfer loop, T'={args.timesteps} ({n_iter} UNet+update iterations "
                     f"per step, content encoded and q_sampled at T'-1 before timing), batch {B}/GPU, "
-                    f"eta={args.eta}, fp32 compute and accumulators (>= the config's fp16), hipGraph replay"),
+                    f"eta={args.eta}, {args.dtype} step-kernel operands with fp32 accumulators, hipGraph replay"),
                    "global_batch": B * world,
                    "latent": [B, 32, 16, 64], "parallelism": f"dp{world} (independent batch shards)"},
         "us_per_denoise_iteration": round(us_iter, 2),
@@ -439,7 +458,8 @@ def main():
     # whole-step composite roofline
     flops_iter = UNET_GFLOP_PER_SAMPLE * 1e9 * B
     bytes_iter = 27.37e6 + B * (2.52e6 + 0.655e6)
-    t_roof = max(flops_iter / (FP32_PEAK_TFLOPS * 1e12), bytes_iter / (HBM_PEAK_GBS * 1e9))
+    peak_c = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
+    t_roof = max(flops_iter / (peak_c * 1e12), bytes_iter / (HBM_PEAK_GBS * 1e9))
     result["step_roofline"] = {"t_roof_us": round(t_roof * 1e6, 2), "t_measured_us": round(us_iter, 2),
                                "frac": round(t_roof * 1e6 / us_iter, 4),
                                "achieved_tflops": round(flops_iter / (us_iter * 1e-6) / 1e12, 2)}
@@ -457,9 +477,12 @@ def main():
                 traffic = pmc.get("per_launch_bytes", {}).get(dom)
             except (OSError, ValueError):
                 traffic = None
+        peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
+        if args.dtype != "fp32":
+            traffic = None     # profiles/r02/pmc_traffic_step.json holds the fp32 kernels' counters
         result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
-                              "achieved": dk["tflops"], "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": round(dk["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                              "achieved": dk["tflops"], "peak": peak, "unit": "TFLOP/s",
+                              "frac": round(dk["tflops"] / peak, 4), "traffic": traffic,
                               "flops_per_launch": dk["flops"], "avg_launch_us": dk["us"]}
         result["kernels"] = {k: {kk: vv for kk, vv in v.items() if kk not in ("flops", "bytes")} for k, v in kt.items()}
 

@@ -53,6 +53,11 @@ enum {
     LDM_ACT_GELU = 4       /* exact erf GELU (nn.GELU(), model.py:173)                     */
 };
 
+/* Operand precision of the MFMA kernels: fp32 operands (exact), or rounded to fp16 / bf16 in registers
+ * with fp32 accumulation, fp32 epilogue and fp32 outputs / sampler state (the torch.autocast fp16 / bf16
+ * regions of the train step and of a sampling loop; BASELINE configs 3 and 5). */
+enum { LDM_DT_F32 = 0, LDM_DT_F16 = 1, LDM_DT_BF16 = 2 };
+
 typedef struct ldm_epilogue {
     const float* bias;      /* [Cout] or NULL                                                */
     const float* bn_weight; /* eval-mode BatchNorm2d after bias (NULL = none): gamma [Cout]    */
@@ -65,6 +70,8 @@ typedef struct ldm_epilogue {
     const float* skip_add;  /* [B,Cout,Hout,Wout] added after act (UNet skips, model.py:221) */
     float* act_out;         /* [B,Cout,Hout,Wout] or NULL: also store act(.) before the adds  */
                             /* (training: the activation's backward needs it)                */
+    int32_t dtype;          /* operand precision LDM_DT_* of the MFMA kernels (kinds 1 / 2): fp32, or */
+                            /* x and w rounded to fp16 / bf16 with fp32 accumulation (autocast)     */
 } ldm_epilogue;
 
 typedef struct ldm_conv_plan {
@@ -229,6 +236,7 @@ typedef struct ldm_unet_weights {
     const float* step_w[9];
     const float* step_pb[2];
     int32_t use_step;
+    int32_t step_dtype;   /* LDM_DT_*: operand precision of the step kernels (not F32: uconv.hip only) */
 } ldm_unet_weights;
 
 typedef struct ldm_unet_shape {
@@ -273,6 +281,9 @@ int64_t ldm_step_packed_floats(int32_t layer);
 int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream);
 int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                   const float* bias, const float* bcast, const float* skip, float* y, void* stream);
+/* ldm_step_conv with an operand precision LDM_DT_* (ldm_step_conv = LDM_DT_F32). */
+int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                     const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype, void* stream);
 /* The LDS-staged variant (ustep.hip) of the same layers at the canonical latent H = 16, W = 64 with B a
  * multiple of 4 (else -1).  The deep layers split K across blocks: they need a zero-filled workspace of
  * ldm_ustep_workspace_floats(layer, B) floats (0: none), which they leave zero-filled; layers running one
@@ -288,6 +299,10 @@ int ldm_ustep_conv(int32_t layer, int32_t B, const float* x, const float* packed
  * dy = gradient at the layer's pre-epilogue output.  dw in the torch weight layout; accumulate != 0 adds.
  * workspace: ldm_conv_wgrad_workspace_floats(d) floats. */
 int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d);
+/* ldm_conv_backward_weight with an operand precision LDM_DT_* (the tap-shared kernel rounds x and dy;
+ * shapes it does not cover run the fp32 kernel). */
+int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                int32_t accumulate, float* workspace, int32_t dtype, void* stream);
 int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
                              float* workspace, void* stream);
 /* Backward of the fused epilogue act(v) (+bcast[b,c]) (+skip): dv = dy*act'(v) (from act_out = act(v);

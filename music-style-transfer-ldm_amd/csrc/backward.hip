@@ -316,7 +316,13 @@ extern "C" int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d) {
 
 extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                         int32_t accumulate, float* workspace, void* stream) {
+    return ldm_conv_backward_weight_dt(d, x, dy, dw, accumulate, workspace, LDM_DT_F32, stream);
+}
+
+extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                           int32_t accumulate, float* workspace, int32_t dtype, void* stream) {
     LDM_REQUIRE(d && x && dy && dw && workspace, "wgrad: null argument");
+    LDM_REQUIRE(dtype >= LDM_DT_F32 && dtype <= LDM_DT_BF16, "wgrad: unknown operand precision");
     WgradArgs a;
     int kk;
     int rc = wgrad_setup(*d, a, kk);
@@ -326,7 +332,7 @@ extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, 
     hipStream_t st = (hipStream_t)stream;
     const int MN = a.M * a.N;
     int S2 = 0;
-    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, st);   // the tap-shared form (wgrad.hip) where it applies
+    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st);   // the tap-shared form (wgrad.hip) where it applies
     if (rc > 0) return rc;
     if (rc == 0) {
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)workspace, S2,

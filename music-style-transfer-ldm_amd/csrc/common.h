@@ -34,6 +34,36 @@ int fail(int code, const std::string& msg);
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+
+// Operand precision of the reduced-precision step kernels (ldm_capi.h LDM_DT_*): fp32 operands rounded to
+// nearest-even fp16 / bf16 in registers, one v_mfma_f32_16x16x16_{f16,bf16} per 16-deep K chunk (the
+// 4 consecutive elements a lane holds are exactly that MFMA's per-lane operand), fp32 accumulation.
+template <int DT>
+__device__ __forceinline__ floatx16 mma32_lowp(floatx4 a, floatx4 b, floatx16 c) {
+    if constexpr (DT == 1) {
+        return __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_convertvector(a, halfx4), __builtin_convertvector(b, halfx4),
+                                                    c, 0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, __builtin_convertvector(a, bf16x4)),
+                                                        __builtin_bit_cast(shortx4, __builtin_convertvector(b, bf16x4)),
+                                                        c, 0, 0, 0);
+    }
+}
+
+template <int DT>
+__device__ __forceinline__ floatx4 mma16_lowp(floatx4 a, floatx4 b, floatx4 c) {
+    if constexpr (DT == 1) {
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_convertvector(a, halfx4), __builtin_convertvector(b, halfx4),
+                                                     c, 0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(shortx4, __builtin_convertvector(a, bf16x4)),
+                                                         __builtin_bit_cast(shortx4, __builtin_convertvector(b, bf16x4)),
+                                                         c, 0, 0, 0);
+    }
+}
 
 // Division of a non-negative int < 2^31 by a runtime constant with one mul_hi + shift (Granlund-
 // Montgomery, round-up multiplier): the GPU's integer division is a ~30-instruction VALU sequence.
@@ -111,6 +141,7 @@ struct EpiArgs {
     float* ddim_x;
     float* ddim_x0_log;
     float* ddim_eps_log;
+    int32_t lowp;   // operand precision LDM_DT_* (MFMA kernels)
 };
 
 // conv.hip: implicit-GEMM conv with the full internal epilogue (incl. the fused DDIM update); y may be
@@ -141,6 +172,7 @@ struct StepConv {
     float* xs;            // dec1: sampler state (NHWC), updated in place
     float* x0_log;        // dec1: NCHW logs (or NULL)
     float* eps_log;
+    int dtype;            // operand precision: LDM_DT_F32 / LDM_DT_F16 / LDM_DT_BF16 (uconv.hip)
 };
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
@@ -151,7 +183,7 @@ int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 
 // wgrad.hip: the tap-shared weight-gradient kernel (ldm_conv_backward_weight where it applies)
 bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats);
-int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits,
+int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
                hipStream_t st);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile

@@ -304,6 +304,9 @@ struct Mfma<1> {
         return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
     }
     static __device__ __forceinline__ int row(int r, int lg) { return (r & 3) + 8 * (r >> 2) + 4 * lg; }
+    // the 4 consecutive k of a lane's fragment as one reduced-precision MFMA (32x32x8)
+    template <int DT>
+    static __device__ __forceinline__ acc_t mma4(floatx4 a, floatx4 b, acc_t c) { return mma32_lowp<DT>(a, b, c); }
 };
 
 template <>
@@ -314,6 +317,8 @@ struct Mfma<2> {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
     }
     static __device__ __forceinline__ int row(int r, int lg) { return 4 * lg + r; }
+    template <int DT>
+    static __device__ __forceinline__ acc_t mma4(floatx4 a, floatx4 b, acc_t c) { return mma16_lowp<DT>(a, b, c); }
 };
 
 constexpr int kMaxKSplit = 16;   // blocks splitting K (ldm_conv_plan.ks)
@@ -360,7 +365,8 @@ __device__ __forceinline__ float part_load(const float* p) {
 
 // NT = tap slots scanned per phase (1 for 1x1 projections, 4 for transposed-conv phases, 9 for 3x3,
 // 16 for 4x4): the per-lane tap offsets are precomputed for NT slots only.
-template <int KIND, int TM, int TN, int WK, int NT, bool NHWC>
+// DT: operand precision (0 fp32; 2 bf16 operands with fp32 accumulation, NCHW instances only).
+template <int KIND, int TM, int TN, int WK, int NT, bool NHWC, int DT>
 __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
     LDM_STAMP(0);
     using MF = Mfma<KIND>;
@@ -653,6 +659,17 @@ __global__ __launch_bounds__(64 * WK) void conv_mfma_kernel(ConvArgs a) {
             if (!decltype(all_live)::value && grp * kGroup + q >= nmine) break;   // wave-uniform: no MFMAs on padding
             if constexpr (LDM_DIAG & 16) {          // diagnostic: no MFMAs either (fixed cost only)
                 acc[0][0][0] = acc[0][0][0] + f[q].a[0][0] * f[q].b[0][0];
+                continue;
+            }
+            if constexpr (DT != 0) {   // fp16 / bf16 operands: a lane's 4 consecutive k in one MFMA
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const floatx4 bv = {f[q].b[ni][0], f[q].b[ni][1], f[q].b[ni][2], f[q].b[ni][3]};
+                        if (NCH == 2 && (q & 1)) acc2[mi][ni] = MF::template mma4<DT>(f[q].a[mi], bv, acc2[mi][ni]);
+                        else acc[mi][ni] = MF::template mma4<DT>(f[q].a[mi], bv, acc[mi][ni]);
+                    }
                 continue;
             }
 #pragma unroll
@@ -1145,7 +1162,7 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     return 0;
 }
 
-template <int KIND, int NT, bool NHWC>
+template <int KIND, int NT, bool NHWC, int DT>
 static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     const int TILE = Mfma<KIND>::TILE;
     const int BMx = TILE * p.tm, BNx = TILE * p.tn;
@@ -1157,7 +1174,7 @@ static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq,
     const int code = (p.tm - 1) * 2 + (p.tn - 1);
 #define LDM_CASE(WK, C, TM, TN)                                                                              \
     case WK * 10 + C: {                                                                                      \
-        auto kfn = conv_mfma_kernel<KIND, TM, TN, WK, NT, NHWC>;                                            \
+        auto kfn = conv_mfma_kernel<KIND, TM, TN, WK, NT, NHWC, DT>;                                        \
         if (lds > 64 * 1024) {                                                                               \
             static size_t opted = 0;                                                                         \
             if (opted < lds) {                                                                               \
@@ -1181,19 +1198,19 @@ static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq,
     return 0;
 }
 
-template <int KIND, bool NHWC>
+template <int KIND, bool NHWC, int DT>
 static int launch_mfma(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     int maxtap = 0;
     for (int i = 0; i < a.pt.nphase; ++i) maxtap = std::max(maxtap, a.pt.ntap[i]);
     // NT = 4 <=> the 4-phase kernels (kMaxTap per phase of a stride-2 transposed conv with k <= 4 is 4)
     if (a.pt.nphase == 4) {
         if (maxtap > 4) return fail(3, "conv: 4-phase layer with more than 4 taps per phase");
-        return launch_mfma_nt<KIND, 4, NHWC>(a, p, Nq, st);
+        return launch_mfma_nt<KIND, 4, NHWC, DT>(a, p, Nq, st);
     }
     if (a.pt.nphase != 1) return fail(3, "conv: unsupported phase count");
-    if (maxtap <= 1) return launch_mfma_nt<KIND, 1, NHWC>(a, p, Nq, st);
-    if (maxtap <= 9) return launch_mfma_nt<KIND, 9, NHWC>(a, p, Nq, st);
-    return launch_mfma_nt<KIND, 16, NHWC>(a, p, Nq, st);
+    if (maxtap <= 1) return launch_mfma_nt<KIND, 1, NHWC, DT>(a, p, Nq, st);
+    if (maxtap <= 9) return launch_mfma_nt<KIND, 9, NHWC, DT>(a, p, Nq, st);
+    return launch_mfma_nt<KIND, 16, NHWC, DT>(a, p, Nq, st);
 }
 
 namespace ldm {
@@ -1242,8 +1259,12 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
                     p.packed_floats * 4 < 0x7ff00000LL && (int64_t)d.B * d.Cout * d.Hout * d.Wout * 4 < 0x7ff00000LL,
                 "conv forward: tensor too large for 32-bit buffer offsets (split the batch)");
     const bool in_nhwc = d.layout & 1;
-    if (p.kind == 1) return in_nhwc ? launch_mfma<1, true>(a, p, Nq, st) : launch_mfma<1, false>(a, p, Nq, st);
-    return in_nhwc ? launch_mfma<2, true>(a, p, Nq, st) : launch_mfma<2, false>(a, p, Nq, st);
+    // reduced-precision operands (autocast): bf16 instances for NCHW tensors (the train step's convs);
+    // fp16 autocast runs the fp32 kernels (exact operands, wider than asked)
+    if (a.ep.lowp == LDM_DT_BF16 && !in_nhwc)
+        return p.kind == 1 ? launch_mfma<1, false, 2>(a, p, Nq, st) : launch_mfma<2, false, 2>(a, p, Nq, st);
+    if (p.kind == 1) return in_nhwc ? launch_mfma<1, true, 0>(a, p, Nq, st) : launch_mfma<1, false, 0>(a, p, Nq, st);
+    return in_nhwc ? launch_mfma<2, true, 0>(a, p, Nq, st) : launch_mfma<2, false, 0>(a, p, Nq, st);
 }
 
 }  // namespace ldm
@@ -1263,6 +1284,8 @@ extern "C" int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* 
         e.bcast = ep->bcast_add;
         e.skip = ep->skip_add;
         e.act_out = ep->act_out;
+        e.lowp = ep->dtype;
+        LDM_REQUIRE(e.lowp >= LDM_DT_F32 && e.lowp <= LDM_DT_BF16, "conv forward: unknown operand precision");
     }
     return conv_forward_ex(*d, *plan, x, w, e, y, workspace, (hipStream_t)stream);
 }

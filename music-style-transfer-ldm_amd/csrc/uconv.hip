@@ -87,7 +87,7 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT>
 __global__ __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu((WN * WK + 3) / 4, (WN * WK + 3) / 4)))
 void uconv_kernel(UArgs a) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
@@ -195,6 +195,15 @@ void uconv_kernel(UArgs a) {
             constexpr int i = decltype(ic)::value;
             constexpr int c = st * S + i;
             constexpr int p = MODE == 2 ? tphase(c % CPC) : 0;
+            if constexpr (DT != 0) {   // fp16 / bf16 operands: the whole 16-channel chunk in one MFMA
+                constexpr int u = NACC2 == 2 ? (c & 1) : 0;
+#pragma unroll
+                for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni)
+                        acc[u][p][mi][ni] = mma16_lowp<DT>(fa[bf][i][mi], fb[bf][i][ni], acc[u][p][mi][ni]);
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -391,15 +400,26 @@ struct LayerGeo {
     int mode, cin, cout, tm, tn, wn, wk;
 };
 
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
-static int launch(const UArgs& a, hipStream_t st) {
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT>
+static int launch_dt(const UArgs& a, hipStream_t st) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
     const int blocks = a.nMt * a.nNt;
     const size_t lds = WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0;
-    auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI>;
+    auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * WN * WK), lds, st, a);
     LDM_CHECK_LAUNCH("uconv_kernel");
     return 0;
+}
+
+// operand precision (StepConv::dtype) -> instance
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
+static int launch(const UArgs& a, int dtype, hipStream_t st) {
+    switch (dtype) {
+        case LDM_DT_F32: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 0>(a, st);
+        case LDM_DT_F16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 1>(a, st);
+        case LDM_DT_BF16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 2>(a, st);
+        default: return fail(2, "step conv: unknown operand precision");
+    }
 }
 
 constexpr LayerGeo kGeo[9] = {
@@ -468,20 +488,20 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 "step conv: tensor too large for 32-bit buffer offsets");
     LDM_REQUIRE(s.x && s.w && s.bias, "step conv: null operand");
     switch (layer) {
-        case 0: LDM_REQUIRE(s.y, "enc1: y"); return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, st);
+        case 0: LDM_REQUIRE(s.y, "enc1: y"); return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 1: LDM_REQUIRE(s.y && s.bcast, "enc2: y, t_emb");
-            return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, st);
-        case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, st);
-        case 3: LDM_REQUIRE(s.y, "enc4: y"); return launch<1, 256, 512, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_POSB>(a, st);
-        case 4: LDM_REQUIRE(s.y, "bottleneck: y"); return launch<0, 512, 512, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_POSB>(a, st);
+            return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, s.dtype, st);
+        case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, s.dtype, st);
+        case 3: LDM_REQUIRE(s.y, "enc4: y"); return launch<1, 256, 512, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_POSB>(a, s.dtype, st);
+        case 4: LDM_REQUIRE(s.y, "bottleneck: y"); return launch<0, 512, 512, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_POSB>(a, s.dtype, st);
         case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
-            return launch<2, 512, 256, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_SKIP>(a, st);
+            return launch<2, 512, 256, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         case 6: LDM_REQUIRE(s.y && s.skip, "dec3: y, skip");
-            return launch<2, 256, 128, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_SKIP>(a, st);
+            return launch<2, 256, 128, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         case 7: LDM_REQUIRE(s.y && s.skip, "dec2: y, skip");
-            return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP>(a, st);
+            return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         default: LDM_REQUIRE(s.xs && s.coef, "dec1: sampler state, coefficients");
-            return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, st);
+            return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, s.dtype, st);
     }
 }
 
@@ -521,7 +541,14 @@ extern "C" int ldm_step_pack_weight(int32_t layer, const float* w, float* packed
 
 extern "C" int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                              const float* bias, const float* bcast, const float* skip, float* y, void* stream) {
+    return ldm_step_conv_dt(layer, B, H, W, x, packed, bias, bcast, skip, y, LDM_DT_F32, stream);
+}
+
+extern "C" int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                                const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
+                                void* stream) {
     StepConv s{};
+    s.dtype = dtype;
     s.x = x;
     s.w = packed;
     s.bias = bias;

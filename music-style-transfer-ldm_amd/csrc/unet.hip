@@ -115,7 +115,8 @@ static int64_t conv_ws_floats(const ldm_unet_weights* w) {
 
 // The LDS-staged step kernels (ustep.hip) run when use_step == 2 at their canonical shape.
 static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
-    return w && w->use_fold && w->use_step == 2 && s.C == 32 && s.nf == 64 && ustep_supported(s.B, s.H, s.W);
+    return w && w->use_fold && w->use_step == 2 && w->step_dtype == LDM_DT_F32 && s.C == 32 && s.nf == 64 &&
+           ustep_supported(s.B, s.H, s.W);
 }
 
 // Layers that run on ustep.hip under use_step 2: measured in the reverse loop (rocprofv3, B=8), the
@@ -301,6 +302,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
         c.bias = bias;
         c.bcast = bcast;
         c.skip = skip;
+        c.dtype = w.step_dtype;
         return v3 && ustep_layer(layer) ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
     };
     LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
@@ -322,6 +324,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     c.xs = ws.xs;
     c.x0_log = fuse.x0_log;
     c.eps_log = fuse.eps_log;
+    c.dtype = w.step_dtype;
     return v3 && ustep_layer(8) ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
 }
 
@@ -392,6 +395,7 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
             LDM_REQUIRE(s->C == 32 && s->nf == 64, "ddim_sample: the step kernels are built for latent 32 / 64 filters");
             for (int l = 0; l < 9; ++l) LDM_REQUIRE(w->step_w[l], "ddim_sample: use_step needs the step weights");
             LDM_REQUIRE(w->step_pb[0] && w->step_pb[1], "ddim_sample: use_step needs the folded biases");
+            LDM_REQUIRE(w->step_dtype >= LDM_DT_F32 && w->step_dtype <= LDM_DT_BF16, "ddim_sample: step_dtype");
             LDM_TRY(step_layout(x, ws.xs, s->B, s->C, HW, true, st));
             for (int i = 0; i < nsteps; ++i) {
                 DdimFuse fuse{coef_table + 4 * (size_t)i, eta, ws.xs, x0_logs ? x0_logs + (size_t)i * n : nullptr,

@@ -37,6 +37,7 @@ struct Args {
     int32_t nchunk, per_split;
     int32_t wr, wca, e;   // window rows, row pitch (floats, multiple of 4), column shift of the aligned origin
     int32_t pitch_c;      // floats per channel in the window (wr * wca)
+    int32_t lowp;         // LDM_DT_*: operands rounded to fp16 / bf16, fp32 accumulation
 };
 
 template <int B_, int E_, class F>
@@ -64,7 +65,7 @@ __host__ __device__ inline int buf_floats(int a_floats, int bc, int pitch_c) {
     return a_floats + (bc * pitch_c + 255) / 256 * 256;
 }
 
-template <int S, int KK, int BM, int BC>
+template <int S, int KK, int BM, int BC, int DT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad_kernel(Args a) {
     using g = Cfg<S, KK, BM, BC>;
     constexpr int T = g::T, WCF = g::WCF, FM = g::FM, AF = g::A_FLOATS;
@@ -161,24 +162,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __syncthreads();   // chunk ch landed everywhere; every wave is done with the other buffer
         if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
         const float* sb = smem + buf * bufF;
+        {   // DT = operand precision (compile time: a runtime branch between MFMA forms miscompiled in conv.hip)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            floatx4 fa[FM];
+            for (int u = 0; u < 4; ++u) {
+                floatx4 fa[FM];
 #pragma unroll
-            for (int f = 0; f < FM; ++f) fa[f] = *reinterpret_cast<const floatx4*>(sb + aoff[f][u]);
-            static_for<0, T>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                constexpr int ky = t / KK, kx = t % KK;
-                const float* bp = sb + boff[u] + ky * a.wca + kx;
-                float bv[4];
+                for (int f = 0; f < FM; ++f) fa[f] = *reinterpret_cast<const floatx4*>(sb + aoff[f][u]);
+                static_for<0, T>([&](auto tc) {
+                    constexpr int t = decltype(tc)::value;
+                    constexpr int ky = t / KK, kx = t % KK;
+                    const float* bp = sb + boff[u] + ky * a.wca + kx;
+                    floatx4 bv;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bv[j] = bp[j * S];
+                    for (int j = 0; j < 4; ++j) bv[j] = bp[j * S];
+                    if constexpr (DT == 0) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                        for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int f = 0; f < FM; ++f)
-                        acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[f][j], bv[j], acc[t][f], 0, 0, 0);
-            });
+                            for (int f = 0; f < FM; ++f)
+                                acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[f][j], bv[j], acc[t][f], 0, 0, 0);
+                    } else {
+#pragma unroll
+                        for (int f = 0; f < FM; ++f) acc[t][f] = mma16_lowp<DT>(fa[f], bv, acc[t][f]);
+                    }
+                });
+            }
         }
     }
 
@@ -246,9 +254,9 @@ bool plan(const ldm_conv_desc& d, Plan& p) {
     return true;
 }
 
-template <int S, int KK, int BM, int BC>
-int launch(const Plan& p, hipStream_t st) {
-    auto kfn = wgrad_kernel<S, KK, BM, BC>;
+template <int S, int KK, int BM, int BC, int DT>
+int launch_dt(const Plan& p, hipStream_t st) {
+    auto kfn = wgrad_kernel<S, KK, BM, BC, DT>;
     static bool opted = false;
     if (!opted) {
         LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -258,6 +266,15 @@ int launch(const Plan& p, hipStream_t st) {
     hipLaunchKernelGGL(kfn, grid, dim3(256), p.lds_bytes, st, p.a);
     LDM_CHECK_LAUNCH("wgrad_kernel (tap-shared)");
     return 0;
+}
+
+template <int S, int KK, int BM, int BC>
+int launch(const Plan& p, hipStream_t st) {
+    switch (p.a.lowp) {
+        case LDM_DT_F32: return launch_dt<S, KK, BM, BC, 0>(p, st);
+        case LDM_DT_F16: return launch_dt<S, KK, BM, BC, 1>(p, st);
+        default: return launch_dt<S, KK, BM, BC, 2>(p, st);
+    }
 }
 
 }  // namespace wg
@@ -271,10 +288,11 @@ bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats) {
 
 // Runs the tap-shared kernel into `partial` ([splits][M][N]); returns the split count through `splits`,
 // or -1 when the form does not apply.
-int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits,
+int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
                hipStream_t st) {
     wg::Plan p;
     if (!wg::plan(d, p)) return -1;
+    p.a.lowp = dtype;
     p.a.dense = dense;
     p.a.gath = gath;
     p.a.partial = partial;

@@ -33,7 +33,8 @@ class ConvDesc(ctypes.Structure):
 
 class Epilogue(ctypes.Structure):
     _fields_ = [("bias", c_fp), ("bn_weight", c_fp), ("bn_bias", c_fp), ("bn_mean", c_fp), ("bn_var", c_fp),
-                ("bn_eps", c_float), ("act", c_int32), ("bcast_add", c_fp), ("skip_add", c_fp), ("act_out", c_fp)]
+                ("bn_eps", c_float), ("act", c_int32), ("bcast_add", c_fp), ("skip_add", c_fp), ("act_out", c_fp),
+                ("dtype", c_int32)]
 
 
 class ConvPlan(ctypes.Structure):
@@ -55,7 +56,8 @@ class UNetWeights(ctypes.Structure):
                 ("ca_wo", c_fp * 2), ("ca_bo", c_fp * 2), ("ca_plan_o", ConvPlan * 2),
                 ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp),
                 ("ca_wq_raw", c_fp * 2), ("fold_w", c_fp * 2), ("fold_pb", c_fp * 2), ("use_fold", c_int32),
-                ("step_w", c_fp * 9), ("step_pb", c_fp * 2), ("use_step", c_int32)]
+                ("step_w", c_fp * 9), ("step_pb", c_fp * 2), ("use_step", c_int32),
+                ("step_dtype", c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
@@ -77,6 +79,8 @@ SIGNATURES = {
     "ldm_step_packed_floats": (c_int64, [c_int32]),
     "ldm_step_pack_weight": (c_int32, [c_int32, c_fp, c_fp, c_vp]),
     "ldm_step_conv": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_step_conv_dt": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
+                                   c_vp]),
     "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
     "ldm_ustep_conv": (c_int32, [c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
@@ -111,6 +115,7 @@ SIGNATURES = {
                                   c_fp, c_int32, c_float, c_fp, c_fp, c_int64, c_fp, c_vp]),
     # backward / optimiser
     "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
+    "ldm_conv_backward_weight_dt": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_int32, c_vp]),
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),

@@ -20,8 +20,12 @@ _CONV_NAMES = ("enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "de
 class UNetEngine:
     """Runs `unet` (a models.model.UNet: reference parameter names / shapes) through libldm_amd."""
 
-    def __init__(self, unet, fold=None, step=None):
+    def __init__(self, unet, fold=None, step=None, dtype=None):
         self.unet = unet
+        # Operand precision of the step kernels (ldm_capi.h LDM_DT_*): None follows the caller's
+        # torch.autocast("cuda") region (fp16 / bf16 operands, fp32 accumulation and sampler state) or
+        # LDM_AMD_STEP_DTYPE; "fp32" / "fp16" / "bf16" pins it.
+        self.dtype = dtype
         # Re-associated cross-attentions in the reverse loop (ldm_capi.h use_fold); LDM_AMD_FOLD=0 turns
         # it off (A/B timing, parity of the literal form).
         self.fold = (os.environ.get("LDM_AMD_FOLD", "1") != "0") if fold is None else bool(fold)
@@ -36,6 +40,20 @@ class UNetEngine:
         self._bound = {}      # shape key -> (key of param versions, UNetWeights, keepalive)
         self._ws = {}         # (shape key, device) -> workspace tensor
         self._graphs = {}
+
+    _DT = {"fp32": 0, "f32": 0, "float32": 0, "fp16": 1, "f16": 1, "float16": 1, "bf16": 2, "bfloat16": 2}
+
+    def step_dtype(self):
+        """LDM_DT_* the reverse loop's step kernels run at (see __init__)."""
+        if self.dtype is not None:
+            return self._DT[str(self.dtype).replace("torch.", "")]
+        env = os.environ.get("LDM_AMD_STEP_DTYPE")
+        if env:
+            return self._DT[env]
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            return 1 if dt == torch.float16 else (2 if dt == torch.bfloat16 else 0)
+        return 0
 
     # -------------------------------------------------------------------------------------------
     def shape(self, B, C, H, W):
@@ -63,7 +81,7 @@ class UNetEngine:
             if not p.is_contiguous():
                 raise RuntimeError("UNet parameters must be contiguous")
         vkey = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params) + \
-            tuple(sorted(ops._PLAN_OVERRIDE.items())) + (self.fold, self.step)
+            tuple(sorted(ops._PLAN_OVERRIDE.items())) + (self.fold, self.step, self.step_dtype() if self.step else 0)
         hit = self._bound.get(skey)
         if hit is not None and hit[0] == vkey:
             return hit[1]
@@ -144,6 +162,7 @@ class UNetEngine:
                     keep.append(pbt)
                     w.step_pb[j] = pbt.data_ptr()
                 w.use_step = self.step
+                w.step_dtype = self.step_dtype()
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)

@@ -77,7 +77,9 @@ def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0
         if store["grad"] and act != "none" and (bc_ is not None or sk_ is not None):
             d = _conv_desc(x_, w_, cfg)
             aout = torch.empty((d.B, d.Cout, d.Hout, d.Wout), device=x_.device, dtype=torch.float32)
-        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, **cfg)
+        dt = ops.autocast_dt()
+        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, dtype=dt, **cfg)
+        store["dtype"] = dt      # the backward convs run at the forward's autocast precision
         store["cfg"] = cfg
         store["bn"] = bn_eval
         store["wkey"] = wkey
@@ -109,8 +111,9 @@ def _conv_backward(ctx, gy):
         if nb:
             _, gb, _ = ops.act_backward(gv, "none", need_dv=False, need_bias=True)
     desc = _conv_desc(x, w, cfg)
-    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"]) if nx else None
-    gw = ops.conv_backward_weight(x, gv, desc) if nw else None
+    dt = ctx.store.get("dtype", 0)
+    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt) if nx else None
+    gw = ops.conv_backward_weight(x, gv, desc, dtype=dt) if nw else None
     if gbc is not None:
         gbc = gbc.reshape(ctx.store["bc_shape"])
     return gx, gw, gb, gbc, (gy if nsk else None)

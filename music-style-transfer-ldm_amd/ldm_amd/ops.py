@@ -8,6 +8,8 @@ import ctypes
 import math
 import weakref
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -137,7 +139,7 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
 # convolution with fused epilogue
 # ------------------------------------------------------------------------------------------------
 def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False, output_padding=0, bn=None,
-                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None, act_out=None):
+                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None, act_out=None, dtype=None):
     """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps).
     act_out (preallocated, output-shaped) also receives act(.) before the adds."""
     require_device(x, weight, bias, bcast, skip)
@@ -160,6 +162,7 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
     ep = L.Epilogue()
     ep.bias = _p(bias)
+    ep.dtype = autocast_dt() if dtype is None else int(dtype)
     keep = []
     if bn is not None:
         g, b_, m, v, eps = bn
@@ -184,6 +187,17 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     return y
 
 
+def autocast_dt(device_type="cuda"):
+    """LDM_DT_* for the MFMA kernels from the caller's torch.autocast region: fp16 / bf16 operands (fp32
+    accumulation, epilogue and outputs) inside one, fp32 outside.  LDM_AMD_DTYPE=fp32 turns it off."""
+    if os.environ.get("LDM_AMD_DTYPE", "") in ("fp32", "f32"):
+        return 0
+    if not torch.is_autocast_enabled(device_type):
+        return 0
+    dt = torch.get_autocast_dtype(device_type)
+    return 1 if dt == torch.float16 else (2 if dt == torch.bfloat16 else 0)
+
+
 def dual_desc(desc):
     """Descriptor whose forward is the data gradient of `desc`: conv <-> transposed conv with the same
     kernel, stride and padding (the torch weight tensor is reused unchanged in both directions)."""
@@ -197,13 +211,16 @@ def dual_desc(desc):
     return d
 
 
-def conv_backward_data(dy, weight, desc, wkey=None):
-    """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc)."""
+def conv_backward_data(dy, weight, desc, wkey=None, dtype=0):
+    """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc);
+    dtype = LDM_DT_* operand precision (the forward's autocast precision)."""
     dd = dual_desc(desc)
     plan = get_plan(dd)
     wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
     dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
-    L.call("ldm_conv_forward_ws", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), None, dx.data_ptr(),
+    ep = L.Epilogue()
+    ep.dtype = int(dtype)
+    L.call("ldm_conv_forward_ws", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), byref(ep), dx.data_ptr(),
            split_workspace(plan, dy.device), stream_handle())
     return dx
 
@@ -238,8 +255,9 @@ def split_workspace(plan, device):
     return buf.data_ptr()
 
 
-def conv_backward_weight(x, dy, desc, dw=None, accumulate=False):
-    """dW (torch layout) of conv/convT `desc` from its input x and pre-epilogue gradient dy."""
+def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
+    """dW (torch layout) of conv/convT `desc` from its input x and pre-epilogue gradient dy; dtype =
+    LDM_DT_* operand precision."""
     x = f32c(x)
     dy = f32c(dy)
     if desc.transposed:
@@ -249,8 +267,8 @@ def conv_backward_weight(x, dy, desc, dw=None, accumulate=False):
     if dw is None:
         dw = torch.empty(shape, device=x.device, dtype=torch.float32)
     ws = scratch("wgrad", L.load().ldm_conv_wgrad_workspace_floats(byref(desc)), x.device)
-    L.call("ldm_conv_backward_weight", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate),
-           ws.data_ptr(), stream_handle())
+    L.call("ldm_conv_backward_weight_dt", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate),
+           ws.data_ptr(), int(dtype), stream_handle())
     return dw
 
 

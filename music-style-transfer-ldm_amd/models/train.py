@@ -145,6 +145,9 @@ class LDMTrainer:
         trainable_params = [p for p in model.parameters() if p.requires_grad]
         self.optimizer = hoptim.Adam(trainable_params, lr=lr)
         self.scaler = hoptim.GradScaler("cuda")
+        # dtype of the train step's autocast region (train.py:174 uses the device default: fp16 on a GPU;
+        # bfloat16 = BASELINE config 3); the HIP convs then round their operands to it (ldm_capi.h LDM_DT_*)
+        self.autocast_dtype = None
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", factor=0.5,
                                                                     patience=10)
         self.reducer = None
@@ -166,7 +169,8 @@ class LDMTrainer:
         batch_size = content_spec.shape[0]
         if t is None:
             t = self._sample_t(batch_size)
-        with torch.autocast(device_type=self.device.type):
+        ac = {} if self.autocast_dtype is None else {"dtype": self.autocast_dtype}
+        with torch.autocast(device_type=self.device.type, **ac):
             outputs = self.model(content_spec, style_spec, t, noise=noise)
             noise_pred = outputs["noise_pred"]
             noise = outputs["noise"]

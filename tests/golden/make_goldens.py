@@ -2,6 +2,7 @@
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py          # ref_goldens.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r2     # ref_goldens_r2.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp    # ref_goldens_amp.npz
 
 Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
 stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
@@ -264,6 +265,81 @@ def round2():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
 
 
+def amp():
+    """Reduced-precision fixtures -> tests/golden/ref_goldens_amp.npz: the reference reverse loops run under
+    torch.autocast("cpu", dtype) (convs / linears / attention matmuls in fp16 or bf16, the scheduler
+    arithmetic on the fp32 latent), at the canonical latent [1,32,16,64] (the reference loop logs t.item(),
+    so it runs batch 1): a 10-step DDIM (eta 0, config 2's loop) in fp32 / bf16 / fp16, and the T'=100
+    content-style loop (eta 1, config 5's "fp16 with fp32 scheduler accumulators") in fp32 / fp16.
+    Style embedding computed in fp32 outside the autocast region."""
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+    with torch.no_grad():
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.eval()
+        style = torch.from_numpy(recipe.uniform01((1, 1, 128, 512), 741))
+        zT = torch.from_numpy(recipe.normal((1, 32, 16, 64), 742))
+        emb = ldm.style_encoder(style)
+        for name, dt in (("fp32", None), ("bf16", torch.bfloat16), ("fp16", torch.float16)):
+            if dt is None:
+                x, logs = ldm.style_conditioned_ddim_sample(zT, emb, timesteps=10, eta=0.0)
+            else:
+                with torch.autocast("cpu", dtype=dt):
+                    x, logs = ldm.style_conditioned_ddim_sample(zT, emb, timesteps=10, eta=0.0)
+            G[f"amp10_{name}_x"] = np32(x.float())
+            G[f"amp10_{name}_times"] = np.array(logs["timesteps"], dtype=np.int64)
+        for name, dt in (("fp32", None), ("fp16", torch.float16)):
+            if dt is None:
+                x, _ = ldm.content_style_ddim_sample(zT, emb, timesteps=100, eta=1.0)
+            else:
+                with torch.autocast("cpu", dtype=dt):
+                    x, _ = ldm.content_style_ddim_sample(zT, emb, timesteps=100, eta=1.0)
+            G[f"cs100_{name}_x"] = np32(x.float())
+        # the restated train step of part (7) (fp32 golden: ref_goldens.npz train_*) with its forward and
+        # losses under torch.autocast("cpu", bfloat16) -- the reference's own train_step region on a CPU
+        # device (train.py:174) -- and backward outside it; the q_sample noise is injected (fp32, the
+        # recorded train_noise) by standing in for torch.randn_like, which would otherwise draw it in the
+        # autocast dtype of the encoder output.
+    g1 = np.load(os.path.join(HERE, "ref_goldens.npz"))
+    ldm = M.LDM(32, pretrained_path="")
+    recipe.fill_module(ldm, seed=700)
+    ldm.train()
+    for p_ in ldm.encoder.parameters():
+        p_.requires_grad_(False)
+    content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 710))
+    style2 = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 711))
+    t2 = torch.from_numpy(recipe.timesteps(2, 712))
+    noise = torch.from_numpy(g1["train_noise"])
+    real_randn_like = torch.randn_like
+    torch.randn_like = lambda t, *a, **k: noise.clone()
+    try:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            out = ldm(content, style2, t2)
+            dl = L.diffusion_loss(out["noise_pred"], out["noise"])
+            mse = torch.nn.MSELoss()(out["reconstructed"], content)
+            kl = L.kl_regularization_loss(out["z_0"])
+            total = mse + 0.01 * kl + dl
+    finally:
+        torch.randn_like = real_randn_like
+    total.backward()
+    G["trainbf16_total"] = np32(total.float())
+    G["trainbf16_recon"] = np32(out["reconstructed"].float())
+    named = dict(ldm.named_parameters())
+    for k in TRAIN_GRAD_KEYS:
+        g = named[k].grad
+        G["trainbf16_grad_" + k] = np32(g[:256] if g.dim() == 2 and g.shape[0] > 256 else g)
+    path = os.path.join(HERE, "ref_goldens_amp.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
+TRAIN_GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
+                   "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
+                   "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
+                   "style_encoder.enc1.weight")
+
 AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.encoder.4.bias", "encoder.encoder.6.bias",
            "encoder.encoder.7.weight", "decoder.decoder.0.weight", "decoder.decoder.1.bias", "decoder.decoder.4.weight",
            "decoder.decoder.6.weight", "decoder.decoder.6.bias")
@@ -272,5 +348,7 @@ AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.enco
 if __name__ == "__main__":
     if "--r2" in sys.argv:
         round2()
+    elif "--amp" in sys.argv:
+        amp()
     else:
         main()
