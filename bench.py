@@ -412,15 +412,23 @@ def main():
         eng = M.engine_for(ldm.unet)
         eng.dtype = args.dtype
         gd = GraphedDDIM(eng, z_T, emb["s5"], emb["s6"], t_table, coefs, args.eta, logs=True, split=args.split)
-        for _ in range(args.warmup):
+        # N > 1: every step ends with the sample all-gather of dist.sharded_style_sample (RCCL over xGMI),
+        # so the timed region holds the job's only collective
+        gathered = torch.empty((world,) + tuple(gd.x.shape), device=dev) if world > 1 else None
+
+        def one_step():
             gd.replay()
+            if gathered is not None:
+                dist.all_gather_into_tensor(gathered, gd.x)
+        for _ in range(args.warmup):
+            one_step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            gd.replay()
+            one_step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -452,7 +460,9 @@ def main():
                     f"per step, content encoded and q_sampled at T'-1 before timing), batch {B}/GPU, "
                     f"eta={args.eta}, {args.dtype} step-kernel operands with fp32 accumulators, hipGraph replay"),
                    "global_batch": B * world,
-                   "latent": [B, 32, 16, 64], "parallelism": f"dp{world} (independent batch shards)"},
+                   "latent": [B, 32, 16, 64],
+                   "parallelism": f"dp{world} (batch shards" + (", all-gather of the samples every step)" if world > 1
+                                                                 else ")")},
         "us_per_denoise_iteration": round(us_iter, 2),
     }
     # whole-step composite roofline

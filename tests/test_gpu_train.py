@@ -123,15 +123,19 @@ def test_linear_and_gelu_backward(cuda):
         assert rel_err(npy(g.grad), r.grad.numpy()) < TOL
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 8, 8), (3, 8, 36, 36), (5, 4, 30, 30), (32, 16, 16, 64)])
 @pytest.mark.parametrize("act", ["none", "relu"])
-def test_batchnorm_train_backward(cuda, act):
+def test_batchnorm_train_backward(cuda, act, shape):
+    """Train-mode BN forward / backward against fp64 autograd; the shapes force several slices per
+    channel (P > 1), slices crossing plane boundaries, the scalar path (HW % 4 != 0) and the B=32 form."""
     from ldm_amd import nn as hnn
-    x = _rand((4, 64, 8, 8), 21, -2, 2)
-    bn_ref = torch.nn.BatchNorm2d(64).double()
-    bn = hnn.BatchNorm2d(64).to(cuda)
+    C = shape[1]
+    x = _rand(shape, 21, -2, 2)
+    bn_ref = torch.nn.BatchNorm2d(C).double()
+    bn = hnn.BatchNorm2d(C).to(cuda)
     with torch.no_grad():
-        g = torch.from_numpy(_rand((64,), 22, 0.5, 1.5))
-        b = torch.from_numpy(_rand((64,), 23, -0.1, 0.1))
+        g = torch.from_numpy(_rand((C,), 22, 0.5, 1.5))
+        b = torch.from_numpy(_rand((C,), 23, -0.1, 0.1))
         bn_ref.weight.copy_(g.double())
         bn_ref.bias.copy_(b.double())
         bn.weight.copy_(g.to(cuda))
@@ -140,7 +144,7 @@ def test_batchnorm_train_backward(cuda, act):
     ref = bn_ref(xt)
     if act == "relu":
         ref = torch.relu(ref)
-    R = _rand((4, 64, 8, 8), 24)
+    R = _rand(shape, 24)
     (ref * torch.from_numpy(R).double()).sum().backward()
     xg = T(x, cuda).requires_grad_()
     y = bn(xg, act=act)
@@ -456,3 +460,29 @@ def test_wgrad_tap_shared(cuda, case):
     acc = torch.ones_like(dw1)
     ops.conv_backward_weight(xg, dyg, desc, dw=acc, accumulate=True)
     assert rel_err(npy(acc), wt.grad.numpy() + 1.0) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(32, 128, 1, 1), (32, 512, 2, 8), (3, 8, 36, 36), (2, 64, 5, 5)])
+@pytest.mark.parametrize("act", ["none", "relu", "gelu"])
+def test_act_backward_sums(cuda, shape, act):
+    """ldm_act_backward (dv, dbias, dbcast) against fp64 on the small-plane kernel (HW <= 16) and the
+    sliced one (scalar and float4 paths)."""
+    from ldm_amd import ops
+    B, C = shape[0], shape[1]
+    v = torch.from_numpy(_rand(shape, 31, -2, 2)).double()
+    dy = torch.from_numpy(_rand(shape, 32)).double()
+    if act == "gelu":
+        a = torch.nn.functional.gelu(v)
+        dv_ref = dy * (0.5 * (1 + torch.erf(v / 2 ** 0.5)) + v * torch.exp(-0.5 * v * v) / (2 * 3.141592653589793) ** 0.5)
+    elif act == "relu":
+        a = torch.relu(v)
+        dv_ref = dy * (a > 0)
+    else:
+        a = v
+        dv_ref = dy
+    dv, db, dbc = ops.act_backward(dy.float().to(cuda), act, act_out=a.float().to(cuda),
+                                   pre_act=v.float().to(cuda) if act == "gelu" else None, need_dv=True,
+                                   need_bias=True, need_bcast=True)
+    assert rel_err(npy(dv), dv_ref.numpy()) < 1e-5
+    assert rel_err(npy(db), dv_ref.sum(dim=(0, 2, 3)).numpy()) < 1e-5
+    assert rel_err(npy(dbc).reshape(B, C), dy.sum(dim=(2, 3)).numpy()) < 1e-5
