@@ -271,6 +271,15 @@ int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* w, float* x
                     const float* s6, const int64_t* t_table, const float* coef_table, int32_t nsteps, float eta,
                     float* x0_logs, float* eps_logs, int64_t log_step_stride, float* workspace, void* stream);
 
+/* ---- data formats either side of the path (dataio.hip) ---------------------------
+ * ldm_mel_quantize: the reference's 8-bit mel PNG pixels, uint8(clip((db + max_db) * 255/max_db, 0, 255)
+ * + 0.5) (audio_processor.py:55-73, fp32 arithmetic, bit-exact with its numpy); ldm_mel_dequantize: its
+ * inverse db = u8 * max_db/255 - max_db (audio_processor.py:91-93); ldm_u8_to_unit: the [0,1] tensor the
+ * model consumes, u8 / 255 (dataset.py:258, torchvision ToTensor). */
+int ldm_mel_quantize(const float* db, uint8_t* out, int64_t n, float max_db, void* stream);
+int ldm_mel_dequantize(const uint8_t* in, float* db, int64_t n, float max_db, void* stream);
+int ldm_u8_to_unit(const uint8_t* in, float* out, int64_t n, void* stream);
+
 /* ---- step kernels (uconv.hip): fixed-structure implicit GEMMs of the nine UNet convs -------------------
  * Packed size (floats) of layer `layer` (0..8 = enc1..dec1) and its packing from the torch weight layout
  * (conv [Cout][Cin][3][3], transposed conv [Cin][Cout][3][3]).  ldm_step_conv runs one layer on NHWC

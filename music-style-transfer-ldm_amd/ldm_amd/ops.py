@@ -551,3 +551,37 @@ def ddim_step_(x, eps, coef4, eta, x0_log=None, eps_log=None):
     L.call("ldm_ddim_step", x.data_ptr(), eps.data_ptr(), coef4.data_ptr(), float(eta), _p(x0_log), _p(eps_log),
            x.numel(), stream_handle())
     return x
+
+
+# ------------------------------------------------------------------------------------------------
+# data formats either side of the path (dataio.hip): 8-bit mel PNG pixels <-> dB, ToTensor
+# ------------------------------------------------------------------------------------------------
+def mel_quantize(db, max_db=80):
+    """uint8 pixels of the reference's mel PNG (audio_processor.py:55-73) from a log-mel dB tensor."""
+    require_device(db)
+    db = f32c(db)
+    out = torch.empty(db.shape, device=db.device, dtype=torch.uint8)
+    L.call("ldm_mel_quantize", db.data_ptr(), out.data_ptr(), db.numel(), float(max_db), stream_handle())
+    return out
+
+
+def mel_dequantize(u8, max_db=80):
+    """log-mel dB from the 8-bit pixels (audio_processor.py:91-93)."""
+    require_device(u8, dtype=torch.uint8)
+    if u8.dtype != torch.uint8:
+        raise RuntimeError("mel_dequantize: expects uint8 pixels")
+    u8 = u8.contiguous()
+    out = torch.empty(u8.shape, device=u8.device, dtype=torch.float32)
+    L.call("ldm_mel_dequantize", u8.data_ptr(), out.data_ptr(), u8.numel(), float(max_db), stream_handle())
+    return out
+
+
+def u8_to_unit(u8):
+    """The [0,1] fp32 tensor torchvision's ToTensor makes of 8-bit pixels (u8 / 255)."""
+    require_device(u8, dtype=torch.uint8)
+    if u8.dtype != torch.uint8:
+        raise RuntimeError("u8_to_unit: expects uint8 pixels")
+    u8 = u8.contiguous()
+    out = torch.empty(u8.shape, device=u8.device, dtype=torch.float32)
+    L.call("ldm_u8_to_unit", u8.data_ptr(), out.data_ptr(), u8.numel(), stream_handle())
+    return out
