@@ -318,41 +318,46 @@ __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float*
     if (dbias) dbias[c] = sb;
 }
 
-// Small planes (HW <= 16: the Linear layers, HW = 1, and the 2x8 projections): one lane per channel walks
-// its B*HW elements in order and writes dv, dbcast and dbias directly -- one launch instead of the
-// sliced kernel's B*C tiny blocks plus the finalize pass.
+// Small planes (HW <= 16: the Linear layers, HW = 1, and the 2x8 projections): one block per channel
+// over its B*HW elements (dv elementwise, dbias by a block sum, dbcast[b] by the first B lanes over their
+// HW elements) -- one launch instead of the sliced kernel's B*C tiny blocks plus the finalize pass.
 __global__ __launch_bounds__(kThreads) void act_bwd_small_kernel(const float* __restrict__ dy,
                                                                  const float* __restrict__ aval,
                                                                  const float* __restrict__ pre, int act, int B, int C,
                                                                  int HW, float* __restrict__ dv,
                                                                  float* __restrict__ dbias, float* __restrict__ dbcast) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float sb = 0.f;
-    for (int b = 0; b < B; ++b) {
-        const size_t base = ((size_t)b * C + c) * HW;
-        float sd = 0.f, sg = 0.f;
-        for (int i = 0; i < HW; ++i) {
-            const float g = dy[base + i];
-            float d;
-            if (act == LDM_ACT_GELU) {
-                const float v = pre[base + i];
-                const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752440f));
-                const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
-                d = g * (cdf + v * pdf);
-            } else if (aval) {
-                d = g * act_grad(act, aval[base + i]);
-            } else {
-                d = g;
-            }
-            if (dv) dv[base + i] = d;
-            sd += d;
-            sg += g;
+    __shared__ float red[kThreads / 64];
+    const int c = blockIdx.x;
+    auto dval = [&](size_t o) {
+        const float g = dy[o];
+        if (act == LDM_ACT_GELU) {
+            const float v = pre[o];
+            const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752440f));
+            const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
+            return g * (cdf + v * pdf);
         }
-        sb += sd;
-        if (dbcast) dbcast[(size_t)b * C + c] = sg;
+        return aval ? g * act_grad(act, aval[o]) : g;
+    };
+    float sd = 0.f;
+    for (int e = threadIdx.x; e < B * HW; e += blockDim.x) {
+        const int b = e / HW, i = e - b * HW;
+        const size_t o = ((size_t)b * C + c) * HW + i;
+        const float d = dval(o);
+        if (dv) dv[o] = d;
+        sd += d;
     }
-    if (dbias) dbias[c] = sb;
+    if (dbias) {
+        sd = block_sum(sd, red);
+        if (threadIdx.x == 0) dbias[c] = sd;
+    }
+    if (dbcast) {
+        for (int b = threadIdx.x; b < B; b += blockDim.x) {
+            const size_t o = ((size_t)b * C + c) * HW;
+            float sg = 0.f;
+            for (int i = 0; i < HW; ++i) sg += dy[o + i];
+            dbcast[(size_t)b * C + c] = sg;
+        }
+    }
 }
 
 bool vec_ok(int HW, const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr) {
@@ -495,7 +500,7 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
     const bool sums = dbias || dbcast;
     const float* aval0 = act == LDM_ACT_NONE || act == LDM_ACT_GELU ? nullptr : act_out;
     if (HW <= 16) {
-        hipLaunchKernelGGL(act_bwd_small_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
+        hipLaunchKernelGGL(act_bwd_small_kernel, dim3(C), dim3(kThreads), 0,
                            (hipStream_t)stream, dy, aval0, pre_act, act, B, C, HW, dv, dbias, dbcast);
         LDM_CHECK_LAUNCH("act_bwd_small_kernel");
         return 0;
