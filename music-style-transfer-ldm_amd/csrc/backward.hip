@@ -90,13 +90,29 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WgradArgs a) {
 
 // sum of split partials in split order.  Tap t is the kernel-window index (kh*kw + kw), so the
 // [m][c*T + t] GEMM layout IS the torch weight layout [m][c][kh][kw].
+// 256 threads = 16 outputs x 16 split groups: group g sums its contiguous range of splits serially, the
+// 16 group sums are added in group order (a fixed partition and order: bitwise reproducible).  One thread
+// per output walking all S splits serially was latency-bound at small M*N (60 us for 1024 outputs x 256
+// splits).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial, int S, int MN,
                                                            float* __restrict__ dw, int accumulate) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= MN) return;
+    __shared__ float red[16][17];
+    const int ol = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int i = blockIdx.x * 16 + ol;
+    const int G = S < 16 ? S : 16;
+    const int per = (S + G - 1) / G;
     float v = 0.f;
-    for (int s = 0; s < S; ++s) v = v + partial[(size_t)s * MN + i];
-    dw[i] = accumulate ? dw[i] + v : v;
+    if (i < MN && g < G) {
+        const int s1 = min(S, (g + 1) * per);
+        for (int s = g * per; s < s1; ++s) v = v + partial[(size_t)s * MN + i];
+    }
+    red[g][ol] = v;
+    __syncthreads();
+    if (g == 0 && i < MN) {
+        float t = red[0][ol];
+        for (int k = 1; k < G; ++k) t = t + red[k][ol];
+        dw[i] = accumulate ? dw[i] + t : t;
+    }
 }
 
 // ================================================================================================
@@ -194,6 +210,20 @@ __global__ __launch_bounds__(256) void attention_backward_kernel(const float* __
 // ================================================================================================
 // multi-tensor Adam (torch.optim.Adam, train.py:156) with GradScaler unscale / inf check / skip
 // ================================================================================================
+// A chunk's elements, float4 at a time where every pointer of the slot is 16-byte aligned (the chunk
+// start is a multiple of 4 elements), the ragged tail one at a time; f(i, W) handles elements i..i+W-1.
+template <class F4, class F1>
+__device__ __forceinline__ void chunk_for(int64_t s0, int64_t e0, bool vec, F4&& f4, F1&& f1) {
+    int64_t t0 = s0;
+    if (vec) {
+        const int64_t n4 = (e0 - s0) >> 2;
+        for (int64_t j = threadIdx.x; j < n4; j += blockDim.x) f4(s0 + 4 * j);
+        t0 = s0 + 4 * n4;
+    }
+    for (int64_t i = t0 + threadIdx.x; i < e0; i += blockDim.x) f1(i);
+}
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 __global__ __launch_bounds__(256) void unscale_check_kernel(const ldm_tensor_slot* __restrict__ slots,
                                                             const int32_t* __restrict__ chunk_tensor,
                                                             const int64_t* __restrict__ chunk_start, int chunk_len,
@@ -204,40 +234,68 @@ __global__ __launch_bounds__(256) void unscale_check_kernel(const ldm_tensor_slo
     const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
     const float is = inv_scale ? inv_scale[0] : 1.f;
     bool bad = false;
-    for (int64_t i = s0 + threadIdx.x; i < e0; i += blockDim.x) {
-        const float g = sl.grad[i] * is;
-        sl.grad[i] = g;
-        bad |= !isfinite(g);
-    }
+    chunk_for(
+        s0, e0, al16(sl.grad + s0),
+        [&](int64_t i) {
+            float4 g = *reinterpret_cast<const float4*>(sl.grad + i);
+            g.x *= is, g.y *= is, g.z *= is, g.w *= is;
+            *reinterpret_cast<float4*>(sl.grad + i) = g;
+            bad |= !isfinite(g.x) || !isfinite(g.y) || !isfinite(g.z) || !isfinite(g.w);
+        },
+        [&](int64_t i) {
+            const float g = sl.grad[i] * is;
+            sl.grad[i] = g;
+            bad |= !isfinite(g);
+        });
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found_inf, 1);   // a flag, not a sum: order-free
+}
+
+struct AdamScalars {
+    float one_m_beta1, beta2, one_m_beta2, eps, weight_decay, decay_mul, step_size, bc2_sqrt;
+};
+// torch.optim.Adam / AdamW (_single_tensor_adam, non-capturable) on one element
+__device__ __forceinline__ void adam_elem(const AdamScalars& k, float& p, float g, float& m, float& v) {
+    if (k.decay_mul != 1.f) p = p * k.decay_mul;                 // AdamW: param.mul_(1 - lr * weight_decay)
+    else if (k.weight_decay != 0.f) g = g + k.weight_decay * p;  // Adam: grad.add(param, alpha=wd)
+    m = m + k.one_m_beta1 * (g - m);                              // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * k.beta2;                                              // exp_avg_sq.mul_(beta2)
+    v = v + (k.one_m_beta2 * g) * g;                              //   .addcmul_(grad, grad, value=1 - beta2)
+    const float denom = sqrtf(v) / k.bc2_sqrt + k.eps;
+    p = p + (-k.step_size) * (m / denom);                         // param.addcdiv_(exp_avg, denom, value=-step_size)
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(const ldm_tensor_slot* __restrict__ slots,
                                                    const int32_t* __restrict__ chunk_tensor,
                                                    const int64_t* __restrict__ chunk_start, int chunk_len,
-                                                   float one_m_beta1, float beta2, float one_m_beta2, float eps,
-                                                   float weight_decay, float decay_mul, float step_size,
-                                                   float bias_correction2_sqrt, const int32_t* __restrict__ found_inf) {
+                                                   AdamScalars k, const int32_t* __restrict__ found_inf) {
     if (found_inf && found_inf[0]) return;   // GradScaler.step skips the update on inf/nan
     const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
     const int64_t s0 = chunk_start[blockIdx.x];
     const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
     // scalars arrive as torch's: host doubles cast once to fp32 (1-beta computed in double)
-    for (int64_t i = s0 + threadIdx.x; i < e0; i += blockDim.x) {
-        float g = sl.grad[i];
-        float p = sl.param[i];
-        if (decay_mul != 1.f) p = p * decay_mul;          // AdamW: param.mul_(1 - lr * weight_decay)
-        else if (weight_decay != 0.f) g = g + weight_decay * p;   // Adam: grad.add(param, alpha=wd)
-        float m = sl.exp_avg[i], v = sl.exp_avg_sq[i];
-        m = m + one_m_beta1 * (g - m);                // exp_avg.lerp_(grad, 1 - beta1)
-        v = v * beta2;                                // exp_avg_sq.mul_(beta2)
-        v = v + (one_m_beta2 * g) * g;                //   .addcmul_(grad, grad, value=1 - beta2)
-        const float denom = sqrtf(v) / bias_correction2_sqrt + eps;
-        p = p + (-step_size) * (m / denom);           // param.addcdiv_(exp_avg, denom, value=-step_size)
-        sl.exp_avg[i] = m;
-        sl.exp_avg_sq[i] = v;
-        sl.param[i] = p;
-    }
+    const bool vec = al16(sl.grad + s0) && al16(sl.param + s0) && al16(sl.exp_avg + s0) && al16(sl.exp_avg_sq + s0);
+    chunk_for(
+        s0, e0, vec,
+        [&](int64_t i) {
+            const float4 g = *reinterpret_cast<const float4*>(sl.grad + i);
+            float4 p = *reinterpret_cast<const float4*>(sl.param + i);
+            float4 m = *reinterpret_cast<const float4*>(sl.exp_avg + i);
+            float4 v = *reinterpret_cast<const float4*>(sl.exp_avg_sq + i);
+            adam_elem(k, p.x, g.x, m.x, v.x);
+            adam_elem(k, p.y, g.y, m.y, v.y);
+            adam_elem(k, p.z, g.z, m.z, v.z);
+            adam_elem(k, p.w, g.w, m.w, v.w);
+            *reinterpret_cast<float4*>(sl.exp_avg + i) = m;
+            *reinterpret_cast<float4*>(sl.exp_avg_sq + i) = v;
+            *reinterpret_cast<float4*>(sl.param + i) = p;
+        },
+        [&](int64_t i) {
+            float p = sl.param[i], m = sl.exp_avg[i], v = sl.exp_avg_sq[i];
+            adam_elem(k, p, sl.grad[i], m, v);
+            sl.exp_avg[i] = m;
+            sl.exp_avg_sq[i] = v;
+            sl.param[i] = p;
+        });
 }
 
 // torch.amp.GradScaler._amp_update_scale_: backoff on inf, grow after growth_interval clean steps
@@ -335,7 +393,7 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st);   // the tap-shared form (wgrad.hip) where it applies
     if (rc > 0) return rc;
     if (rc == 0) {
-        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)workspace, S2,
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 15) / 16), dim3(256), 0, st, (const float*)workspace, S2,
                            MN, dw, accumulate);
         LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
         return 0;
@@ -346,7 +404,7 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     dim3 grid((a.N + 15) / 16, (a.M + 15) / 16, S);
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(64), 0, st, a);
     LDM_CHECK_LAUNCH("wgrad_kernel");
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 255) / 256), dim3(256), 0, st, (const float*)a.partial, S, MN,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 15) / 16), dim3(256), 0, st, (const float*)a.partial, S, MN,
                        dw, accumulate);
     LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
     return 0;
@@ -386,10 +444,17 @@ extern "C" int ldm_adam_step(const ldm_tensor_slot* slots, const int32_t* chunk_
     const double bc1 = 1.0 - std::pow(beta1, (double)step);
     const double bc2 = 1.0 - std::pow(beta2, (double)step);
     const double step_size = lr / bc1;
+    AdamScalars k;
+    k.one_m_beta1 = (float)(1.0 - beta1);
+    k.beta2 = (float)beta2;
+    k.one_m_beta2 = (float)(1.0 - beta2);
+    k.eps = (float)eps;
+    k.weight_decay = (float)weight_decay;
+    k.decay_mul = decoupled ? (float)(1.0 - lr * weight_decay) : 1.f;
+    k.step_size = (float)step_size;
+    k.bc2_sqrt = (float)std::sqrt(bc2);
     hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, slots, chunk_tensor, chunk_start,
-                       chunk_len, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
-                       (float)weight_decay, decoupled ? (float)(1.0 - lr * weight_decay) : 1.f, (float)step_size,
-                       (float)std::sqrt(bc2), found_inf);
+                       chunk_len, k, found_inf);
     LDM_CHECK_LAUNCH("adam_kernel");
     return 0;
 }

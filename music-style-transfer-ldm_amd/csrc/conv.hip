@@ -933,6 +933,151 @@ __global__ __launch_bounds__(256) void conv_cin1_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Thin VAE layers at full mel resolution (B = 32 in the train step: 134 MB activations each), four
+// adjacent output columns per lane so that every store is one 16-byte store and each input window is
+// loaded once for 4 (or 16) outputs.  Simple epilogues only (bias, eval-BN, act, act_out: the host
+// routes anything else to the kernels above); arithmetic and accumulation order equal conv_cin1_kernel /
+// conv_direct_kernel's, so the results are the same bits.
+// ------------------------------------------------------------------------------------------------
+struct ChanEpi {
+    float bias, alpha, beta;
+};
+__device__ __forceinline__ ChanEpi chan_epi(const ConvArgs& a, int m) {
+    const EpiArgs& e = a.ep;
+    ChanEpi c{0.f, 1.f, 0.f};
+    if (e.bias) c.bias = e.bias[m];
+    if (e.bn_w) {   // as epi_finish
+        const float invstd = 1.0f / sqrtf(e.bn_v[m] + e.bn_eps);
+        c.alpha = invstd * e.bn_w[m];
+        c.beta = e.bn_b[m] - e.bn_m[m] * c.alpha;
+    }
+    return c;
+}
+__device__ __forceinline__ float chan_apply(const ConvArgs& a, const ChanEpi& c, float v) {
+    if (a.ep.bias) v = v + c.bias;
+    if (a.ep.bn_w) v = v * c.alpha + c.beta;
+    return apply_act(v, a.ep.act);
+}
+__device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float (&v)[4]) {
+    const float4 t = make_float4(v[0], v[1], v[2], v[3]);
+    if (a.ep.act_out) *reinterpret_cast<float4*>(a.ep.act_out + o) = t;
+    *reinterpret_cast<float4*>(a.y + o) = t;
+}
+
+// Cin = 1, stride 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
+// 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (6 + K) input window in registers,
+// every output channel from it, weights in LDS.
+template <int K>
+__global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
+    __shared__ float ws[64 * K * K];
+    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = a.w[i];   // [co][ky*K + kx]
+    __syncthreads();
+    const int W4 = a.Wout >> 2;
+    const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (idx >= a.B * a.Hout * W4) return;
+    const int r = a.fd_dwo.div(idx);   // fd_dwo = W4 here
+    const int ox0 = (idx - r * W4) * 4;
+    const int b = a.fd_dho.div(r);
+    const int oy = r - b * a.Hout;
+    constexpr int NC = 6 + K;
+    const int pad = -a.pt.dy[0][0];
+    const int iy0 = 2 * oy - pad, ix0 = 2 * ox0 - pad;
+    const float* xb = a.x + (size_t)b * a.Hin * a.Win;
+    float win[K][NC];
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+        const int iy = iy0 + ky;
+        const bool rok = (unsigned)iy < (unsigned)a.Hin;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int ix = ix0 + c;
+            const bool ok = rok && (unsigned)ix < (unsigned)a.Win;
+            win[ky][c] = ok ? xb[iy * a.Win + ix] : 0.f;
+        }
+    }
+    const size_t plane = (size_t)a.Hout * a.Wout;
+    size_t o = ((size_t)b * a.Cout * a.Hout + oy) * a.Wout + ox0;
+    for (int co = 0; co < a.Cout; ++co, o += plane) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) {
+                const float w = ws[co * K * K + ky * K + kx];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = fmaf(win[ky][kx + 2 * j], w, acc[j]);
+            }
+        const ChanEpi ce = chan_epi(a, co);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[j]);
+        store4(a, o, v);
+    }
+}
+
+// ConvTranspose2d(Cin -> 1, k4, s2, p1) (the decoder's output layer): lane = (b, qy, 4 input columns
+// qx0..qx0+3) -> the 2 x 8 outputs they feed (all four parities); per input channel a 3 x 6 window.
+// Taps in the phase-table order of build_phase_table: parity r uses kernel rows {1, 3} (r = 0, input
+// offsets 0, -1) or {0, 2} (r = 1, offsets +1, 0).
+__host__ __device__ constexpr int ct4_tap(int r, int i) { return r == 0 ? (i == 0 ? 1 : 3) : (i == 0 ? 0 : 2); }
+__host__ __device__ constexpr int ct4_off(int r, int i) { return (r + 1 - ct4_tap(r, i)) >> 1; }
+
+__global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
+    const int W4 = a.Win >> 2;
+    const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (idx >= a.B * a.Hin * W4) return;
+    const int r = a.fd_dwo.div(idx);   // fd_dwo = W4 here
+    const int qx0 = (idx - r * W4) * 4;
+    const int b = a.fd_dho.div(r);     // fd_dho = Hin here
+    const int qy = r - b * a.Hin;
+    const int HW = a.Hin * a.Win;
+    float acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+    bool rok[3], cok[6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rok[i] = (unsigned)(qy - 1 + i) < (unsigned)a.Hin;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) cok[c] = (unsigned)(qx0 - 1 + c) < (unsigned)a.Win;
+    const float* xp = a.x + (size_t)b * a.Cin * HW + (qy - 1) * a.Win + (qx0 - 1);
+    for (int ci = 0; ci < a.Cin; ++ci, xp += HW) {
+        float xr[3][6];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) xr[i][c] = (rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f;
+        const float* wq = a.w + ci * 16;   // w [Cin][1][4][4]
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+            for (int rx = 0; rx < 2; ++rx)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int ia = t >> 1, ib = t & 1;
+                    const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
+                    const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        acc[ry][2 * jj + rx] = fmaf(xr[1 + dy][1 + jj + dx], w, acc[ry][2 * jj + rx]);
+                }
+    }
+    const ChanEpi ce = chan_epi(a, 0);
+#pragma unroll
+    for (int ry = 0; ry < 2; ++ry) {
+        const size_t o = ((size_t)b * a.Hout + 2 * qy + ry) * a.Wout + 2 * qx0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[ry][4 * h + j]);
+            store4(a, o + 4 * h, v);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // weight packing into fragment order: packed[phase][chunk][Mpad][NLG][4], k = chunk*CK + NLG*j + lg
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w, float* __restrict__ out, ConvArgs a,
@@ -1236,6 +1381,29 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
         a.fd_dwo = FastDiv::make(d.Wout);
         a.fd_dho = FastDiv::make(d.Hout);
         a.fd_dco = FastDiv::make(d.Cout);
+        const bool simple_epi = !ep.pos_bias && !ep.bcast && !ep.skip && !ep.ddim_coef && y;
+        if (simple_epi && d.Cin == 1 && !d.transposed && d.Cout <= 64 && d.kh == d.kw && (d.kh == 3 || d.kh == 4) &&
+            d.stride == 2 && d.Wout % 4 == 0 && a.pt.dy[0][0] == -d.pad && a.pt.dx[0][0] == -d.pad &&
+            ((uintptr_t)y & 15) == 0 && (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
+            a.fd_dwo = FastDiv::make(d.Wout / 4);
+            const int64_t lanes = (int64_t)d.B * d.Hout * (d.Wout / 4);
+            if (d.kh == 3)
+                hipLaunchKernelGGL(conv_cin1_x4_kernel<3>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL(conv_cin1_x4_kernel<4>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+            LDM_CHECK_LAUNCH("conv_cin1_x4_kernel");
+            return 0;
+        }
+        if (simple_epi && d.transposed && d.Cout == 1 && d.kh == 4 && d.kw == 4 && d.stride == 2 && d.pad == 1 &&
+            d.out_pad == 0 && d.Win % 4 == 0 && a.pt.nphase == 4 && ((uintptr_t)y & 15) == 0 &&
+            (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
+            a.fd_dwo = FastDiv::make(d.Win / 4);
+            a.fd_dho = FastDiv::make(d.Hin);
+            const int64_t lanes = (int64_t)d.B * d.Hin * (d.Win / 4);
+            hipLaunchKernelGGL(convT4_cout1_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+            LDM_CHECK_LAUNCH("convT4_cout1_kernel");
+            return 0;
+        }
         if (d.Cin == 1 && !d.transposed && d.Cout <= 64 && a.KK <= 16) {
             const int64_t pix = (int64_t)d.B * d.Hout * d.Wout;
             hipLaunchKernelGGL(conv_cin1_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, st, a);

@@ -209,6 +209,109 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// One gathered channel (C = 1: the Cin = 1 first layers of the VAE / style encoders, and the decoder's
+// 64 -> 1 output convT): the N dimension of the GEMM is the k*k taps instead of 16 channels (the general
+// kernel spent 15/16 of its window DMAs and MFMAs on padding channels there).  Block = 4 waves x 16 rows
+// (m) x 16 columns (taps; k = 3 leaves 7 idle); the lane of column t reads its tap's window value, so the
+// whole 16 x 16 x (64 positions) product of a chunk is 4 (16 in f32) MFMAs per wave.
+template <int S, int KK, int DT>
+__global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
+    constexpr int T = KK * KK, BM = 64, AF = BM * kKQ;
+    static_assert(T <= 16, "taps per column tile");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane & 15, lg = lane >> 4;
+    const int m0 = blockIdx.y * BM;
+    const int HQ = a.Hq * a.Wq;
+    const int bufF = buf_floats(AF, 1, a.pitch_c);
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.gath), (short)0, uni(a.B * a.Hg * a.Wg * 4), 0x00020000);
+
+    auto issue = [&](int ch, int buf) {
+        int b, qy0, qx0;
+        b = ch / a.cps;
+        const int r = ch - b * a.cps;
+        if (a.cols == a.Wq) {
+            qy0 = r * a.rows, qx0 = 0;
+        } else {
+            const int segs = a.Wq / kKQ;
+            qy0 = r / segs, qx0 = (r - qy0 * segs) * kKQ;
+        }
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+        for (int gi = wave; gi < BM / 4; gi += 4) {
+            const int row = gi * 4 + (lane >> 4);
+            const int p = lane & 15;
+            const int sp = p ^ (row & 15);
+            const int m = m0 + row;
+            const int ql = sp * 4;
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const bool ok = m < a.M && qy < a.Hq;
+            const int voff = ok ? (((b * a.M + m) * HQ + qy * a.Wq + qx) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(base + gi * 1024), 16, voff, 0, 0, 0);
+        }
+        const int wq4 = a.wca >> 2;
+        const int npiece = a.wr * wq4;
+        const int row0 = qy0 * S - a.pad, colA = qx0 * S - a.pad - a.e;
+        for (int gi = wave; gi * 64 < npiece; gi += 4) {
+            const int pc = gi * 64 + lane;
+            const int wrow = pc / wq4, wp = pc - wrow * wq4;
+            const int iy = row0 + wrow, ix = colA + wp * 4;
+            const bool ok = pc < npiece && (unsigned)iy < (unsigned)a.Hg && (unsigned)ix < (unsigned)a.Wg;
+            const int voff = ok ? (((b * a.Hg + iy) * a.Wg + ix) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + AF * 4 + gi * 1024), 16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    int aoff[4], boff[4];
+    const int row = wave * 16 + col;
+    const int tcol = col < T ? col : 0;   // idle columns (k = 3) re-read tap 0; their results are dropped
+    const int ky = tcol / KK, kx = tcol - ky * KK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        aoff[u] = row * kKQ + (((4 * u + lg) ^ (row & 15)) << 2);
+        const int ql = (16 * u + 4 * lg < a.rows * a.cols) ? 16 * u + 4 * lg : 0;
+        const int rl = ql / a.cols, xl = ql - rl * a.cols;
+        boff[u] = AF + (rl * S + ky) * a.wca + a.e + xl * S + kx;
+    }
+
+    if (ch_begin < ch_end) issue(ch_begin, 0);
+    for (int ch = ch_begin; ch < ch_end; ++ch) {
+        const int buf = (ch - ch_begin) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+        const float* sb = smem + buf * bufF;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const floatx4 fa = *reinterpret_cast<const floatx4*>(sb + aoff[u]);
+            floatx4 bv;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = sb[boff[u] + j * S];
+            if constexpr (DT == 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[j], bv[j], acc, 0, 0, 0);
+            } else {
+                acc = mma16_lowp<DT>(fa, bv, acc);
+            }
+        }
+    }
+    // D: row m = m0 + 16*wave + 4*lg + r, column = tap col
+    if (col < T) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * T;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wave * 16 + 4 * lg + r;
+            if (m < a.M) out[(size_t)m * T + col] = acc[r];
+        }
+    }
+}
+
 struct Plan {
     int S, KK, BM, BC, splits;
     Args a;
@@ -241,13 +344,15 @@ bool plan(const ldm_conv_desc& d, Plan& p) {
     a.wca = (a.e + wc + 3) / 4 * 4;
     a.pitch_c = a.wr * a.wca;
     p.S = S, p.KK = KK;
-    p.BC = (a.C <= 16 || KK == 4) ? 16 : 32;
+    p.BC = a.C == 1 ? 1 : (a.C <= 16 || KK == 4) ? 16 : 32;
     p.BM = (p.BC == 32 && a.M <= 32) ? 32 : 64;
     p.lds_bytes = 2 * buf_floats(p.BM * kKQ, p.BC, a.pitch_c) * 4;
     if (p.lds_bytes > 160 * 1024) return false;
     const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + p.BC - 1) / p.BC);
+    // the one-channel kernel keeps 4 blocks per CU resident: up to 1024 splits
+    const int smax = p.BC == 1 ? 1024 : 256, want = p.BC == 1 ? 1024 : 512;
     int s = 1;
-    while (s < 256 && tiles * s < 512 && a.nchunk / (s * 2) >= 2) s *= 2;
+    while (s < smax && tiles * s < want && a.nchunk / (s * 2) >= 2) s *= 2;
     p.splits = s;
     a.per_split = (a.nchunk + s - 1) / s;
     p.a = a;
@@ -266,6 +371,23 @@ int launch_dt(const Plan& p, hipStream_t st) {
     hipLaunchKernelGGL(kfn, grid, dim3(256), p.lds_bytes, st, p.a);
     LDM_CHECK_LAUNCH("wgrad_kernel (tap-shared)");
     return 0;
+}
+
+template <int S, int KK, int DT>
+int launch_c1_dt(const Plan& p, hipStream_t st) {
+    auto kfn = wgrad_c1_kernel<S, KK, DT>;
+    dim3 grid(1, (p.a.M + 63) / 64, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(256), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_c1_kernel");
+    return 0;
+}
+template <int S, int KK>
+int launch_c1(const Plan& p, hipStream_t st) {
+    switch (p.a.lowp) {
+        case LDM_DT_F32: return launch_c1_dt<S, KK, 0>(p, st);
+        case LDM_DT_F16: return launch_c1_dt<S, KK, 1>(p, st);
+        default: return launch_c1_dt<S, KK, 2>(p, st);
+    }
 }
 
 template <int S, int KK, int BM, int BC>
@@ -297,6 +419,15 @@ int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, fl
     p.a.gath = gath;
     p.a.partial = partial;
     splits = p.splits;
+    if (p.BC == 1) {
+        switch (p.S * 10 + p.KK) {
+            case 13: return wg::launch_c1<1, 3>(p, st);
+            case 23: return wg::launch_c1<2, 3>(p, st);
+            case 14: return wg::launch_c1<1, 4>(p, st);
+            case 24: return wg::launch_c1<2, 4>(p, st);
+            default: return -1;
+        }
+    }
     const int key = p.S * 1000 + p.KK * 100 + (p.BM == 64 ? 10 : 0) + (p.BC == 32 ? 1 : 0);
     switch (key) {
         case 1311: return wg::launch<1, 3, 64, 32>(p, st);

@@ -9,32 +9,48 @@ the unscale + inf check and the scale update as device kernels (ldm_unscale_chec
 Reference call sites: torch.optim.Adam + torch.amp.GradScaler in LDMTrainer (train.py:156-157,
 :189-201); torch.optim.AdamW in train_autoencoder (train.py:44).
 """
+import numpy as np
 import torch
 
 from . import _lib as L
 from .ops import require_device, stream_handle
 
-CHUNK = 1 << 16   # elements per workgroup-chunk of the multi-tensor kernels
+CHUNK = 1 << 12   # elements per workgroup-chunk of the multi-tensor kernels (4 float4 per thread)
 
 
 class _SlotTable:
-    """Device table of ldm_tensor_slot {param, grad, exp_avg, exp_avg_sq, numel} + chunk map."""
+    """Device table of ldm_tensor_slot {param, grad, exp_avg, exp_avg_sq, numel} + chunk map.
 
-    def __init__(self, params, grads, m, v):
+    Tables are cached by the tensors' addresses (the same parameters, gradients and state give the same
+    table every step), and the chunk map is built with numpy, so a step costs no per-chunk host work."""
+
+    _cache = {}
+
+    def __new__(cls, params, grads, m, v):
+        key = tuple((p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(), 0 if b is None else b.data_ptr(),
+                     p.numel()) for p, g, a, b in zip(params, grads, m, v))
         dev = params[0].device
-        rows, ct, cs = [], [], []
-        for i, (p, g, a, b) in enumerate(zip(params, grads, m, v)):
-            n = p.numel()
-            rows.append([p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(),
-                         0 if b is None else b.data_ptr(), n])
-            for s in range(0, n, CHUNK):
-                ct.append(i)
-                cs.append(s)
-        self.slots = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=False)
-        self.chunk_tensor = torch.tensor(ct, dtype=torch.int32).to(dev)
-        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(dev)
-        self.nchunks = len(ct)
-        self.key = tuple(r[0] for r in rows) + tuple(r[1] for r in rows)
+        hit = cls._cache.get((dev, key))
+        if hit is not None:
+            return hit
+        self = super().__new__(cls)
+        rows = np.array(key, dtype=np.int64).reshape(-1, 5)
+        nch = (rows[:, 4] + CHUNK - 1) // CHUNK
+        ct = np.repeat(np.arange(len(rows), dtype=np.int32), nch)
+        first = np.repeat(np.cumsum(nch) - nch, nch)
+        cs = (np.arange(int(nch.sum()), dtype=np.int64) - first) * CHUNK
+        self.slots = torch.from_numpy(rows).to(dev)
+        self.chunk_tensor = torch.from_numpy(ct).to(dev)
+        self.chunk_start = torch.from_numpy(cs).to(dev)
+        self.nchunks = int(len(ct))
+        self.key = key
+        if len(cls._cache) > 64:
+            cls._cache.clear()
+        cls._cache[(dev, key)] = self
+        return self
+
+    def __init__(self, *args):
+        pass
 
 
 def scale_tensors_(tensors, factor):

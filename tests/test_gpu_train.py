@@ -47,6 +47,10 @@ CONV_CASES = {
     "vae_dec_convT_k4": (2, 32, 4, 4, 128, 4, 2, 1, 0, True, "none", False, False),
     "vae_dec_out_tanh_half": (2, 64, 16, 16, 1, 4, 2, 1, 0, True, "tanh_half", False, False),
     "batch3_nonsquare_tanh": (3, 8, 6, 10, 16, 3, 2, 1, 0, False, "tanh", False, False),
+    # Cin = 1 with Wout % 4 != 0: the one-output-per-lane kernel (the 4-column kernel needs Wout % 4 == 0)
+    "cin1_k3s2_ragged_cols": (2, 1, 18, 22, 16, 3, 2, 1, 0, False, "relu", False, False),
+    # the decoder output layer's shape class at a wider, non-square plane (4-column convT kernel, W4 = 10)
+    "vae_dec_out_wide": (2, 64, 8, 40, 1, 4, 2, 1, 0, True, "tanh_half", False, False),
 }
 
 
