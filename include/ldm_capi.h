@@ -111,6 +111,11 @@ int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW);
 int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
                         float* running_mean, float* running_var, float momentum, float eps, int32_t act,
                         float* save_mean, float* save_invstd, float* workspace, void* stream);
+/* Out-of-place form (y may equal x): statistics of x, the normalised result into y.  The autograd path
+ * uses it so that no copy of the input is made for the in-place kernel (functional.batchnorm). */
+int ldm_batchnorm_train_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
+                            const float* bias, float* running_mean, float* running_var, float momentum, float eps,
+                            int32_t act, float* save_mean, float* save_invstd, float* workspace, void* stream);
 /* The same in two stages, for SyncBatchNorm (replaces torch.nn.SyncBatchNorm's batch_norm_stats /
  * batch_norm_gather_stats_with_counts / batch_norm_elemt for the data-parallel train path):
  * stats[2c] = sum x, stats[2c+1] = sum x^2 over this rank's batch (fp64) and stats[2C] = this rank's
@@ -123,6 +128,10 @@ int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double
 int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
                         const float* weight, const float* bias, float* running_mean, float* running_var,
                         float momentum, float eps, int32_t act, float* save_mean, float* save_invstd, void* stream);
+int ldm_batchnorm_apply_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const double* stats,
+                            double count, const float* weight, const float* bias, float* running_mean,
+                            float* running_var, float momentum, float eps, int32_t act, float* save_mean,
+                            float* save_invstd, void* stream);
 
 /* ---- eval-mode BatchNorm2d (+activation) as a standalone op, out-of-place (y may equal x) ------ */
 int ldm_batchnorm_eval(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
@@ -320,20 +329,25 @@ int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float
 int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B, int32_t C,
                      int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace, void* stream);
 /* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
- * y = its output, x = its input; dx / dweight / dbias may be NULL.  workspace as ldm_batchnorm_train. */
+ * y = its output, x = its input, weight / bias its affine parameters (NULL = 1 / 0); dx / dweight / dbias
+ * may be NULL.  y may be NULL when act is NONE or RELU: the ReLU mask is then re-evaluated from x with the
+ * forward's own arithmetic (one tensor read less per pass).  workspace as ldm_batchnorm_train. */
 int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
-                           const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
-                           int32_t HW, float* dx, float* dweight, float* dbias, float* workspace, void* stream);
+                           const float* save_invstd, const float* weight, const float* bias, int32_t act, int32_t B,
+                           int32_t C, int32_t HW, float* dx, float* dweight, float* dbias, float* workspace,
+                           void* stream);
 /* The same in two stages for SyncBatchNorm: sums[2c] = sum g, sums[2c+1] = sum g*xhat over this rank
  * (g = dy*act'(y)) and sums[2C] = this rank's B*H*W (sums holds 2C+1 doubles); dbias / dweight get the
  * local sums (parameter grads stay local, as in torch.nn.SyncBatchNorm; the DP gradient all-reduce
  * averages them) -> the caller all-reduces all 2C+1 doubles -> apply (count <= 0: read sums[2C]). */
 int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
-                                  const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
-                                  double* sums, float* dweight, float* dbias, float* workspace, void* stream);
+                                  const float* save_invstd, const float* weight, const float* bias, int32_t act,
+                                  int32_t B, int32_t C, int32_t HW, double* sums, float* dweight, float* dbias,
+                                  float* workspace, void* stream);
 int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
-                                 const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
-                                 int32_t HW, const double* sums, double count, float* dx, void* stream);
+                                 const float* save_invstd, const float* weight, const float* bias, int32_t act,
+                                 int32_t B, int32_t C, int32_t HW, const double* sums, double count, float* dx,
+                                 void* stream);
 /* Backward of ldm_attention_core: dq [B,E,L], dkv [B,2E,S] (dK then dV). */
 int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv, int32_t B,
                            int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream);

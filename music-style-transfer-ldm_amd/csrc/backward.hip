@@ -90,29 +90,43 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WgradArgs a) {
 
 // sum of split partials in split order.  Tap t is the kernel-window index (kh*kw + kw), so the
 // [m][c*T + t] GEMM layout IS the torch weight layout [m][c][kh][kw].
-// 256 threads = 16 outputs x 16 split groups: group g sums its contiguous range of splits serially, the
-// 16 group sums are added in group order (a fixed partition and order: bitwise reproducible).  One thread
-// per output walking all S splits serially was latency-bound at small M*N (60 us for 1024 outputs x 256
-// splits).
+// 256 threads = (256 / G) outputs x G split groups (G = S rounded up to a power of two, at most 16): group
+// g sums its contiguous range of splits serially, the G group sums are added in group order (a fixed
+// partition and order: bitwise reproducible).  One thread per output walking all S splits serially was
+// latency-bound at small M*N (60 us for 1024 outputs x 256 splits).
+inline int wgrad_groups(int S) {
+    int G = 1;
+    while (G < S && G < 16) G *= 2;
+    return G;
+}
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial, int S, int MN,
-                                                           float* __restrict__ dw, int accumulate) {
-    __shared__ float red[16][17];
-    const int ol = threadIdx.x & 15, g = threadIdx.x >> 4;
-    const int i = blockIdx.x * 16 + ol;
-    const int G = S < 16 ? S : 16;
+                                                           float* __restrict__ dw, int accumulate, int G) {
+    __shared__ float red[256];
+    const int NO = 256 / G;
+    const int ol = threadIdx.x % NO, g = threadIdx.x / NO;
+    const int i = blockIdx.x * NO + ol;
     const int per = (S + G - 1) / G;
     float v = 0.f;
-    if (i < MN && g < G) {
+    if (i < MN) {
         const int s1 = min(S, (g + 1) * per);
         for (int s = g * per; s < s1; ++s) v = v + partial[(size_t)s * MN + i];
     }
-    red[g][ol] = v;
+    if (G == 1) {
+        if (i < MN) dw[i] = accumulate ? dw[i] + v : v;
+        return;
+    }
+    red[threadIdx.x] = v;
     __syncthreads();
     if (g == 0 && i < MN) {
-        float t = red[0][ol];
-        for (int k = 1; k < G; ++k) t = t + red[k][ol];
+        float t = red[ol];
+        for (int k = 1; k < G; ++k) t = t + red[k * NO + ol];
         dw[i] = accumulate ? dw[i] + t : t;
     }
+}
+static void wgrad_reduce(const float* partial, int S, int MN, float* dw, int accumulate, hipStream_t st) {
+    const int G = wgrad_groups(S), NO = 256 / G;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + NO - 1) / NO), dim3(256), 0, st, partial, S, MN, dw, accumulate,
+                       G);
 }
 
 // ================================================================================================
@@ -393,8 +407,7 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st);   // the tap-shared form (wgrad.hip) where it applies
     if (rc > 0) return rc;
     if (rc == 0) {
-        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 15) / 16), dim3(256), 0, st, (const float*)workspace, S2,
-                           MN, dw, accumulate);
+        wgrad_reduce((const float*)workspace, S2, MN, dw, accumulate, st);
         LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
         return 0;
     }
@@ -404,8 +417,7 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     dim3 grid((a.N + 15) / 16, (a.M + 15) / 16, S);
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(64), 0, st, a);
     LDM_CHECK_LAUNCH("wgrad_kernel");
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 15) / 16), dim3(256), 0, st, (const float*)a.partial, S, MN,
-                       dw, accumulate);
+    wgrad_reduce((const float*)a.partial, S, MN, dw, accumulate, st);
     LDM_CHECK_LAUNCH("wgrad_reduce_kernel");
     return 0;
 }

@@ -100,6 +100,19 @@ __device__ __forceinline__ void slice_for(int64_t e0, int64_t e1, int C, int c, 
     }
 }
 
+// the normalisation of the forward (and its re-evaluation for the ReLU mask in the backward): one
+// helper, so both sides compute the same bits
+__device__ __forceinline__ float bn_affine(float v, float alpha, float beta) { return v * alpha + beta; }
+
+// g * act'(output) of the BN backward: from the saved output y, or, when y is NULL (act NONE / RELU), from
+// the input x through the forward's affine map (alpha = invstd * w, beta = b - mean * alpha)
+__device__ __forceinline__ float bn_act_grad(int act, float g, const float* y, float yv, float xv, float alpha,
+                                             float beta) {
+    if (y) return g * act_grad(act, yv);
+    if (act == LDM_ACT_RELU) return bn_affine(xv, alpha, beta) > 0.f ? g : 0.f;
+    return g;
+}
+
 // ---- BatchNorm forward ---------------------------------------------------------------------------
 template <int W>
 __global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const float* __restrict__ x, int C, int HW,
@@ -148,7 +161,8 @@ __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double*
 }
 
 template <int W>
-__global__ __launch_bounds__(kThreads) void bn_apply_kernel(float* __restrict__ x, int C, int HW, int64_t n, int64_t S,
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, float* x, int C,
+                                                            int HW, int64_t n, int64_t S,
                                                             const double* __restrict__ stats, double count_arg,
                                                             const float* __restrict__ weight,
                                                             const float* __restrict__ bias, float* __restrict__ rmean,
@@ -167,9 +181,9 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(float* __restrict__ 
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float v[W];
-        ld<W>(x + o, v);
+        ld<W>(src + o, v);
 #pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = apply_act(v[j] * alpha + beta, act);
+        for (int j = 0; j < W; ++j) v[j] = apply_act(bn_affine(v[j], alpha, beta), act);
         st<W>(x + o, v);
     });
     if (k == 0 && threadIdx.x == 0) {
@@ -189,22 +203,26 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const float* _
                                                                   const float* __restrict__ y,
                                                                   const float* __restrict__ x,
                                                                   const float* __restrict__ mean,
-                                                                  const float* __restrict__ invstd, int act, int C,
+                                                                  const float* __restrict__ invstd,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias, int act, int C,
                                                                   int HW, int64_t n, int64_t S,
                                                                   double* __restrict__ part) {
     __shared__ double red[kThreads / 64];
     const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
     const float mu = mean[c], is = invstd[c];
+    const float alpha = is * (w ? w[c] : 1.0f);
+    const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     float sg = 0.f, sgx = 0.f;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float g[W], yv[W], xv[W];
+        float g[W], yv[W] = {}, xv[W];
         ld<W>(dy + o, g);
-        ld<W>(y + o, yv);
+        if (y) ld<W>(y + o, yv);
         ld<W>(x + o, xv);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            const float gj = g[j] * act_grad(act, yv[j]);
+            const float gj = bn_act_grad(act, g[j], y, yv[j], xv[j], alpha, beta);
             sg += gj;
             sgx += gj * ((xv[j] - mu) * is);
         }
@@ -223,7 +241,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __r
                                                                 const float* __restrict__ x,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ invstd,
-                                                                const float* __restrict__ w, int act, int C, int HW,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias, int act, int C, int HW,
                                                                 int64_t n, int64_t S, const double* __restrict__ sums,
                                                                 double count_arg, float* __restrict__ dx) {
     const int k = blockIdx.x, c = blockIdx.y;
@@ -231,15 +250,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __r
     const float mu = mean[c], is = invstd[c];
     const float sgN = (float)(sums[2 * c] / count), sgxN = (float)(sums[2 * c + 1] / count);
     const float kk = (w ? w[c] : 1.f) * is;
+    const float alpha = is * (w ? w[c] : 1.0f);
+    const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float g[W], yv[W], xv[W], d[W];
+        float g[W], yv[W] = {}, xv[W], d[W];
         ld<W>(dy + o, g);
-        ld<W>(y + o, yv);
+        if (y) ld<W>(y + o, yv);
         ld<W>(x + o, xv);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            const float gj = g[j] * act_grad(act, yv[j]);
+            const float gj = bn_act_grad(act, g[j], y, yv[j], xv[j], alpha, beta);
             d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
         }
         st<W>(dx + o, d);
@@ -414,42 +435,62 @@ extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t
     return 0;
 }
 
-extern "C" int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
-                                   const float* weight, const float* bias, float* running_mean, float* running_var,
-                                   float momentum, float eps, int32_t act, float* save_mean, float* save_invstd,
-                                   void* stream) {
-    LDM_REQUIRE(stats && B >= 0 && C > 0 && HW > 0 && (x || B == 0), "batchnorm_apply: bad argument");
+extern "C" int ldm_batchnorm_apply_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const double* stats,
+                                       double count, const float* weight, const float* bias, float* running_mean,
+                                       float* running_var, float momentum, float eps, int32_t act, float* save_mean,
+                                       float* save_invstd, void* stream) {
+    LDM_REQUIRE(stats && B >= 0 && C > 0 && HW > 0 && ((x && y) || B == 0), "batchnorm_apply: bad argument");
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
     const dim3 grid(P, C);
-    if (vec_ok(HW, x))
-        hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, stats,
+    if (vec_ok(HW, x, y))
+        hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
                            count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
     else
-        hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, stats,
+        hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
                            count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
     LDM_CHECK_LAUNCH("bn_apply_kernel");
     return 0;
 }
 
-extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
-                                   float* running_mean, float* running_var, float momentum, float eps, int32_t act,
-                                   float* save_mean, float* save_invstd, float* workspace, void* stream) {
-    LDM_REQUIRE(x && workspace && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
+extern "C" int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
+                                   const float* weight, const float* bias, float* running_mean, float* running_var,
+                                   float momentum, float eps, int32_t act, float* save_mean, float* save_invstd,
+                                   void* stream) {
+    return ldm_batchnorm_apply_out(x, x, B, C, HW, stats, count, weight, bias, running_mean, running_var, momentum,
+                                   eps, act, save_mean, save_invstd, stream);
+}
+
+extern "C" int ldm_batchnorm_train_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const float* weight,
+                                       const float* bias, float* running_mean, float* running_var, float momentum,
+                                       float eps, int32_t act, float* save_mean, float* save_invstd, float* workspace,
+                                       void* stream) {
+    LDM_REQUIRE(x && y && workspace && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
     const int64_t n = (int64_t)B * HW;
     double* stats = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
     int rc = ldm_batchnorm_stats(x, B, C, HW, stats, workspace, stream);
     if (rc) return rc;
-    return ldm_batchnorm_apply(x, B, C, HW, stats, (double)n, weight, bias, running_mean, running_var, momentum, eps,
-                               act, save_mean, save_invstd, stream);
+    return ldm_batchnorm_apply_out(x, y, B, C, HW, stats, (double)n, weight, bias, running_mean, running_var,
+                                   momentum, eps, act, save_mean, save_invstd, stream);
 }
 
+extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
+                                   float* running_mean, float* running_var, float momentum, float eps, int32_t act,
+                                   float* save_mean, float* save_invstd, float* workspace, void* stream) {
+    return ldm_batchnorm_train_out(x, x, B, C, HW, weight, bias, running_mean, running_var, momentum, eps, act,
+                                   save_mean, save_invstd, workspace, stream);
+}
+
+// y may be NULL when act is NONE or RELU (bn_act_grad: the mask is re-evaluated from x)
+static bool bn_need_y(int act) { return act != LDM_ACT_NONE && act != LDM_ACT_RELU; }
+
 extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
-                                             const float* save_invstd, int32_t act, int32_t B, int32_t C, int32_t HW,
-                                             double* sums, float* dweight, float* dbias, float* workspace,
-                                             void* stream) {
-    LDM_REQUIRE(save_mean && save_invstd && sums && workspace && B >= 0 && C > 0 && HW > 0 && ((dy && y && x) || B == 0),
+                                             const float* save_invstd, const float* weight, const float* bias,
+                                             int32_t act, int32_t B, int32_t C, int32_t HW, double* sums,
+                                             float* dweight, float* dbias, float* workspace, void* stream) {
+    LDM_REQUIRE(save_mean && save_invstd && sums && workspace && B >= 0 && C > 0 && HW > 0 &&
+                    ((dy && x && (y || !bn_need_y(act))) || B == 0),
                 "bn_backward_reduce: bad argument");
     LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward_reduce: workspace must be 8-byte aligned");
     const int64_t n = (int64_t)B * HW;
@@ -459,10 +500,10 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
     const dim3 grid(P, C);
     if (vec_ok(HW, dy, y, x))
         hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, act, C, HW, n, S, part);
+                           save_invstd, weight, bias, act, C, HW, n, S, part);
     else
         hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, act, C, HW, n, S, part);
+                           save_invstd, weight, bias, act, C, HW, n, S, part);
     LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
     // local sums: db = sum g, dw = sum g*xhat (SyncBatchNorm keeps the parameter grads local)
     hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
@@ -472,10 +513,11 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
 }
 
 extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
-                                            const float* save_invstd, const float* weight, int32_t act, int32_t B,
-                                            int32_t C, int32_t HW, const double* sums, double count, float* dx,
-                                            void* stream) {
-    LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 && ((dy && y && x && dx) || B == 0),
+                                            const float* save_invstd, const float* weight, const float* bias,
+                                            int32_t act, int32_t B, int32_t C, int32_t HW, const double* sums,
+                                            double count, float* dx, void* stream) {
+    LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 &&
+                    ((dy && x && dx && (y || !bn_need_y(act))) || B == 0),
                 "bn_backward_apply: bad argument");
     if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
@@ -484,26 +526,26 @@ extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, con
     const dim3 grid(P, C);
     if (vec_ok(HW, dy, y, x, dx))
         hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, act, C, HW, n, S, sums, count, dx);
+                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx);
     else
         hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, act, C, HW, n, S, sums, count, dx);
+                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx);
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
     return 0;
 }
 
 extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
-                                      const float* save_invstd, const float* weight, int32_t act, int32_t B, int32_t C,
-                                      int32_t HW, float* dx, float* dweight, float* dbias, float* workspace,
-                                      void* stream) {
+                                      const float* save_invstd, const float* weight, const float* bias, int32_t act,
+                                      int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
+                                      float* workspace, void* stream) {
     LDM_REQUIRE(workspace && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
     const int64_t n = (int64_t)B * HW;
     double* sums = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
-    int rc = ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, act, B, C, HW, sums, dweight, dbias,
-                                           workspace, stream);
+    int rc = ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums,
+                                           dweight, dbias, workspace, stream);
     if (rc || !dx) return rc;
-    return ldm_batchnorm_backward_apply(dy, y, x, save_mean, save_invstd, weight, act, B, C, HW, sums, (double)n, dx,
-                                        stream);
+    return ldm_batchnorm_backward_apply(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums, (double)n,
+                                        dx, stream);
 }
 
 extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,

@@ -88,6 +88,10 @@ SIGNATURES = {
     "ldm_ustep_conv": (c_int32, [c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
                                       c_int32, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_train_out": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float,
+                                          c_float, c_int32, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_apply_out": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_vp, ctypes.c_double, c_fp, c_fp,
+                                          c_fp, c_fp, c_float, c_float, c_int32, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_stats": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),
     "ldm_batchnorm_apply": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, ctypes.c_double, c_fp, c_fp, c_fp, c_fp,
                                       c_float, c_float, c_int32, c_fp, c_fp, c_vp]),
@@ -122,12 +126,12 @@ SIGNATURES = {
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),
-    "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
-                                         c_fp, c_fp, c_fp, c_fp, c_vp]),
-    "ldm_batchnorm_backward_reduce": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
-                                                c_vp, c_fp, c_fp, c_fp, c_vp]),
-    "ldm_batchnorm_backward_apply": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32,
-                                               c_vp, ctypes.c_double, c_fp, c_vp]),
+    "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
+                                         c_int32, c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward_reduce": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
+                                                c_int32, c_vp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward_apply": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
+                                               c_int32, c_vp, ctypes.c_double, c_fp, c_vp]),
     "ldm_attention_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          c_float, c_vp]),
     "ldm_unscale_check": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, c_fp, c_vp, c_vp]),

@@ -193,9 +193,10 @@ def batchnorm(x, bn_module, act="none"):
     sync = sync_group_for(m) if m.training else False
 
     def fwd_train(store, x_, w_, b_):
-        y = ops.f32c(x_).clone()
-        sm, si = ops.batchnorm_train_(y, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
-                                      act, save=True, sync=sync)
+        xc = ops.f32c(x_)
+        y = torch.empty_like(xc)
+        sm, si = ops.batchnorm_train_(xc, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
+                                      act, save=True, sync=sync, out=y)
         store["saved"] = (x_, w_, b_, sm, si, y)
         store["act"] = act
         store["sync"] = sync
@@ -210,7 +211,7 @@ def _bn_train_backward(ctx, gy):
     nx, nw, nb = ctx.needs_input_grad[3:6]
     dx, dw, db = ops.batchnorm_backward(gy, y, x, sm, si, w, ctx.store["act"], need_dx=nx,
                                         need_w=nw and w is not None, need_b=nb and b is not None,
-                                        sync=ctx.store.get("sync", False))
+                                        sync=ctx.store.get("sync", False), bias=b)
     return dx, dw, db
 
 

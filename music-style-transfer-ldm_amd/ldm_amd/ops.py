@@ -316,10 +316,11 @@ def _allreduce_sum(t, group):
 
 
 def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True,
-                       sync=False):
+                       sync=False, bias=None):
     """Train-mode BN backward.  sync: SyncBatchNorm over the default group (True) or a given group.  The
     per-rank sums and the per-rank element count travel in ONE fp64 all-reduce of 2C+1 values; the apply
-    stage reads the global count on the device (reduce.hip), so there is no host synchronisation."""
+    stage reads the global count on the device (reduce.hip), so there is no host synchronisation.  For act
+    none / relu the output y is not read (the ReLU mask is re-evaluated from x, weight and bias)."""
     dy = f32c(dy)
     B, C = dy.shape[0], dy.shape[1]
     HW = max(1, math.prod(dy.shape[2:]))
@@ -327,24 +328,26 @@ def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=Tr
     dw = torch.empty(C, device=dy.device, dtype=torch.float32) if need_w else None
     db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_b else None
     ws = reduce_workspace(B, C, HW, dy.device)
+    if act in ("none", "relu"):
+        y = None
     pg = _sync_group(sync)
+    x = f32c(x)
     if pg is None:
-        L.call("ldm_batchnorm_backward", dy.data_ptr(), y.data_ptr(), f32c(x).data_ptr(), save_mean.data_ptr(),
-               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db), ws.data_ptr(),
-               stream_handle())
+        L.call("ldm_batchnorm_backward", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
+               save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db),
+               ws.data_ptr(), stream_handle())
         return dx, dw, db
     # SyncBatchNorm: local sums (+ local count) -> all-reduce -> dx with the global count (parameter
     # grads stay local, as in torch.nn.SyncBatchNorm)
     sums = torch.empty(2 * C + 1, device=dy.device, dtype=torch.float64)
-    x = f32c(x)
     L.call("ldm_batchnorm_backward_reduce", _p(dy if B else None), _p(y if B else None), _p(x if B else None),
-           save_mean.data_ptr(), save_invstd.data_ptr(), L.ACT[act], B, C, HW, sums.data_ptr(), _p(dw), _p(db),
-           ws.data_ptr(), stream_handle())
+           save_mean.data_ptr(), save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW,
+           sums.data_ptr(), _p(dw), _p(db), ws.data_ptr(), stream_handle())
     _allreduce_sum(sums, pg.pg)
     if dx is not None and B:
-        L.call("ldm_batchnorm_backward_apply", dy.data_ptr(), y.data_ptr(), x.data_ptr(), save_mean.data_ptr(),
-               save_invstd.data_ptr(), _p(weight), L.ACT[act], B, C, HW, sums.data_ptr(), -1.0, dx.data_ptr(),
-               stream_handle())
+        L.call("ldm_batchnorm_backward_apply", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
+               save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW, sums.data_ptr(), -1.0,
+               dx.data_ptr(), stream_handle())
     return dx, dw, db
 
 
@@ -360,10 +363,14 @@ def attention_backward(q, kv, dout, heads):
     return dq, dkv
 
 
-def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False, sync=False):
-    """In-place train-mode BatchNorm2d (+activation); updates running stats like nn.BatchNorm2d."""
+def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, act="none", save=False, sync=False,
+                     out=None):
+    """Train-mode BatchNorm2d (+activation), in place on x, or from x into `out` when given; updates running
+    stats like nn.BatchNorm2d."""
     require_device(x, weight, bias, running_mean, running_var)
     assert x.is_contiguous() and x.dtype == torch.float32
+    y = x if out is None else out
+    assert y.is_contiguous() and y.shape == x.shape and y.dtype == torch.float32
     B, C, H, W = x.shape
     sm = si = None
     if save:
@@ -372,9 +379,9 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
     ws = reduce_workspace(B, C, H * W, x.device)
     pg = _sync_group(sync)
     if pg is None:
-        L.call("ldm_batchnorm_train", x.data_ptr(), B, C, H * W, _p(weight), _p(bias), _p(running_mean),
-               _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si), ws.data_ptr(),
-               stream_handle())
+        L.call("ldm_batchnorm_train_out", x.data_ptr(), y.data_ptr(), B, C, H * W, _p(weight), _p(bias),
+               _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
+               ws.data_ptr(), stream_handle())
     else:
         # SyncBatchNorm (torch.nn.SyncBatchNorm semantics): fp64 (sum x, sum x^2, count) all-reduced over the
         # group in one collective, normalised with the global batch statistics (the global count is read on
@@ -382,9 +389,10 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
         # joins the collective with zero sums and updates its running statistics like every other rank.
         stats = torch.empty(2 * C + 1, device=x.device, dtype=torch.float64)
         xp = x.data_ptr() if B else None
+        yp = y.data_ptr() if B else None
         L.call("ldm_batchnorm_stats", xp, B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
         _allreduce_sum(stats, pg.pg)
-        L.call("ldm_batchnorm_apply", xp, B, C, H * W, stats.data_ptr(), -1.0, _p(weight), _p(bias),
+        L.call("ldm_batchnorm_apply_out", xp, yp, B, C, H * W, stats.data_ptr(), -1.0, _p(weight), _p(bias),
                _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
                stream_handle())
     return (sm, si) if save else None

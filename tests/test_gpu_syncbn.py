@@ -37,7 +37,9 @@ def _rand(shape, seed, lo=-1.0, hi=1.0):
 
 @pytest.mark.parametrize("shape", [(4, 64, 8, 8), (4, 8, 36, 36), (6, 4, 30, 31), (2, 16, 3, 5)])
 @pytest.mark.parametrize("act", ["none", "relu"])
-def test_two_stage_bn_equals_single_call(cuda, shape, act):
+@pytest.mark.parametrize("pass_y", [True, False])
+def test_two_stage_bn_equals_single_call(cuda, shape, act, pass_y):
+    """pass_y False: the backward re-evaluates the ReLU mask from x, weight and bias (no output read)."""
     from ldm_amd import _lib as L, ops
     B, C, H, W = shape
     HW = H * W
@@ -57,6 +59,13 @@ def test_two_stage_bn_equals_single_call(cuda, shape, act):
     ws = ops.reduce_workspace(B, C, HW, cuda)
     L.call("ldm_batchnorm_train", x1.data_ptr(), B, C, HW, gd.data_ptr(), bd.data_ptr(), rm1.data_ptr(), rv1.data_ptr(),
            0.1, 1e-5, A, sm1.data_ptr(), si1.data_ptr(), ws.data_ptr(), st)
+    # out-of-place form: the same bits, input untouched
+    xo, yo = x.clone().to(cuda), torch.empty((B, C, H, W), device=cuda)
+    rmo, rvo = rm0.clone().to(cuda), rv0.clone().to(cuda)
+    L.call("ldm_batchnorm_train_out", xo.data_ptr(), yo.data_ptr(), B, C, HW, gd.data_ptr(), bd.data_ptr(),
+           rmo.data_ptr(), rvo.data_ptr(), 0.1, 1e-5, A, None, None, ops.reduce_workspace(B, C, HW, cuda).data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(yo, x1) and torch.equal(xo.cpu(), x) and torch.equal(rmo, rm1) and torch.equal(rvo, rv1)
     # --- two halves: stats per half, summed (what the all-reduce does), apply with the device count
     h = B // 2
     halves = [x[:h].clone().to(cuda), x[h:].clone().to(cuda)]
@@ -99,17 +108,19 @@ def test_two_stage_bn_equals_single_call(cuda, shape, act):
     dyd = dy.to(cuda)
     xin = x.to(cuda)
     dx1, dw1, db1 = torch.empty_like(xin), torch.empty(C, device=cuda), torch.empty(C, device=cuda)
-    L.call("ldm_batchnorm_backward", dyd.data_ptr(), x1.data_ptr(), xin.data_ptr(), sm1.data_ptr(), si1.data_ptr(),
-           gd.data_ptr(), A, B, C, HW, dx1.data_ptr(), dw1.data_ptr(), db1.data_ptr(), ws.data_ptr(), st)
+    L.call("ldm_batchnorm_backward", dyd.data_ptr(), x1.data_ptr() if pass_y else None, xin.data_ptr(), sm1.data_ptr(),
+           si1.data_ptr(), gd.data_ptr(), bd.data_ptr(), A, B, C, HW, dx1.data_ptr(), dw1.data_ptr(), db1.data_ptr(),
+           ws.data_ptr(), st)
     sums, parts = [], []
     for i, sl in enumerate((slice(0, h), slice(h, B))):
         s = torch.empty(2 * C + 1, device=cuda, dtype=torch.float64)
         dwh, dbh = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
         n = sl.stop - sl.start
         wsh = ops.reduce_workspace(n, C, HW, cuda).clone()
-        L.call("ldm_batchnorm_backward_reduce", dyd[sl].contiguous().data_ptr(), outs[i].data_ptr(),
-               xin[sl].contiguous().data_ptr(), rms[i][2].data_ptr(), rms[i][3].data_ptr(), A, n, C, HW, s.data_ptr(),
-               dwh.data_ptr(), dbh.data_ptr(), wsh.data_ptr(), st)
+        L.call("ldm_batchnorm_backward_reduce", dyd[sl].contiguous().data_ptr(),
+               outs[i].data_ptr() if pass_y else None, xin[sl].contiguous().data_ptr(), rms[i][2].data_ptr(),
+               rms[i][3].data_ptr(), gd.data_ptr(), bd.data_ptr(), A, n, C, HW, s.data_ptr(), dwh.data_ptr(),
+               dbh.data_ptr(), wsh.data_ptr(), st)
         torch.cuda.synchronize()
         sums.append(s)
         parts.append((dwh, dbh))
@@ -119,9 +130,10 @@ def test_two_stage_bn_equals_single_call(cuda, shape, act):
     for i, sl in enumerate((slice(0, h), slice(h, B))):
         n = sl.stop - sl.start
         dxh = torch.empty((n, C, H, W), device=cuda)
-        L.call("ldm_batchnorm_backward_apply", dyd[sl].contiguous().data_ptr(), outs[i].data_ptr(),
-               xin[sl].contiguous().data_ptr(), rms[i][2].data_ptr(), rms[i][3].data_ptr(), gd.data_ptr(), A, n, C, HW,
-               tot_b.data_ptr(), -1.0, dxh.data_ptr(), st)
+        L.call("ldm_batchnorm_backward_apply", dyd[sl].contiguous().data_ptr(),
+               outs[i].data_ptr() if pass_y else None, xin[sl].contiguous().data_ptr(), rms[i][2].data_ptr(),
+               rms[i][3].data_ptr(), gd.data_ptr(), bd.data_ptr(), A, n, C, HW, tot_b.data_ptr(), -1.0,
+               dxh.data_ptr(), st)
         dxs.append(dxh)
     torch.cuda.synchronize()
     dx2 = torch.cat(dxs, 0)
