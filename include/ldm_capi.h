@@ -352,6 +352,21 @@ int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x
 int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv, int32_t B,
                            int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream);
 
+/* ---- VGGish feature / style loss (loss.py:52-101, VGGishFeatureLoss.forward) ----
+ * The conv stack runs on ldm_conv_forward (ReLU fused: each conv launch yields one feature tap).
+ * ldm_maxpool2x2: nn.MaxPool2d(2, 2) on NCHW fp32 (floor mode, NaN-propagating), y [B,C,H/2,W/2].
+ * ldm_std_mse_moments: per sample b of p, t [B][n] (n = C*H*W contiguous): moments[b][0..4] = sum p,
+ *   sum p^2, sum t, sum t^2, sum p*t (fp64, fixed slices and order; workspace
+ *   ldm_std_mse_workspace_floats(B, n) floats, 8-byte aligned).
+ * ldm_std_mse_accumulate: *acc += scale * mse(p / (std(p) + eps), t / (std(t) + eps)) from the moments
+ *   (torch.std per sample over dims 1..3, unbiased), and *out = (float)*acc when out is not NULL. */
+int ldm_maxpool2x2(const float* x, float* y, int32_t B, int32_t C, int32_t H, int32_t W, void* stream);
+int64_t ldm_std_mse_workspace_floats(int32_t B, int64_t n);
+int ldm_std_mse_moments(const float* p, const float* t, int32_t B, int64_t n, double* moments, float* workspace,
+                        void* stream);
+int ldm_std_mse_accumulate(const double* moments, int32_t B, int64_t n, double eps, double scale, double* acc,
+                           float* out, void* stream);
+
 /* ---- optimiser: torch.optim.Adam (train.py:156) + torch.amp.GradScaler (train.py:157,189-201) ----
  * Multi-tensor: `slots` (device array) lists the parameters; the work is cut into chunks of
  * chunk_len elements, chunk i covering slots[chunk_tensor[i]] from element chunk_start[i]. */

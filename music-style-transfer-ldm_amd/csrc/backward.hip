@@ -90,13 +90,14 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WgradArgs a) {
 
 // sum of split partials in split order.  Tap t is the kernel-window index (kh*kw + kw), so the
 // [m][c*T + t] GEMM layout IS the torch weight layout [m][c][kh][kw].
-// 256 threads = (256 / G) outputs x G split groups (G = S rounded up to a power of two, at most 16): group
-// g sums its contiguous range of splits serially, the G group sums are added in group order (a fixed
-// partition and order: bitwise reproducible).  One thread per output walking all S splits serially was
-// latency-bound at small M*N (60 us for 1024 outputs x 256 splits).
-inline int wgrad_groups(int S) {
+// 256 threads = (256 / G) outputs x G split groups: group g sums its contiguous range of splits serially,
+// then the G group sums meet in a pairwise tree in LDS (a fixed partition and order: bitwise
+// reproducible).  G grows as M*N shrinks, so that ~2^18 threads share the S*M*N partial reads: one thread
+// per output walking all S splits serially was latency-bound at small M*N (60 us for 1024 outputs x 256
+// splits), while at large M*N that form (G = 1) streams whole 256-B rows per wave.
+inline int wgrad_groups(int S, int MN) {
     int G = 1;
-    while (G < S && G < 16) G *= 2;
+    while (G < S && G < 256 && (int64_t)MN * G < (1 << 18)) G *= 2;
     return G;
 }
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial, int S, int MN,
@@ -111,20 +112,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
         const int s1 = min(S, (g + 1) * per);
         for (int s = g * per; s < s1; ++s) v = v + partial[(size_t)s * MN + i];
     }
-    if (G == 1) {
-        if (i < MN) dw[i] = accumulate ? dw[i] + v : v;
-        return;
+    if (G > 1) {
+        red[threadIdx.x] = v;
+        for (int st = G / 2; st >= 1; st /= 2) {
+            __syncthreads();
+            if (g < st) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + st * NO];
+        }
+        __syncthreads();
+        v = red[ol];
     }
-    red[threadIdx.x] = v;
-    __syncthreads();
-    if (g == 0 && i < MN) {
-        float t = red[ol];
-        for (int k = 1; k < G; ++k) t = t + red[k * NO + ol];
-        dw[i] = accumulate ? dw[i] + t : t;
-    }
+    if (g == 0 && i < MN) dw[i] = accumulate ? dw[i] + v : v;
 }
 static void wgrad_reduce(const float* partial, int S, int MN, float* dw, int accumulate, hipStream_t st) {
-    const int G = wgrad_groups(S), NO = 256 / G;
+    const int G = wgrad_groups(S, MN), NO = 256 / G;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + NO - 1) / NO), dim3(256), 0, st, partial, S, MN, dw, accumulate,
                        G);
 }

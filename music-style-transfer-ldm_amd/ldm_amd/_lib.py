@@ -92,6 +92,10 @@ SIGNATURES = {
                                           c_float, c_int32, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_apply_out": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_vp, ctypes.c_double, c_fp, c_fp,
                                           c_fp, c_fp, c_float, c_float, c_int32, c_fp, c_fp, c_vp]),
+    "ldm_maxpool2x2": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_vp]),
+    "ldm_std_mse_workspace_floats": (c_int64, [c_int32, c_int64]),
+    "ldm_std_mse_moments": (c_int32, [c_fp, c_fp, c_int32, c_int64, c_vp, c_fp, c_vp]),
+    "ldm_std_mse_accumulate": (c_int32, [c_vp, c_int32, c_int64, ctypes.c_double, ctypes.c_double, c_vp, c_fp, c_vp]),
     "ldm_batchnorm_stats": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),
     "ldm_batchnorm_apply": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_vp, ctypes.c_double, c_fp, c_fp, c_fp, c_fp,
                                       c_float, c_float, c_int32, c_fp, c_fp, c_vp]),

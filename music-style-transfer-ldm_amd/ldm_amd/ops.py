@@ -593,3 +593,31 @@ def u8_to_unit(u8):
     out = torch.empty(u8.shape, device=u8.device, dtype=torch.float32)
     L.call("ldm_u8_to_unit", u8.data_ptr(), out.data_ptr(), u8.numel(), stream_handle())
     return out
+
+
+# ---- VGGish feature / style loss pieces (features.hip; reference loss.py:52-101) ---------------------------
+def maxpool2x2(x):
+    """nn.MaxPool2d(kernel_size=2, stride=2) on NCHW fp32 (floor mode)."""
+    require_device(x, what="maxpool2x2")
+    x = f32c(x)
+    B, C, H, W = x.shape
+    y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=torch.float32)
+    L.call("ldm_maxpool2x2", x.data_ptr(), y.data_ptr(), B, C, H, W, stream_handle())
+    return y
+
+
+def std_mse_accumulate(p, t, acc, scale, eps=1e-8, out=None):
+    """acc (fp64 [1], device) += scale * mse(p / (std(p) + eps), t / (std(t) + eps)), std per sample over
+    dims 1.. (unbiased, torch.std(dim=[1,2,3])); out (fp32 0-dim, optional) = acc.  One pass over p, t."""
+    require_device(p, t, what="std_mse")
+    p, t = f32c(p), f32c(t)
+    if p.shape != t.shape:
+        raise RuntimeError(f"std_mse: shape mismatch {tuple(p.shape)} vs {tuple(t.shape)}")
+    B = p.shape[0]
+    n = p.numel() // B
+    mom = torch.empty((B, 5), device=p.device, dtype=torch.float64)
+    ws = scratch("std_mse", L.load().ldm_std_mse_workspace_floats(B, n), p.device)
+    L.call("ldm_std_mse_moments", p.data_ptr(), t.data_ptr(), B, n, mom.data_ptr(), ws.data_ptr(), stream_handle())
+    L.call("ldm_std_mse_accumulate", mom.data_ptr(), B, n, float(eps), float(scale), acc.data_ptr(), _p(out),
+           stream_handle())
+    return mom

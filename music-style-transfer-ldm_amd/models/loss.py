@@ -7,10 +7,12 @@ reference (loss.py:10, :56).  Both are pluggable here:
 
   * set_perceptual_backend(fn)   fn(original, reconstructed) -> scalar tensor (e.g. an LPIPS model
                                  loaded from local weights).  Unset: the term is 0 (warned once).
-  * VGGishFeatureLoss(features)  takes a user-supplied VGGish `features` nn.Sequential; without one
-                                 the style term is a zero constant.  In the reference it is computed
-                                 under torch.no_grad() (loss.py:78), so it never changes an update —
-                                 only the reported loss value.
+  * VGGishFeatureLoss(features)  takes a VGGish `features` nn.Sequential (vggish_features() with
+                                 local weights) and computes the loss on the HIP kernels (conv +
+                                 fused ReLU taps, ldm_maxpool2x2, one-pass std-normalised MSE);
+                                 without one the style term is a zero constant.  In the reference it
+                                 is computed under torch.no_grad() (loss.py:78), so it never changes
+                                 an update — only the reported loss value.
 """
 import warnings
 
@@ -80,12 +82,33 @@ def diffusion_loss(noise_pred, noise_target):
     return HF.mse_loss(noise_pred, noise_target)
 
 
+def vggish_features():
+    """The VGGish `features` stack (torchvggish VGG.features: 3x3 convs 64-M-128-M-256-256-M-512-512-M, each
+    conv followed by ReLU, M = MaxPool2d(2, 2)), randomly initialised: load local weights into it
+    (state_dict keys '0.weight', '0.bias', '3.weight', ...) and pass it to VGGishFeatureLoss."""
+    layers, cin = [], 1
+    for v in (64, "M", 128, "M", 256, 256, "M", 512, 512, "M"):
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+        else:
+            layers += [nn.Conv2d(cin, v, kernel_size=3, padding=1), nn.ReLU(inplace=True)]
+            cin = v
+    return nn.Sequential(*layers)
+
+
 class VGGishFeatureLoss(nn.Module):
     """Std-normalised multi-tap feature MSE of a frozen VGGish conv stack (reference loss.py:52-101).
 
-    `features`: the VGGish `features` nn.Sequential with weights loaded from a local file.  The
-    reference fetches it with torch.hub (remote), which this offline build never does; without it the
-    loss is a zero constant (see module docstring)."""
+    `features`: the VGGish `features` nn.Sequential (vggish_features() + local weights).  The reference
+    fetches it with torch.hub (remote), which this offline build never does; without it the loss is a zero
+    constant (see module docstring).
+
+    With features, forward runs on the HIP kernels (no_grad, as the reference's loss.py:78): predicted and
+    target go through the stack as ONE batch (each Conv2d + ReLU pair is one conv launch with the ReLU
+    fused, MaxPool2d(2, 2) is ldm_maxpool2x2), and each ReLU tap's std-normalised MSE comes from one moment
+    pass (ldm_std_mse_moments / _accumulate: the normalised copies are never materialised).  Convs run at
+    the caller's autocast precision, like the reference's (the style loss sits inside train.py:174's
+    autocast region)."""
 
     def __init__(self, features=None):
         super().__init__()
@@ -100,20 +123,47 @@ class VGGishFeatureLoss(nn.Module):
             _warn_once("vggish", "VGGishFeatureLoss: no VGGish weights (remote torch.hub in the reference); "
                                  "style loss is 0 (it is gradient-free in the reference, loss.py:78).")
             return torch.zeros((), device=predicted.device, dtype=torch.float32)
-        pred_feats, targ_feats = [], []
+        from ldm_amd import ops
+        layers = list(self.features)
+        ntaps = sum(isinstance(m, nn.ReLU) for m in layers)
+        if ntaps == 0:
+            raise RuntimeError("VGGishFeatureLoss: the feature stack has no ReLU taps")
+        ops.require_device(predicted, target, what="VGGishFeatureLoss")
+        B = predicted.shape[0]
+        dev = predicted.device
+        acc = torch.zeros(1, device=dev, dtype=torch.float64)
+        out = torch.empty((), device=dev, dtype=torch.float32)
         with torch.no_grad():
-            xp, xt = predicted, target
-            for layer in self.features:
-                xp, xt = layer(xp), layer(xt)
-                if isinstance(layer, nn.ReLU):
-                    pred_feats.append(xp)
-                    targ_feats.append(xt)
-        total = 0
-        for p, t in zip(pred_feats, targ_feats):
-            p = p / (torch.std(p, dim=[1, 2, 3], keepdim=True) + 1e-8)
-            t = t / (torch.std(t, dim=[1, 2, 3], keepdim=True) + 1e-8)
-            total = total + HF.mse_loss(p, t)
-        return total / len(pred_feats)
+            x = torch.cat([ops.f32c(predicted), ops.f32c(target)], 0)
+            i = 0
+            while i < len(layers):
+                m = layers[i]
+                if isinstance(m, nn.Conv2d):
+                    if (m.groups != 1 or m.dilation != (1, 1) or m.stride[0] != m.stride[1]
+                            or m.padding[0] != m.padding[1] or m.padding_mode != "zeros"):
+                        raise NotImplementedError(f"VGGishFeatureLoss: unsupported conv {m}")
+                    relu = i + 1 < len(layers) and isinstance(layers[i + 1], nn.ReLU)
+                    x = ops.conv_forward(x, m.weight, m.bias, stride=m.stride[0], padding=m.padding[0],
+                                         act="relu" if relu else "none")
+                    i += 2 if relu else 1
+                    if not relu:
+                        continue
+                elif isinstance(m, nn.ReLU):
+                    x = ops.activation(x, "relu")
+                    i += 1
+                elif isinstance(m, nn.MaxPool2d):
+                    k, s_ = m.kernel_size, m.stride
+                    if (k not in (2, (2, 2)) or s_ not in (2, (2, 2)) or m.padding not in (0, (0, 0))
+                            or m.ceil_mode or m.dilation not in (1, (1, 1))):
+                        raise NotImplementedError(f"VGGishFeatureLoss: unsupported pooling {m}")
+                    x = ops.maxpool2x2(x)
+                    i += 1
+                    continue
+                else:
+                    raise NotImplementedError(f"VGGishFeatureLoss: unsupported layer {type(m).__name__}")
+                # a ReLU tap: std-normalised MSE of the predicted half against the target half
+                ops.std_mse_accumulate(x[:B], x[B:], acc, 1.0 / ntaps, eps=1e-8, out=out)
+        return out
 
 
 def style_loss(reconstructed, style_spec, feature_loss_net):

@@ -180,3 +180,32 @@ def ldm_forward(sd, x, style, t, noise, alpha_bar, train_decoder=False, train_en
 
 def kl_loss(z):
     return torch.mean(0.5 * (z.pow(2) - 1 - torch.log(z.pow(2) + 1e-8)))
+
+
+VGGISH_CFG = (64, "M", 128, "M", 256, 256, "M", 512, 512, "M")
+
+
+def vggish_feature_loss(sd, predicted, target, cfg=VGGISH_CFG):
+    """VGGishFeatureLoss.forward (reference loss.py:64-101) over a VGGish-shaped stack whose state dict `sd`
+    uses the nn.Sequential keys '<index>.weight' / '<index>.bias': every 3x3 conv (padding 1) is followed by
+    a ReLU whose output is a tap, 'M' is max_pool2d(2, 2); per tap the per-sample unbiased std over dims
+    1..3 normalises both sides (+1e-8), the tap loss is their MSE, the result the mean over taps."""
+    xp, xt = predicted, target
+    taps, i = [], 0
+    for v in cfg:
+        if v == "M":
+            xp, xt = F.max_pool2d(xp, 2, 2), F.max_pool2d(xt, 2, 2)
+            i += 1
+            continue
+        w, b = sd[f"{i}.weight"], sd[f"{i}.bias"]
+        xp = torch.relu(F.conv2d(xp, w, b, padding=1))
+        xt = torch.relu(F.conv2d(xt, w, b, padding=1))
+        taps.append((xp, xt))
+        i += 2
+    total = 0
+    for p_, t_ in taps:
+        p_ = p_ / (torch.std(p_, dim=[1, 2, 3], keepdim=True) + 1e-8)
+        t_ = t_ / (torch.std(t_, dim=[1, 2, 3], keepdim=True) + 1e-8)
+        total = total + F.mse_loss(p_, t_)
+    return total / len(taps)
+

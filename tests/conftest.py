@@ -27,6 +27,15 @@ def goldens2():
     return np.load(os.path.join(ROOT, "tests", "golden", "ref_goldens_r2.npz"))
 
 
+@pytest.fixture(scope="session")
+def goldens_vgg():
+    """VGGishFeatureLoss.forward of the reference on recipe-filled VGGish-shaped stacks (make_goldens.py --vggish)."""
+    return np.load(os.path.join(ROOT, "tests", "golden", "ref_goldens_vggish.npz"))
+
+
+VGG_CASES = {"a": ((2, 1, 32, 64), 800), "odd": ((2, 1, 20, 36), 810)}   # as make_goldens.VGG_CASES
+
+
 AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.encoder.4.bias", "encoder.encoder.6.bias",
            "encoder.encoder.7.weight", "decoder.decoder.0.weight", "decoder.decoder.1.bias", "decoder.decoder.4.weight",
            "decoder.decoder.6.weight", "decoder.decoder.6.bias")

@@ -3,6 +3,7 @@
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py          # ref_goldens.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r2     # ref_goldens_r2.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp    # ref_goldens_amp.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --vggish # ref_goldens_vggish.npz
 
 Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
 stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
@@ -335,6 +336,45 @@ def amp():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
 
 
+def vggish_stack():
+    """A VGGish-shaped `features` stack (3x3 convs 64-M-128-M-256-256-M-512-512-M, ReLU after each conv,
+    MaxPool2d(2, 2)): the architecture torchvggish's VGG.features is built from; the weights are the
+    recipe's (the real ones are a remote download, loss.py:56)."""
+    layers, cin = [], 1
+    for v in (64, "M", 128, "M", 256, 256, "M", 512, 512, "M"):
+        if v == "M":
+            layers.append(torch.nn.MaxPool2d(kernel_size=2, stride=2))
+        else:
+            layers += [torch.nn.Conv2d(cin, v, kernel_size=3, padding=1), torch.nn.ReLU(inplace=True)]
+            cin = v
+    return torch.nn.Sequential(*layers)
+
+
+VGG_CASES = {"a": ((2, 1, 32, 64), 800), "odd": ((2, 1, 20, 36), 810)}
+
+
+def vggish():
+    """(10) VGGishFeatureLoss.forward (loss.py:64-101) -> tests/golden/ref_goldens_vggish.npz: the REFERENCE
+    class, instantiated without its constructor (a remote torch.hub fetch, loss.py:56) and given a recipe-
+    filled VGGish-shaped stack; inputs U[0,1) like spectrograms.  Case 'odd' exercises floor-mode pooling."""
+    torch.set_num_threads(8)
+    _, L = import_reference()
+    G = {}
+    for name, (shape, seed) in VGG_CASES.items():
+        feats = vggish_stack()
+        recipe.fill_module(feats, seed=seed)
+        feats.eval()
+        obj = L.VGGishFeatureLoss.__new__(L.VGGishFeatureLoss)
+        torch.nn.Module.__init__(obj)
+        obj.features = feats
+        pred = torch.from_numpy(recipe.uniform01(shape, seed + 1))
+        targ = torch.from_numpy(recipe.uniform01(shape, seed + 2))
+        G[f"vgg_{name}_loss"] = np32(obj(pred, targ))
+    path = os.path.join(HERE, "ref_goldens_vggish.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays", {k: float(v) for k, v in G.items()})
+
+
 TRAIN_GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
                    "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
                    "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
@@ -350,5 +390,7 @@ if __name__ == "__main__":
         round2()
     elif "--amp" in sys.argv:
         amp()
+    elif "--vggish" in sys.argv:
+        vggish()
     else:
         main()

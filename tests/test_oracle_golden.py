@@ -223,3 +223,18 @@ def test_autoencoder_step(M, goldens2):
         assert rel_err(sd[k].detach().numpy(), goldens2["ae_adamw1_" + k]) < 1e-6, k
     assert rel_err(state["encoder.encoder.4.running_mean"].numpy(), goldens2["ae_enc_rm4"]) < 2e-6
     assert rel_err(state["decoder.decoder.1.running_var"].numpy(), goldens2["ae_dec_rv1"]) < 2e-6
+
+
+@pytest.mark.parametrize("case", ["a", "odd"])
+def test_vggish_feature_loss(goldens_vgg, case):
+    """oracle restatement of VGGishFeatureLoss.forward (loss.py:64-101) vs the reference's own forward on
+    the same recipe-filled VGGish-shaped stack (fp32 CPU both: 2e-6)."""
+    from conftest import VGG_CASES
+    from models.loss import vggish_features
+    shape, seed = VGG_CASES[case]
+    sd = sd_for(vggish_features, seed)
+    p = torch.from_numpy(recipe.uniform01(shape, seed + 1))
+    t = torch.from_numpy(recipe.uniform01(shape, seed + 2))
+    out = TC.vggish_feature_loss(sd, p, t)
+    assert rel_err(out.numpy(), goldens_vgg[f"vgg_{case}_loss"]) < 2e-6
+

@@ -1,0 +1,69 @@
+"""Per-kernel summary of tools/pmc_train.sh's counter passes (one train step = 1/3 of the dispatches).
+
+HBM bytes: FETCH_SIZE (KiB) x 2 (the gfx950 correction of MI355X_MICROARCH.md: FETCH_SIZE reports half the
+bytes of 16-B streaming reads) + WRITE_SIZE (KiB), x 1024.  MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES /
+(GRBM_GUI_ACTIVE / 8 x 256 CUs x 4 SIMDs): GRBM_GUI_ACTIVE is summed over the 8 XCDs (checked: it equals 8 x
+the dispatch duration x 2.3 GHz), and SQ_VALU_MFMA_BUSY_CYCLES is the instructions' issue cycles summed over
+all SIMDs (checked: 32 x SQ_INSTS_MFMA for the 32x32x8 bf16 form).
+usage: python tools/pmc_train_summary.py <dir written by pmc_train.sh>
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def load(d, name):
+    files = glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        return []
+    return list(csv.DictReader(open(files[0])))
+
+
+def short(n):
+    n = re.sub(r"\(.*", "", n).replace("void ", "")
+    return re.sub(r"^ldm::(\(anonymous namespace\)::|wg::)?", "", n)
+
+
+def main(d):
+    per = defaultdict(lambda: defaultdict(float))
+    calls = defaultdict(set)
+    for name in ("fetch", "write", "mfma"):
+        for r in load(d, name):
+            k = short(r["Kernel_Name"])
+            per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            calls[(k, name)].add(r["Dispatch_Id"])
+    steps = 3.0   # bench --steps 2 --warmup 1
+    out = {}
+    tot_bytes = tot_busy = tot_gui = 0.0
+    for k, c in per.items():
+        n = max(len(calls[(k, "fetch")]), 1)
+        by = (2.0 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024.0
+        nm = max(len(calls[(k, "mfma")]), 1)
+        busy, gui = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0), c.get("GRBM_GUI_ACTIVE", 0.0)
+        out[k] = {
+            "dispatches_per_step": round(n / steps, 2),
+            "hbm_bytes_per_step": by / steps,
+            "hbm_bytes_per_dispatch": by / n,
+            "mfma_insts_per_step": c.get("SQ_INSTS_MFMA", 0.0) / steps,
+            "mfma_util": (busy / (gui / 8 * 256 * 4)) if gui else None,
+        }
+        tot_bytes += by
+        tot_busy += busy
+        tot_gui += gui
+    res = {
+        "workload": "bench.py --workload train (config 3: B=32, bf16 autocast), 2 timed + 1 warm-up steps",
+        "formulas": {"hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024",
+                     "mfma_util": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 256 * 4)"},
+        "step_hbm_bytes": tot_bytes / steps,
+        "step_mfma_util": (tot_busy / (tot_gui / 8 * 256 * 4)) if tot_gui else None,
+        "kernels": dict(sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_step"])),
+    }
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
