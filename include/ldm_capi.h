@@ -75,7 +75,8 @@ typedef struct ldm_epilogue {
 } ldm_epilogue;
 
 typedef struct ldm_conv_plan {
-    int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32         */
+    int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32, 3 LDS-staged */
+                           /* 16-bit-operand MFMA 32x32x16 (tm = BM/64, tn = LDM_DT_F16 / _BF16)    */
     int32_t tm, tn, wk;    /* MFMA tiles per wave along M / N, waves splitting K per block      */
     int32_t ks;            /* blocks splitting K (>1: partial tiles + fixed-order last-arriver sum) */
     int32_t balance;       /* 4-phase transposed convs: phase p splits K ks*ntap_p ways (equal K per block) */
@@ -84,6 +85,10 @@ typedef struct ldm_conv_plan {
 } ldm_conv_plan;
 
 int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan);
+/* The kind-3 plan for d at operand precision dtype (LDM_DT_F16 / LDM_DT_BF16): the LDS-staged implicit
+ * GEMM for large-plane NCHW layers (Cin % 32 == 0, >= 4096 positions per phase; bias / eval-BN /
+ * activation epilogues only).  Returns 0 and fills plan, or 1 when the layer is not of that class. */
+int ldm_conv_tiled_plan(const ldm_conv_desc* d, int32_t dtype, ldm_conv_plan* plan);
 /* Force a specific plan (autotuning / tests).  Fills packed_floats / ws_floats; validates.
  * ks < 0 requests the phase-balanced split with base -ks (4-phase layers only). */
 int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,

@@ -120,6 +120,13 @@ struct PhaseTable {
 
 int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt);
 
+// tconv.hip: the LDS-staged 16-bit-operand implicit GEMM (plan kind 3) for large-plane NCHW layers
+struct EpiArgs;
+bool tconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan);
+int tconv_pack(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* w, float* packed, hipStream_t st);
+int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
+                  float* y, hipStream_t st);
+
 // Device-side epilogue parameters (by value in kernel args).
 struct EpiArgs {
     const float* bias;

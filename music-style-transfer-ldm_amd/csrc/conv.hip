@@ -1295,6 +1295,7 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     LDM_REQUIRE(d && plan && w, "conv pack: null argument");
     if (plan->kind == 0) return 0;
     LDM_REQUIRE(packed, "conv pack: null output");
+    if (plan->kind == 3) return tconv_pack(*d, *plan, w, packed, (hipStream_t)stream);
     ConvArgs a;
     int rc = make_args(*d, *plan, a);
     if (rc) return rc;
@@ -1365,6 +1366,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     LDM_REQUIRE(x && w && (y || ep.ddim_coef), "conv forward: null argument");
     LDM_REQUIRE(p.ws_floats == 0 || ws, "conv forward: this plan splits K across blocks and needs a workspace");
     LDM_REQUIRE(!ep.ddim_coef || ep.ddim_x, "conv forward: fused DDIM update needs x");
+    if (p.kind == 3) return tconv_forward(d, p, x, w, ep, y, st);
     ConvArgs a;
     int rc = make_args(d, p, a);
     if (rc) return rc;

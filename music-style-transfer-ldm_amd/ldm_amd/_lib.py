@@ -125,6 +125,7 @@ SIGNATURES = {
     "ldm_ddim_sample": (c_int32, [ctypes.POINTER(UNetShape), ctypes.POINTER(UNetWeights), c_fp, c_fp, c_fp, c_vp,
                                   c_fp, c_int32, c_float, c_fp, c_fp, c_int64, c_fp, c_vp]),
     # backward / optimiser
+    "ldm_conv_tiled_plan": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, ctypes.POINTER(ConvPlan)]),
     "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
     "ldm_conv_backward_weight_dt": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_int32, c_vp]),
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),

@@ -101,6 +101,22 @@ def get_plan(desc, force=None):
     return plan
 
 
+_TILED_CACHE = {}
+
+
+def tiled_plan(desc, dt):
+    """The kind-3 plan (tconv.hip: LDS-staged 16-bit-operand implicit GEMM) for desc at operand precision dt,
+    or None when the layer is not of that kernel's class.  LDM_AMD_TILED=0 turns the path off."""
+    if dt == 0 or os.environ.get("LDM_AMD_TILED", "1") == "0":
+        return None
+    key = (desc.key(), int(dt))
+    if key not in _TILED_CACHE:
+        plan = L.ConvPlan()
+        rc = L.load().ldm_conv_tiled_plan(byref(desc), int(dt), byref(plan))
+        _TILED_CACHE[key] = plan if rc == 0 else None
+    return _TILED_CACHE[key]
+
+
 def set_plan_override(desc, kind, tm=1, tn=1, wk=1, ks=1):
     _PLAN_OVERRIDE[desc.key()] = (kind, tm, tn, wk, ks)
 
@@ -118,7 +134,7 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
         return weight
     owner = weight if owner is None else owner
     key = (owner._version, tag, desc.Cin, desc.Cout, desc.kh, desc.kw, desc.stride, desc.pad, desc.out_pad,
-           desc.transposed, plan.kind, plan.tm)
+           desc.transposed, plan.kind, plan.tm, plan.tn if plan.kind == 3 else 0)
     per = _PACK_CACHE.get(owner)
     if per is None:
         per = {}
@@ -157,12 +173,15 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     if B == 0:   # an empty batch shard (data-parallel sampling with B < world size): nothing to launch
         return out if out is not None else torch.empty((0, Cout, desc.Hout, desc.Wout), device=x.device,
                                                        dtype=torch.float32)
+    dt = autocast_dt() if dtype is None else int(dtype)
+    if plan is None and bcast is None and skip is None:
+        plan = tiled_plan(desc, dt)
     plan = plan or get_plan(desc)
     wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
     y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
     ep = L.Epilogue()
     ep.bias = _p(bias)
-    ep.dtype = autocast_dt() if dtype is None else int(dtype)
+    ep.dtype = dt
     keep = []
     if bn is not None:
         g, b_, m, v, eps = bn
@@ -215,7 +234,7 @@ def conv_backward_data(dy, weight, desc, wkey=None, dtype=0):
     """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc);
     dtype = LDM_DT_* operand precision (the forward's autocast precision)."""
     dd = dual_desc(desc)
-    plan = get_plan(dd)
+    plan = tiled_plan(dd, int(dtype)) or get_plan(dd)
     wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
     dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
     ep = L.Epilogue()

@@ -1,0 +1,90 @@
+"""GPU parity of the LDS-staged 16-bit-operand conv (tconv.hip, plan kind 3): the path the train step's
+large-plane layers (VAE encoder / decoder, style encoder, their data gradients) and the VGGish stack take
+inside a torch.autocast(bf16 / fp16) region.  Reference: float64 torch conv / conv_transpose of the SAME
+operands rounded to the 16-bit type (what the kernel multiplies; fp32 accumulation), tolerance 1e-5 of
+max |y| (fp32 sums over K <= 1152 of exact 16-bit products), plus the fused epilogues and run-to-run
+bitwise equality."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as tF
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+# (B, Cin, H, W, Cout, k, stride, pad, out_pad, transposed)
+CASES = {
+    "k3s1_64to128": (2, 64, 32, 64, 128, 3, 1, 1, 0, False),
+    "k3s2_64to128": (4, 64, 64, 128, 128, 3, 2, 1, 0, False),
+    "k4s2_128to64": (2, 128, 64, 128, 64, 4, 2, 1, 0, False),        # the decoder convT's data gradient
+    "convT_k4_128to64": (2, 128, 32, 64, 64, 4, 2, 1, 0, True),       # decoder.3 class: 4 phases x 4 taps
+    "convT_k3op1_64to32": (2, 64, 32, 64, 32, 3, 2, 1, 1, True),      # style-encoder dgrad class: 1/2/2/4 taps
+    "ragged_32to40": (3, 32, 17, 97, 40, 3, 1, 1, 0, False),          # N % 128 != 0, Cout % 32 != 0
+}
+EPIS = {"plain": {}, "bias_relu_actout": {"bias": True, "act": "relu", "act_out": True},
+        "bn_relu": {"bias": True, "bn": True, "act": "relu"}, "tanh": {"act": "tanh"}}
+
+
+def _rand(shape, seed, lo=-1.0, hi=1.0):
+    g = np.random.Generator(np.random.PCG64(seed))
+    return torch.from_numpy(g.uniform(lo, hi, shape).astype(np.float32))
+
+
+@pytest.mark.parametrize("dt", [2, 1])
+@pytest.mark.parametrize("epi", sorted(EPIS))
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_tiled_conv(cuda, case, epi, dt):
+    from ldm_amd import ops
+    if dt == 1 and epi != "bias_relu_actout":
+        pytest.skip("fp16: one epilogue per shape is enough")
+    B, Cin, H, W, Cout, k, s, p, op, tr = CASES[case]
+    e = EPIS[epi]
+    seed = zlib.crc32((case + epi).encode()) % 1000
+    x = _rand((B, Cin, H, W), seed)
+    wshape = (Cin, Cout, k, k) if tr else (Cout, Cin, k, k)
+    w = _rand(wshape, seed + 1, -0.1, 0.1)
+    b = _rand((Cout,), seed + 2, -0.1, 0.1) if e.get("bias") else None
+    bn = None
+    if e.get("bn"):
+        bn = (_rand((Cout,), seed + 3, 0.5, 1.5), _rand((Cout,), seed + 4, -0.1, 0.1),
+              _rand((Cout,), seed + 5, -0.2, 0.2), _rand((Cout,), seed + 6, 0.5, 1.5), 1e-5)
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, s, p, op, tr)
+    assert ops.tiled_plan(desc, dt) is not None, "the case must take the kind-3 path"
+    tdt = torch.bfloat16 if dt == 2 else torch.float16
+    xr, wr = x.to(tdt).double(), w.to(tdt).double()
+    if tr:
+        v = tF.conv_transpose2d(xr, wr, None if b is None else b.double(), stride=s, padding=p, output_padding=op)
+    else:
+        v = tF.conv2d(xr, wr, None if b is None else b.double(), stride=s, padding=p)
+    if bn is not None:
+        g_, be, m, var, eps = bn
+        v = (v - m.double()[None, :, None, None]) / torch.sqrt(var.double()[None, :, None, None] + eps) \
+            * g_.double()[None, :, None, None] + be.double()[None, :, None, None]
+    act = e.get("act", "none")
+    ref = {"none": lambda u: u, "relu": torch.relu, "tanh": torch.tanh}[act](v)
+    dev = lambda t: None if t is None else t.to(cuda)   # noqa: E731
+    aout = torch.empty(tuple(ref.shape), device=cuda) if e.get("act_out") else None
+    bng = None if bn is None else tuple(dev(t) for t in bn[:4]) + (bn[4],)
+    y = ops.conv_forward(dev(x), dev(w), dev(b), stride=s, padding=p, transposed=tr, output_padding=op, act=act,
+                         bn=bng, act_out=aout, dtype=dt)
+    y2 = ops.conv_forward(dev(x), dev(w), dev(b), stride=s, padding=p, transposed=tr, output_padding=op, act=act,
+                          bn=bng, dtype=dt)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape
+    assert rel_err(y.double().cpu().numpy(), ref.numpy()) < 1e-5
+    assert torch.equal(y, y2)
+    if aout is not None:
+        assert torch.equal(aout, y)
+
+
+def test_tiled_plan_classes(cuda):
+    """Which layers take the kind-3 path: 16-bit operands only, Cin % 32 == 0, >= 4096 positions."""
+    from ldm_amd import ops
+    big = ops.make_desc(32, 128, 32, 128, 64, 4, 4, 2, 1, 0, True)        # decoder.3 at B = 32
+    assert ops.tiled_plan(big, 2) is not None and ops.tiled_plan(big, 0) is None
+    assert ops.tiled_plan(ops.make_desc(8, 256, 4, 16, 512, 3, 3, 2, 1), 2) is None        # UNet-sized: general
+    assert ops.tiled_plan(ops.make_desc(32, 1, 128, 512, 64, 3, 3, 2, 1), 2) is None      # Cin = 1: x4 kernel
+    assert ops.tiled_plan(ops.make_desc(32, 48, 64, 64, 64, 3, 3, 1, 1), 2) is None       # Cin % 32 != 0
