@@ -8,8 +8,9 @@ Differences from the reference, all deliberate:
   * torch.optim.Adam / AdamW are ldm_amd.optim.Adam / AdamW (same update, one fused multi-tensor HIP
     launch per group); torch.amp.GradScaler is ldm_amd.optim.GradScaler (same scale / skip / growth
     rules).  Both are torch.optim-compatible (ReduceLROnPlateau and state_dicts work unchanged).
-  * The forward runs inside torch.autocast like the reference (train.py:176), but the HIP kernels
-    compute in fp32 regardless (>= the reference's fp16 autocast precision).
+  * The forward runs inside torch.autocast like the reference (train.py:176); inside it the HIP
+    convolutions round their operands to the region's dtype (fp16 by default on a GPU, bf16 with
+    autocast_dtype) and accumulate in fp32.  autocast_enabled = False runs the step in fp32.
   * Data-parallel: when torch.distributed is initialised with world_size > 1, each rank trains on its
     own batch shard and the gradients are all-reduced (bucketed, overlapped with backward) before the
     optimiser step (ldm_amd.dist.GradAllReduce).  Single-process behaviour is unchanged.
@@ -148,6 +149,7 @@ class LDMTrainer:
         # dtype of the train step's autocast region (train.py:174 uses the device default: fp16 on a GPU;
         # bfloat16 = BASELINE config 3); the HIP convs then round their operands to it (ldm_capi.h LDM_DT_*)
         self.autocast_dtype = None
+        self.autocast_enabled = True
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", factor=0.5,
                                                                     patience=10)
         self.reducer = None
@@ -170,7 +172,7 @@ class LDMTrainer:
         if t is None:
             t = self._sample_t(batch_size)
         ac = {} if self.autocast_dtype is None else {"dtype": self.autocast_dtype}
-        with torch.autocast(device_type=self.device.type, **ac):
+        with torch.autocast(device_type=self.device.type, enabled=self.autocast_enabled, **ac):
             outputs = self.model(content_spec, style_spec, t, noise=noise)
             noise_pred = outputs["noise_pred"]
             noise = outputs["noise"]
