@@ -17,6 +17,8 @@
 // order, so the result is bitwise reproducible.
 // MFMA v_mfma_f32_16x16x4_f32: lane l = (col l&15, group g = l>>4); for the 16 positions of step u the
 // lane supplies positions 16u + 4g + j at MFMA j (A as one float4 from LDS, B as 4 window values).
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -312,6 +314,268 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// The same weight gradient with 16-bit operands (the train step's torch.autocast region) on the gfx950
+// double-rate v_mfma_f32_32x32x16_{f16,bf16}: K = 16 positions per MFMA instead of 4 per f32 MFMA.
+//
+// The fp32 form above reads its gathered operand one scalar per position per tap, so at 16-bit rates
+// it would be bound by LDS reads and their conversions.  Here a block owns BM rows (m) x 32 gathered
+// channels (c) x all k*k taps; its NW = WM * KK waves split the rows (wm) and the tap rows (ky): a wave
+// covers BM/WM rows and the KK taps (ky, 0..KK-1) of 32 channels.  K is walked in chunks of 32 output
+// positions (one 32-wide row segment, or two 16-wide rows), two MFMA k-steps of 16 positions each.
+// Per k-step a lane of column c needs positions q0 .. q0+7 (q0 = 16 ks + 8 h) of every kx tap, i.e.
+// window columns 3 + kx + S j of one window row; their union is one aligned run of 4*NB floats, read as
+// NB ds_read_b128 (channel pitch = 4 mod 64 floats: 16 lanes' 16-B reads are conflict-free), and each
+// tap's fragment is 8 of those registers rounded to 16 bits.  The Dense rows are read two pieces
+// (8 positions) per fragment from an XOR-swizzled [BM][32] tile.  Both tiles arrive by LDS DMA, double-
+// buffered.  Requires pad = 1 (every k3 / k4 layer of the model), so the window origin shift e = 3.
+// MFMA maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j] and
+// B[k = 8h + j][col r]; D col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4h.
+// ------------------------------------------------------------------------------------------------------
+constexpr int kLQ = 32;    // positions per chunk
+constexpr int kLC = 32;    // gathered channels per block
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+
+template <int DT>
+__device__ __forceinline__ floatx16 mma32x16(const floatx8& a, const floatx8& b, const floatx16& c) {
+    if constexpr (DT == 1)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_convertvector(a, halfx8), __builtin_convertvector(b, halfx8),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_convertvector(a, bf16x8),
+                                                       __builtin_convertvector(b, bf16x8), c, 0, 0, 0);
+}
+
+struct LpArgs {
+    const float* dense;   // [B][M][Hq*Wq]
+    const float* gath;    // [B][C][Hg][Wg]
+    float* partial;       // [splits][M][C*T]
+    int32_t B, M, C, Hq, Wq, Hg, Wg;
+    int32_t cols, rows, cps, nchunk, per_split;
+    int32_t wr, wca, pitch_c;   // window rows, row pitch, channel pitch (floats)
+};
+
+__host__ __device__ constexpr int lp_nb(int S, int KK) { return (3 + 7 * S + KK + 3) / 4; }   // b128 reads per k-step
+__host__ __device__ inline int lp_buf_floats(int bm, int pitch_c) { return bm * kLQ + (kLC * pitch_c + 255) / 256 * 256; }
+__host__ __device__ constexpr int lp_swz(int row) { return (row >> 1) & 7; }
+
+template <int S, int KK, int BM, int WM, int DT>
+__global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
+    constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp_nb(S, KK);
+    static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ky = wave % KK, wm = wave / KK;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * BM, c0 = blockIdx.x * kLC;
+    const int HQ = a.Hq * a.Wq;
+    const int bufF = lp_buf_floats(BM, a.pitch_c);
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 4), 0x00020000);
+
+    // chunk ch -> sample, first row, first column; its DMAs into buffer buf
+    auto issue = [&](int ch, int buf) {
+        const int b = ch / a.cps;
+        const int rr = ch - b * a.cps;
+        int qy0, qx0;
+        if (a.cols == a.Wq) {
+            qy0 = rr * a.rows, qx0 = 0;
+        } else {
+            const int segs = a.Wq / kLQ;
+            qy0 = rr / segs, qx0 = (rr - qy0 * segs) * kLQ;
+        }
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+        // Dense: BM rows x 8 pieces; one wave-instruction = 8 rows
+        for (int gi = wave; gi < BM / 8; gi += NW) {
+            const int row = gi * 8 + (lane >> 3);
+            const int sp = (lane & 7) ^ lp_swz(row);        // source piece landing in destination piece lane & 7
+            const int ql = sp * 4;
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const int m = m0 + row;
+            const int voff = m < a.M ? (((b * a.M + m) * HQ + qy * a.Wq + qx) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(base + gi * 1024), 16, voff, 0, 0, 0);
+        }
+        // window [32][pitch_c]: rows of wca floats, pieces past wr * wca in a channel are padding (zeros)
+        const int wq4 = a.wca >> 2, pq = a.pitch_c >> 2;
+        const int npiece = kLC * pq;
+        const int row0 = qy0 * S - 1, colA = qx0 * S - 4;   // pad 1, e = 3
+        for (int gi = wave; gi * 64 < npiece; gi += NW) {
+            const int pc = gi * 64 + lane;
+            const int cl = pc / pq;
+            const int rem = pc - cl * pq;
+            const int wrow = rem / wq4, wp = rem - wrow * wq4;
+            const int c = c0 + cl, iy = row0 + wrow, ix = colA + wp * 4;
+            const bool ok = pc < npiece && c < a.C && wrow < a.wr && (unsigned)iy < (unsigned)a.Hg &&
+                            (unsigned)ix < (unsigned)a.Wg;
+            const int voff = ok ? ((((b * a.C + c) * a.Hg + iy) * a.Wg + ix) * 4) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + BM * kLQ * 4 + gi * 1024), 16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx16 acc[MF][KK];
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int t = 0; t < KK; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
+
+    // per-lane LDS offsets (floats) inside a buffer for k-step ks: A pieces of fragment f, window run start
+    int aoff[2][MF][2], boff[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const int q0 = ks * 16 + 8 * h;
+        const int rl = q0 / a.cols, xl0 = q0 - rl * a.cols;
+#pragma unroll
+        for (int f = 0; f < MF; ++f) {
+            const int row = (wm * MF + f) * 32 + r;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) aoff[ks][f][u] = row * kLQ + ((((q0 >> 2) + u) ^ lp_swz(row)) << 2);
+        }
+        boff[ks] = BM * kLQ + r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S;
+    }
+
+    if (ch_begin < ch_end) issue(ch_begin, 0);
+    for (int ch = ch_begin; ch < ch_end; ++ch) {
+        const int buf = (ch - ch_begin) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // chunk ch landed; every wave is done with the other buffer
+        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+        const float* sb = smem + buf * bufF;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            floatx8 fa[MF];
+#pragma unroll
+            for (int f = 0; f < MF; ++f) {
+                const floatx4 lo = *reinterpret_cast<const floatx4*>(sb + aoff[ks][f][0]);
+                const floatx4 hi = *reinterpret_cast<const floatx4*>(sb + aoff[ks][f][1]);
+                fa[f] = floatx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+            float v[4 * NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const floatx4 p = *reinterpret_cast<const floatx4*>(sb + boff[ks] + 4 * i);
+                v[4 * i + 0] = p[0], v[4 * i + 1] = p[1], v[4 * i + 2] = p[2], v[4 * i + 3] = p[3];
+            }
+#pragma unroll
+            for (int kx = 0; kx < KK; ++kx) {
+                floatx8 fb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fb[j] = v[3 + kx + S * j];
+#pragma unroll
+                for (int f = 0; f < MF; ++f) acc[f][kx] = mma32x16<DT>(fa[f], fb, acc[f][kx]);
+            }
+        }
+    }
+
+    // partial[z][m][c*T + ky*KK + kx]: D col = channel c0 + r, rows (reg & 3) + 8 (reg >> 2) + 4h
+    const int c = c0 + r;
+    if (c < a.C) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * a.C * T + (size_t)c * T + ky * KK;
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int m = m0 + (wm * MF + f) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (m < a.M) {
+                    float* o = out + (size_t)m * a.C * T;
+                    if constexpr (KK == 4) {
+                        *reinterpret_cast<floatx4*>(o) = floatx4{acc[f][0][reg], acc[f][1][reg], acc[f][2][reg], acc[f][3][reg]};
+                    } else {
+#pragma unroll
+                        for (int kx = 0; kx < KK; ++kx) o[kx] = acc[f][kx][reg];
+                    }
+                }
+            }
+    }
+}
+
+struct LpPlan {
+    int S, KK, BM, WM, splits, lds_bytes;
+    LpArgs a;
+};
+
+// 16-bit form: pad 1, k 3 / 4, stride 1 / 2, rows of 16 or a multiple of 32 positions, C >= 16.  K is
+// split over blocks until the grid covers the 256 CUs (one block per CU: the double buffer takes
+// 60-110 KB of LDS); the workspace query (wgrad2_plan_ws) sizes the partials for the larger of the forms.
+bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
+    if (d.kh != d.kw || (d.kh != 3 && d.kh != 4) || (d.stride != 1 && d.stride != 2) || d.pad != 1) return false;
+    LpArgs a{};
+    a.B = d.B;
+    if (!d.transposed) {
+        a.M = d.Cout, a.C = d.Cin, a.Hq = d.Hout, a.Wq = d.Wout, a.Hg = d.Hin, a.Wg = d.Win;
+    } else {
+        a.M = d.Cin, a.C = d.Cout, a.Hq = d.Hin, a.Wq = d.Win, a.Hg = d.Hout, a.Wg = d.Wout;
+    }
+    if (a.C < 16 || a.Wg % 4) return false;
+    if (a.Wq == 16) {
+        if (a.Hq % 2) return false;
+        a.cols = 16, a.rows = 2;
+    } else if (a.Wq % kLQ == 0) {
+        a.cols = kLQ, a.rows = 1;
+    } else {
+        return false;
+    }
+    const int S = d.stride, KK = d.kh;
+    a.cps = a.Hq * a.Wq / kLQ;
+    a.nchunk = a.B * a.cps;
+    a.wr = (a.rows - 1) * S + KK;
+    a.wca = (3 + (a.cols - 1) * S + KK + 3) / 4 * 4;
+    int pc = a.wr * a.wca;
+    while (pc % 64 != 4) pc += 4;
+    a.pitch_c = pc;
+    p.S = S, p.KK = KK;
+    p.BM = a.M >= 128 ? 128 : (a.M > 32 ? 64 : 32);
+    p.WM = p.BM == 128 ? 2 : 1;
+    p.lds_bytes = 2 * lp_buf_floats(p.BM, a.pitch_c) * 4;
+    if (p.lds_bytes > 160 * 1024) return false;
+    const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + kLC - 1) / kLC);
+    int s = 1;
+    while (s < 256 && tiles * s < 256 && a.nchunk / (s * 2) >= 4) s *= 2;
+    p.splits = s;
+    a.per_split = (a.nchunk + s - 1) / s;
+    p.a = a;
+    return true;
+}
+
+template <int S, int KK, int BM, int WM, int DT>
+int launch_lp_dt(const LpPlan& p, hipStream_t st) {
+    auto kfn = wgrad_lp_kernel<S, KK, BM, WM, DT>;
+    static bool opted = false;
+    if (!opted) {
+        LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        opted = true;
+    }
+    dim3 grid((p.a.C + kLC - 1) / kLC, (p.a.M + BM - 1) / BM, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * KK), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_lp_kernel");
+    return 0;
+}
+template <int S, int KK, int DT>
+int launch_lp_bm(const LpPlan& p, hipStream_t st) {
+    switch (p.BM) {
+        case 128: return launch_lp_dt<S, KK, 128, 2, DT>(p, st);
+        case 64: return launch_lp_dt<S, KK, 64, 1, DT>(p, st);
+        default: return launch_lp_dt<S, KK, 32, 1, DT>(p, st);
+    }
+}
+template <int DT>
+int launch_lp(const LpPlan& p, hipStream_t st) {
+    switch (p.S * 10 + p.KK) {
+        case 13: return launch_lp_bm<1, 3, DT>(p, st);
+        case 23: return launch_lp_bm<2, 3, DT>(p, st);
+        case 14: return launch_lp_bm<1, 4, DT>(p, st);
+        default: return launch_lp_bm<2, 4, DT>(p, st);
+    }
+}
+
 struct Plan {
     int S, KK, BM, BC, splits;
     Args a;
@@ -401,10 +665,19 @@ int launch(const Plan& p, hipStream_t st) {
 
 }  // namespace wg
 
+// LDM_WGRAD_LP=0 in the environment keeps 16-bit weight gradients on the tap-shared kernel (A/B timing
+// and the parity test of both forms).
+static bool wgrad_lp_disabled() {
+    const char* e = getenv("LDM_WGRAD_LP");
+    return e && e[0] == '0';
+}
+
 bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats) {
     wg::Plan p;
     if (!wg::plan(d, p)) return false;
     ws_floats = (int64_t)p.splits * p.a.M * p.a.C * p.KK * p.KK;
+    wg::LpPlan lp;
+    if (wg::lp_plan(d, lp)) ws_floats = std::max(ws_floats, (int64_t)lp.splits * lp.a.M * lp.a.C * lp.KK * lp.KK);
     return true;
 }
 
@@ -414,6 +687,16 @@ int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, fl
                hipStream_t st) {
     wg::Plan p;
     if (!wg::plan(d, p)) return -1;
+    if (dtype != LDM_DT_F32 && !wgrad_lp_disabled()) {   // 16-bit operands: the double-rate MFMA form
+        wg::LpPlan lp;
+        if (wg::lp_plan(d, lp)) {
+            lp.a.dense = dense;
+            lp.a.gath = gath;
+            lp.a.partial = partial;
+            splits = lp.splits;
+            return dtype == LDM_DT_F16 ? wg::launch_lp<1>(lp, st) : wg::launch_lp<2>(lp, st);
+        }
+    }
     p.a.lowp = dtype;
     p.a.dense = dense;
     p.a.gath = gath;

@@ -204,3 +204,52 @@ def test_conv_fwd_wgrad_lowp(cuda, name, case):
     (yr * rnd(dy)).sum().backward()
     dw = ops.conv_backward_weight(xd, dy.to(cuda), desc, dtype=dt)
     assert rel_err(npy(dw), wr.grad.numpy()) < 1e-5
+
+
+# the double-rate 16-bit weight-gradient form (wgrad.hip wgrad_lp_kernel) at every geometry class it takes:
+# (B, Cin, H, W, Cout, k, s, p, op, transposed)
+WGRAD_LP_CASES = {
+    "k3s2_vae_enc2": (2, 64, 32, 128, 128, 3, 2, 1, 0, False),     # Wq 64, BM 128, C 64
+    "k3s1_unet_enc1": (2, 32, 16, 64, 64, 3, 1, 1, 0, False),      # stride 1, BM 64, C 32
+    "k3s2_wq32": (2, 128, 16, 64, 256, 3, 2, 1, 0, False),         # Wq 32, M 256 (two row tiles)
+    "k3s2_wq16_rows2": (2, 256, 8, 32, 256, 3, 2, 1, 0, False),    # Wq 16: two rows per chunk
+    "k4s2_convT_m32": (2, 32, 16, 64, 128, 4, 2, 1, 0, True),      # decoder convT 32 -> 128, BM 32
+    "k4s2_convT_m128": (2, 128, 16, 64, 64, 4, 2, 1, 0, True),     # decoder convT 128 -> 64, BM 128
+    "k3s2_convT_op1": (2, 64, 8, 32, 32, 3, 2, 1, 1, True),        # UNet decoder convT (k3 s2 op1)
+    "ragged_m40_c48": (3, 48, 8, 32, 40, 3, 1, 1, 0, False),       # M, C not multiples of the tiles
+}
+
+
+@pytest.mark.parametrize("name", ["fp16", "bf16"])
+@pytest.mark.parametrize("case", sorted(WGRAD_LP_CASES))
+def test_wgrad_lowp_double_rate(cuda, name, case, monkeypatch):
+    """16-bit dW (32x32x16 MFMA form) == float64 of the same-rounded operands to 1e-5 (fp32 accumulation
+    order only), bitwise reproducible, accumulate=1 adds onto dW, and equal within 1e-5 to the tap-shared
+    16-bit form (LDM_WGRAD_LP=0)."""
+    import torch.nn.functional as F
+    import zlib
+    from ldm_amd import ops
+    B, Cin, H, W, Cout, k, s, p, op, tr = WGRAD_LP_CASES[case]
+    g = torch.Generator().manual_seed(zlib.crc32(case.encode()) % 1000)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), generator=g) / (Cin * k * k) ** 0.5
+    dt = 1 if name == "fp16" else 2
+    rnd = (lambda t: t.half().double()) if name == "fp16" else (lambda t: t.bfloat16().double())
+    xr = rnd(x)
+    wr = w.double().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, stride=s, padding=p, output_padding=op) if tr else F.conv2d(xr, wr, stride=s, padding=p)
+    dy = torch.randn(tuple(yr.shape), generator=g)
+    (yr * rnd(dy)).sum().backward()
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, s, p, op, tr)
+    xd, dyd = x.to(cuda), dy.to(cuda)
+    dw1 = ops.conv_backward_weight(xd, dyd, desc, dtype=dt)
+    dw2 = ops.conv_backward_weight(xd, dyd, desc, dtype=dt)
+    acc = torch.ones_like(dw1)
+    ops.conv_backward_weight(xd, dyd, desc, dw=acc, accumulate=True, dtype=dt)
+    monkeypatch.setenv("LDM_WGRAD_LP", "0")
+    dw_ts = ops.conv_backward_weight(xd, dyd, desc, dtype=dt)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2)
+    assert rel_err(npy(dw1), wr.grad.numpy()) < 1e-5
+    assert rel_err(npy(acc), wr.grad.numpy() + 1.0) < 1e-5
+    assert rel_err(npy(dw1), npy(dw_ts)) < 1e-5

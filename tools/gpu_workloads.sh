@@ -12,6 +12,6 @@ timeout -k 10 240 python -u bench.py --workload train --steps 10 --warmup 3 > $O
 cat $O/train.json
 if [ "${PROF:-1}" = 1 ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_train -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload train --steps 5 --warmup 2 > $O/prof_train.log 2>&1 || { echo "rocprof failed"; tail $O/prof_train.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_train -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload train --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_train.log 2>&1 || { echo "rocprof failed"; tail $O/prof_train.log; exit 1; }
   find $O/prof_train -name '*stats*'
 fi

@@ -1,7 +1,8 @@
 set -o pipefail
-export PYTHONUNBUFFERED=1
-R=$GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tiled.py > gpurun_out/h1_tiled.log 2>&1 ; \
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_amp.py tests/test_gpu_features.py tests/test_gpu_train.py > gpurun_out/h1_tests.log 2>&1 ; \
-timeout -k 10 300 python -u tools/time_vggish.py > gpurun_out/h1_vgg.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --workload train --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/h1_train.json 2> gpurun_out/h1_train.err
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/g2; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_amp.py -k "wgrad" -q --timeout 120 --timeout-method thread > $O/t.log 2>&1; rc=$?
+tail -15 $O/t.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 120 python -u tools/time_wgrad.py bf16 > $O/time.log 2>&1 || { tail $O/time.log; exit 1; }
+cat $O/time.log
