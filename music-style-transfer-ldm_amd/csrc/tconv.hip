@@ -7,7 +7,9 @@
 // sharing inside a block; its 1-wave blocks re-fetched ~1 GB per launch of the decoder's 128 -> 64 convT
 // and ran its 32x32x8 MFMAs at 10 % busy (profiles/r02/train_pmc.json).  Here a block owns a BM x 128
 // output tile (BM output channels x 128 positions of one phase grid), K = taps x Cin in chunks of 32
-// (tap-major, so a chunk is one tap and 32 channels), and per chunk:
+// (a chunk is one tap and 32 channels; channel-chunk major, tap minor, so the 3-9 taps that read one
+// input window run back to back and find its lines in L2 — tap-major order re-fetched each input line
+// from the Infinity Cache once per tap), and per chunk:
 //   * every lane gathers 16 channels of one position at the chunk's tap (each load instruction is 64
 //     consecutive positions: coalesced for stride 1, 2 lines per 64 lanes at stride 2), rounds them to
 //     16-bit and writes them as two 16-byte LDS stores: B tile [128 positions][32 k] (double-buffered);
@@ -100,10 +102,11 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
     const int gbase = (gb * a.Cin + gk * 16) * HWin;   // floats
-    float gv[16];
-    auto gather = [&](int c) {
-        const int t = c / a.cpt;   // wave-uniform
-        const int ci0 = (c - t * a.cpt) * KC;
+    float gvA[16], gvB[16];   // two chunks of gathered operands in flight (prefetch distance 2)
+    auto gather = [&](int c, float (&gv)[16]) {
+        const int cc = c / ntap;   // channel-chunk major, tap minor: the taps of a window run back to back
+        const int t = c - cc * ntap;   // (wave-uniform)
+        const int ci0 = cc * KC;
         const int iy = gqy * a.pt.sy + a.pt.dy[ph][t];
         const int ix = gqx * a.pt.sy + a.pt.dx[ph][t];
         const bool ok = gval && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
         for (int j = 0; j < 16; ++j)
             gv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, uni(j * HWin * 4), 0));
     };
-    auto stage = [&](int buf) {
+    auto stage = [&](int buf, const float (&gv)[16]) {
         floatx8 lo, hi;
 #pragma unroll
         for (int j = 0; j < 8; ++j) lo[j] = gv[j], hi[j] = gv[8 + j];
@@ -145,17 +148,18 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
-    gather(0);
+    gather(0, gvA);
     loadA(0, af);
-    stage(0);
+    stage(0, gvA);
     __syncthreads();
-    for (int c = 0; c < nch; ++c) {
+    if (nch > 1) gather(1, gvA);
+    // step c: chunk c+1's gather (issued one step earlier, in gs) is staged after chunk c's MFMAs, while
+    // chunk c+2's gather (into gl) stays in flight across the barrier
+    auto step = [&](int c, const float (&gs)[16], float (&gl)[16]) {
         const int buf = c & 1;
         const bool more = c + 1 < nch;
-        if (more) {
-            gather(c + 1);
-            loadA(c + 1, an);
-        }
+        if (more) loadA(c + 1, an);
+        if (c + 2 < nch) gather(c + 2, gl);
         const unsigned short* bs = bt[buf];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -169,11 +173,15 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
                 for (int j = 0; j < 2; ++j) acc[i][j] = mma<DT>(af[i][s], bf[j], acc[i][j]);
         }
         if (more) {
-            stage(buf ^ 1);
+            stage(buf ^ 1, gs);
 #pragma unroll
             for (int i = 0; i < MT; ++i) af[i][0] = an[i][0], af[i][1] = an[i][1];
         }
         __syncthreads();
+    };
+    for (int c = 0; c < nch; c += 2) {
+        step(c, gvA, gvB);
+        if (c + 1 < nch) step(c + 1, gvB, gvA);
     }
 
     // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store
@@ -211,7 +219,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     }
 }
 
-// packed[p][c][m][e] = w(co = m, tap t = c / cpt, ci = (c % cpt) * 32 + e) in 16 bits, zero past Cout
+// packed[p][c][m][e] = w(co = m, tap t = c % ntap, ci = (c / ntap) * 32 + e) in 16 bits, zero past Cout
 template <int DT>
 __global__ __launch_bounds__(256) void tconv_pack_kernel(const float* __restrict__ w, unsigned short* __restrict__ out,
                                                          PhaseTable pt, int Cin, int Cout, int KK, int transposed,
@@ -226,7 +234,8 @@ __global__ __launch_bounds__(256) void tconv_pack_kernel(const float* __restrict
     const int64_t row = local / KC;
     const int m = (int)(row % Mpad);
     const int c = (int)(row / Mpad);
-    const int t = c / cpt, ci = (c - t * cpt) * KC + e;
+    const int ntap = pt.ntap[p];
+    const int cc = c / ntap, t = c - cc * ntap, ci = cc * KC + e;
     float v = 0.f;
     if (m < Cout) {
         const int kk = pt.kk[p][t];
@@ -255,10 +264,11 @@ static int layout(const ldm_conv_desc& d, int bm, PhaseTable& pt, int& Mpad, int
 }  // namespace tc
 
 // A kind-3 plan for `d` at operand precision `dtype`; false when the layer is not of this kernel's class
-// (16-bit operands, NCHW, Cin % 32 == 0, a phase grid of >= 4096 positions, tensors < 2 GiB).
+// (16-bit operands, NCHW, Cin % 32 == 0, Cout >= 16, a phase grid of >= 4096 positions, tensors < 2 GiB).
 bool tconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan) {
     if (dtype != LDM_DT_F16 && dtype != LDM_DT_BF16) return false;
     if (d.layout != 0 || d.Cin % tc::KC != 0 || d.B <= 0) return false;
+    if (d.Cout < 16) return false;   // a 64- / 128-row tile would be > 90 % padding (the decoder's 64 -> 1 convT)
     PhaseTable pt;
     int Mpad;
     int64_t halfs;
