@@ -21,7 +21,15 @@
 //
 // MFMA operand maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j]
 // and B[k = 8h + j][col r], j = 0..7; D: col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4h.
+#include <type_traits>
+
 #include "common.h"
+
+// Diagnostic builds only (tools/build_diag.sh): TCONV_DIAG bit 0 = no gather loads (B from registers),
+// bit 1 = no MFMAs.
+#ifndef TCONV_DIAG
+#define TCONV_DIAG 0
+#endif
 
 namespace ldm {
 namespace tc {
@@ -102,7 +110,6 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
     const int gbase = (gb * a.Cin + gk * 16) * HWin;   // floats
-    float gvA[16], gvB[16];   // two chunks of gathered operands in flight (prefetch distance 2)
     auto gather = [&](int c, float (&gv)[16]) {
         const int cc = c / ntap;   // channel-chunk major, tap minor: the taps of a window run back to back
         const int t = c - cc * ntap;   // (wave-uniform)
@@ -113,7 +120,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
         const int voff = ok ? (gbase + ci0 * HWin + iy * a.Win + ix) * 4 : kOOB;
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-            gv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, uni(j * HWin * 4), 0));
+            gv[j] = (TCONV_DIAG & 1) ? (float)(voff + j)
+                                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, uni(j * HWin * 4), 0));
     };
     auto stage = [&](int buf, const float (&gv)[16]) {
         floatx8 lo, hi;
@@ -129,7 +137,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.w), (short)0, 0x7ffffff0, 0x00020000);
     const int wph = (int)a.pt.wofs[ph];   // 16-bit elements
-    u16x8 af[MT][2], an[MT][2];   // this chunk's A fragments, the next chunk's (in flight)
+    u16x8 aset[3][MT][2];   // A fragments of chunks c, c+1, c+2 (two chunks of weight loads in flight)
     auto loadA = [&](int c, u16x8 (&dst)[MT][2]) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
@@ -148,18 +156,23 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
-    gather(0, gvA);
-    loadA(0, af);
-    stage(0, gvA);
+    float gv[2][16];
+    gather(0, gv[0]);
+    loadA(0, aset[0]);
+    if (nch > 1) loadA(1, aset[1]);
+    stage(0, gv[0]);
     __syncthreads();
-    if (nch > 1) gather(1, gvA);
-    // step c: chunk c+1's gather (issued one step earlier, in gs) is staged after chunk c's MFMAs, while
-    // chunk c+2's gather (into gl) stays in flight across the barrier
-    auto step = [&](int c, const float (&gs)[16], float (&gl)[16]) {
+    if (nch > 1) gather(1, gv[0]);
+    // step c (G = c % 2, A = c % 3, compile-time so every register set is named, never copied): chunk
+    // c+2's weights and gather are issued, chunk c is multiplied, chunk c+1's gather (issued one step
+    // earlier, in gv[G]) is staged; weights are consumed two steps after their loads, gathers one
+    auto step = [&](int c, auto Gc, auto Ac) {
+        constexpr int G = decltype(Gc)::value, A = decltype(Ac)::value;
         const int buf = c & 1;
-        const bool more = c + 1 < nch;
-        if (more) loadA(c + 1, an);
-        if (c + 2 < nch) gather(c + 2, gl);
+        if (c + 2 < nch) {
+            loadA(c + 2, aset[(A + 2) % 3]);
+            gather(c + 2, gv[G ^ 1]);
+        }
         const unsigned short* bs = bt[buf];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -170,18 +183,26 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = mma<DT>(af[i][s], bf[j], acc[i][j]);
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr ((TCONV_DIAG & 2) != 0)
+                        acc[i][j][0] = acc[i][j][0] + (float)(aset[A][i][s][0] ^ bf[j][1]);
+                    else
+                        acc[i][j] = mma<DT>(aset[A][i][s], bf[j], acc[i][j]);
+                }
         }
-        if (more) {
-            stage(buf ^ 1, gs);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) af[i][0] = an[i][0], af[i][1] = an[i][1];
-        }
+        if (c + 1 < nch) stage(buf ^ 1, gv[G]);
         __syncthreads();
     };
-    for (int c = 0; c < nch; c += 2) {
-        step(c, gvA, gvB);
-        if (c + 1 < nch) step(c + 1, gvB, gvA);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    for (int c = 0; c < nch; c += 6) {
+        step(c, I0{}, I0{});
+        if (c + 1 < nch) step(c + 1, I1{}, I1{});
+        if (c + 2 < nch) step(c + 2, I0{}, I2{});
+        if (c + 3 < nch) step(c + 3, I1{}, I0{});
+        if (c + 4 < nch) step(c + 4, I0{}, I1{});
+        if (c + 5 < nch) step(c + 5, I1{}, I2{});
     }
 
     // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store
