@@ -221,6 +221,103 @@ __global__ __launch_bounds__(256) void attention_backward_kernel(const float* __
     }
 }
 
+// The same backward on f32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products) when L, S and d are
+// multiples of 16 (the UNet's CA2: d 64, L = S = 64; CA1: d 128, L = S = 16 at the canonical latent): every
+// product of the five is a sweep of 16x16 output tiles over the block's 4 waves with both operands read
+// from LDS (the scalar form above spent ~6K dependent LDS-operand FMAs per thread: 128 us per call at B=32).
+// Operand (m, k) of a product lives at base[m * sm + k * sk]; the lane's D rows 4 lg + r, column lane & 15.
+template <class FA, class FB, class FO>
+__device__ __forceinline__ void lds_mfma_gemm(int M, int N, int K, FA&& fa, FB&& fb, FO&& out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int col = lane & 15, lg = lane >> 4;
+    const int tn = N / 16, tiles = (M / 16) * tn;
+    for (int t = wave; t < tiles; t += nw) {
+        const int m0 = (t / tn) * 16, n0 = (t % tn) * 16;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K; k0 += 16) {
+            float a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = fa(m0 + col, k0 + 4 * j + lg);
+                b[j] = fb(k0 + 4 * j + lg, n0 + col);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out(m0 + 4 * lg + r, n0 + col, acc[r]);
+    }
+}
+
+__global__ __launch_bounds__(256) void attention_backward_mfma_kernel(const float* __restrict__ q,
+                                                                      const float* __restrict__ kv,
+                                                                      const float* __restrict__ dout,
+                                                                      float* __restrict__ dq, float* __restrict__ dkv,
+                                                                      int E, int heads, int L, int S, float scale) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int d = E / heads;
+    const int h = blockIdx.x % heads, b = blockIdx.x / heads;
+    // row pitches padded by one float so that the 16 lanes of an MFMA operand column hit 16 banks
+    const int pL = L + 1, pS = S + 1;
+    float* X1 = sm;              // [d][L+1]
+    float* X2 = X1 + d * pL;     // [d][S+1]
+    float* P = X2 + d * pS;      // [L][S+1]
+    float* dP = P + L * pS;      // [L][S+1]
+    const size_t qo = ((size_t)b * E + (size_t)h * d) * L;
+    const size_t ko = ((size_t)b * 2 * E + (size_t)h * d) * S;
+    const size_t vo = ((size_t)b * 2 * E + E + (size_t)h * d) * S;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+    auto load2 = [&](const float* s1, float m1, const float* s2) {
+        for (int e = tid; e < d * L; e += nt) X1[(e / L) * pL + e % L] = s1[e] * m1;
+        for (int e = tid; e < d * S; e += nt) X2[(e / S) * pS + e % S] = s2[e];
+    };
+    // phase 1: P[l][s] = sum_c (q*scale)[c][l] K[c][s], softmax over s
+    load2(q + qo, scale, kv + ko);
+    __syncthreads();
+    lds_mfma_gemm(L, S, d, [&](int l, int c) { return X1[c * pL + l]; }, [&](int c, int s) { return X2[c * pS + s]; },
+                  [&](int l, int s, float v) { P[l * pS + s] = v; });
+    __syncthreads();
+    for (int l = wave; l < L; l += nw) {
+        float* row = P + l * pS;
+        float mx = -INFINITY;
+        for (int s = lane; s < S; s += 64) mx = fmaxf(mx, row[s]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        float sum = 0.f;
+        for (int s = lane; s < S; s += 64) {
+            const float ex = expf(row[s] - mx);
+            row[s] = ex;
+            sum += ex;
+        }
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        for (int s = lane; s < S; s += 64) row[s] = row[s] / sum;
+    }
+    __syncthreads();
+    // phase 2: X1 <- dO, X2 <- V; dV[c][s] = sum_l dO[c][l] P[l][s] (global); dP[l][s] = sum_c dO[c][l] V[c][s]
+    load2(dout + qo, 1.f, kv + vo);
+    __syncthreads();
+    lds_mfma_gemm(d, S, L, [&](int c, int l) { return X1[c * pL + l]; }, [&](int l, int s) { return P[l * pS + s]; },
+                  [&](int c, int s, float v) { dkv[vo + (size_t)c * S + s] = v; });
+    lds_mfma_gemm(L, S, d, [&](int l, int c) { return X1[c * pL + l]; }, [&](int c, int s) { return X2[c * pS + s]; },
+                  [&](int l, int s, float v) { dP[l * pS + s] = v; });
+    __syncthreads();
+    // phase 3: dS = P * (dP - rowsum(dP * P)), in place in dP
+    for (int l = wave; l < L; l += nw) {
+        float s0 = 0.f;
+        for (int s = lane; s < S; s += 64) s0 += dP[l * pS + s] * P[l * pS + s];
+        for (int o = 32; o > 0; o >>= 1) s0 += __shfl_xor(s0, o);
+        for (int s = lane; s < S; s += 64) dP[l * pS + s] = P[l * pS + s] * (dP[l * pS + s] - s0);
+    }
+    __syncthreads();
+    // phase 4: X1 <- q*scale, X2 <- K; dq[c][l] = scale sum_s K[c][s] dS[l][s]; dK[c][s] = sum_l qs[c][l] dS[l][s]
+    load2(q + qo, scale, kv + ko);
+    __syncthreads();
+    lds_mfma_gemm(d, L, S, [&](int c, int s) { return X2[c * pS + s]; }, [&](int s, int l) { return dP[l * pS + s]; },
+                  [&](int c, int l, float v) { dq[qo + (size_t)c * L + l] = v * scale; });
+    lds_mfma_gemm(d, S, L, [&](int c, int l) { return X1[c * pL + l]; }, [&](int l, int s) { return dP[l * pS + s]; },
+                  [&](int c, int s, float v) { dkv[ko + (size_t)c * S + s] = v; });
+}
+
 // ================================================================================================
 // multi-tensor Adam (torch.optim.Adam, train.py:156) with GradScaler unscale / inf check / skip
 // ================================================================================================
@@ -427,6 +524,21 @@ extern "C" int ldm_attention_backward(const float* q, const float* kv, const flo
                                       void* stream) {
     LDM_REQUIRE(q && kv && dout && dq && dkv && B > 0 && heads > 0 && E % heads == 0, "attention_backward: bad argument");
     const int d = E / heads;
+    if (L % 16 == 0 && S % 16 == 0 && d % 16 == 0) {
+        const size_t lds = ((size_t)d * (L + 1) + (size_t)d * (S + 1) + 2 * (size_t)L * (S + 1)) * sizeof(float);
+        if (lds <= 160 * 1024) {
+            static bool opted = false;
+            if (!opted) {
+                LDM_HIP_TRY(hipFuncSetAttribute((const void*)attention_backward_mfma_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                opted = true;
+            }
+            hipLaunchKernelGGL(attention_backward_mfma_kernel, dim3(B * heads), dim3(256), lds, (hipStream_t)stream, q,
+                               kv, dout, dq, dkv, E, heads, L, S, scale);
+            LDM_CHECK_LAUNCH("attention_backward_mfma_kernel");
+            return 0;
+        }
+    }
     const size_t lds = ((size_t)d * L + (size_t)d * S + 2 * (size_t)L * S) * sizeof(float);
     LDM_REQUIRE(lds <= 64 * 1024, "attention_backward: head tile exceeds LDS budget");
     hipLaunchKernelGGL(attention_backward_kernel, dim3(B * heads), dim3(256), lds, (hipStream_t)stream, q, kv, dout, dq,

@@ -160,9 +160,10 @@ def test_batchnorm_train_backward(cuda, act, shape):
     assert rel_err(npy(bn.running_var), bn_ref.running_var.numpy()) < TOL
 
 
-@pytest.mark.parametrize("E,L", [(256, 64), (512, 16)])
+@pytest.mark.parametrize("E,L", [(256, 64), (512, 16), (256, 4), (512, 36)])
 def test_attention_backward(cuda, E, L):
-    """CA2 (E=256, d=64, L=S=64) and CA1 (E=512, d=128, L=S=16) core backward."""
+    """CA2 (E=256, d=64, L=S=64) and CA1 (E=512, d=128, L=S=16) core backward on the MFMA form; L=S=4
+    (a 16x16 latent's CA1) and 36 on the scalar form (dims not multiples of 16)."""
     from ldm_amd import functional as HF
     heads, B = 4, 2
     d = E // heads
