@@ -21,7 +21,9 @@ byref = ctypes.byref
 # helpers
 # ------------------------------------------------------------------------------------------------
 def stream_handle():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t of the caller's current stream (the direct C query: torch.cuda.current_stream()
+    costs ~10 us of Python per call, ~0.5 ms per train step)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def _p(t):

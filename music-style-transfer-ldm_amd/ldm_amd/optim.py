@@ -22,9 +22,12 @@ class _SlotTable:
     """Device table of ldm_tensor_slot {param, grad, exp_avg, exp_avg_sq, numel} + chunk map.
 
     Tables are cached by the tensors' addresses (the same parameters, gradients and state give the same
-    table every step), and the chunk map is built with numpy, so a step costs no per-chunk host work."""
+    table every step).  The chunk map depends only on the sizes and is uploaded once per size list; the
+    slot rows (whose gradient addresses move when zero_grad() drops the grads) go up with an asynchronous
+    copy from pinned memory, so building a table never synchronises the host with the device."""
 
     _cache = {}
+    _maps = {}
 
     def __new__(cls, params, grads, m, v):
         key = tuple((p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(), 0 if b is None else b.data_ptr(),
@@ -35,14 +38,19 @@ class _SlotTable:
             return hit
         self = super().__new__(cls)
         rows = np.array(key, dtype=np.int64).reshape(-1, 5)
-        nch = (rows[:, 4] + CHUNK - 1) // CHUNK
-        ct = np.repeat(np.arange(len(rows), dtype=np.int32), nch)
-        first = np.repeat(np.cumsum(nch) - nch, nch)
-        cs = (np.arange(int(nch.sum()), dtype=np.int64) - first) * CHUNK
-        self.slots = torch.from_numpy(rows).to(dev)
-        self.chunk_tensor = torch.from_numpy(ct).to(dev)
-        self.chunk_start = torch.from_numpy(cs).to(dev)
-        self.nchunks = int(len(ct))
+        numels = tuple(int(k[4]) for k in key)
+        mp = cls._maps.get((dev, numels))
+        if mp is None:
+            nch = (rows[:, 4] + CHUNK - 1) // CHUNK
+            ct = np.repeat(np.arange(len(rows), dtype=np.int32), nch)
+            first = np.repeat(np.cumsum(nch) - nch, nch)
+            cs = (np.arange(int(nch.sum()), dtype=np.int64) - first) * CHUNK
+            mp = (torch.from_numpy(ct).to(dev), torch.from_numpy(cs).to(dev), int(len(ct)))
+            cls._maps[(dev, numels)] = mp
+        self.chunk_tensor, self.chunk_start, self.nchunks = mp
+        host = torch.from_numpy(rows).pin_memory()        # caching host allocator: reused once the copy ran
+        self.slots = torch.empty(rows.shape, dtype=torch.int64, device=dev)
+        self.slots.copy_(host, non_blocking=True)
         self.key = key
         if len(cls._cache) > 64:
             cls._cache.clear()
