@@ -136,6 +136,11 @@ class Adam(torch.optim.Optimizer):
                        None if found_inf is None else found_inf.data_ptr(), stream_handle())
                 # the tables are read by the kernel asynchronously: keep them alive until it ran
                 self._tables[(gi, step)] = tab
+                # the kernel wrote the parameters through raw pointers: move their autograd versions the
+                # way an in-place torch update does, so that version-keyed caches (packed conv weights,
+                # ops.packed_weight; the UNet engine's step weights) re-pack them
+                for p in ps:
+                    torch.autograd.graph.increment_version(p)
         return loss
 
 

@@ -291,6 +291,37 @@ class _ZeroFeat(torch.nn.Module):
         return torch.zeros((), device=a.device)
 
 
+def test_second_step_uses_updated_weights(cuda):
+    """After an optimizer step the next forward must see the new weights: the fused Adam writes them through
+    raw pointers, so it has to move their versions or the packed-weight caches keep serving the old ones.
+    Step 2 of one trainer == step 1 of a fresh model loaded with the trainer's state after step 1."""
+    import models.model as M
+    import models.train as TR
+    content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 850)).to(cuda)
+    style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 851)).to(cuda)
+    t = torch.tensor([10, 150], device=cuda)
+    noise = torch.from_numpy(recipe.normal((2, 32, 16, 16), 852)).to(cuda)
+    a = M.LDM(32, pretrained_path="")
+    recipe.fill_module(a, seed=700)
+    a.feature_loss_net = _ZeroFeat()
+    a = a.to(cuda).train()
+    ta = TR.LDMTrainer(a, [], cuda, lr=1e-3)
+    for tr in (ta,):
+        tr.autocast_enabled = False
+    ta.train_step(content, style, t=t, noise=noise)
+    sd = {k: v.detach().clone() for k, v in a.state_dict().items()}
+    l2 = ta.train_step(content, style, t=t, noise=noise)
+    b = M.LDM(32, pretrained_path="")
+    b.feature_loss_net = _ZeroFeat()
+    b.load_state_dict(sd)
+    b = b.to(cuda).train()
+    tb = TR.LDMTrainer(b, [], cuda, lr=1e-3)
+    tb.autocast_enabled = False
+    l1b = tb.train_step(content, style, t=t, noise=noise)
+    for k in ("total_loss", "denoisinsg_loss", "compression_loss"):
+        assert abs(l2[k] - l1b[k]) <= 1e-5 * abs(l1b[k]), (k, l2[k], l1b[k])
+
+
 def test_trainer_step_runs_and_decreases_loss(cuda):
     """LDMTrainer.train_step end to end (GradScaler + Adam + autocast context) on random data."""
     import models.model as M
