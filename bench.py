@@ -47,6 +47,7 @@ def parse():
                          "(config 2), fp16 for transfer (config 5)")
     ap.add_argument("--split", type=int, default=1,
                     help="run the per-GPU batch as this many sub-batch chains on separate streams (one graph)")
+    ap.add_argument("--train-eager", action="store_true", help="train workload: no hipGraph capture of the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -308,6 +309,9 @@ def run_train(args, world, rank, dev, M):
         hdist.broadcast_parameters(ldm)
     trainer = LDMTrainer(ldm, None, dev, lr=1e-4)                 # LDMTrainer default (train.py:142)
     trainer.autocast_dtype = {"fp32": None, "fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    # one rank: the whole step replayed from a hipGraph (LDMTrainer.graph_step; warm-up covers the 2 eager
+    # steps and the capture); with N > 1 the bucketed RCCL all-reduce keeps the step eager
+    trainer.graph_step = not args.train_eager
     if args.dtype == "fp32":
         os.environ["LDM_AMD_DTYPE"] = "fp32"                      # autocast region present, fp32 operands
     ldm.train()
@@ -350,7 +354,9 @@ def run_train(args, world, rank, dev, M):
         "data": "synthetic (U[0,1) content/style mels; random-init weights; t ~ randint on device)",
         "config": {"workload": f"configs 3/4: LDMTrainer.train_step, batch {B}/GPU, 1x128x512 mels, "
                                f"torch.autocast({args.dtype}) region of train.py:174, Adam + GradScaler"
-                               + (f", RCCL bucketed grad all-reduce over {world} ranks" if world > 1 else ""),
+                               + (f", RCCL bucketed grad all-reduce over {world} ranks" if world > 1 else "")
+                               + (", step replayed from one hipGraph (LDMTrainer.graph_step)"
+                                  if trainer._graph is not None else ", eager step"),
                    "global_batch": B * world, "parallelism": f"dp{world}"},
         "roofline": {"kernel": "whole train step (composite)", "bound": "mfma", "achieved": round(achieved, 2),
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),

@@ -392,6 +392,15 @@ int ldm_unscale_check(const ldm_tensor_slot* slots, const int32_t* chunk_tensor,
 int ldm_adam_step(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
                   int32_t nchunks, int32_t chunk_len, double lr, double beta1, double beta2, double eps,
                   double weight_decay, int32_t decoupled, int32_t step, const int32_t* found_inf, void* stream);
+/* The capturable form of ldm_adam_step (hipGraph-captured train steps, LDMTrainer.graph_step): the step
+ * count is the device float step[0], advanced by one only when found_inf[0] == 0 (or found_inf NULL);
+ * the derived scalars are formed from it on the device exactly as ldm_adam_step forms them on the host,
+ * into the caller's 8-float device workspace `scalars`.  Replaces torch.optim.Adam(capturable=True)'s
+ * _single_tensor_adam capturable branch (train.py:156's optimizer when the step is graph-captured). */
+int ldm_adam_step_dev(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                      int32_t nchunks, int32_t chunk_len, double lr, double beta1, double beta2, double eps,
+                      double weight_decay, int32_t decoupled, float* step, const int32_t* found_inf, float* scalars,
+                      void* stream);
 /* scaler.update(): scale *= backoff on inf (tracker = 0), *= growth after growth_interval clean steps. */
 int ldm_update_scale(float* scale, int32_t* growth_tracker, const int32_t* found_inf, float growth_factor,
                      float backoff_factor, int32_t growth_interval, void* stream);

@@ -378,8 +378,10 @@ __device__ __forceinline__ void adam_elem(const AdamScalars& k, float& p, float 
 __global__ __launch_bounds__(256) void adam_kernel(const ldm_tensor_slot* __restrict__ slots,
                                                    const int32_t* __restrict__ chunk_tensor,
                                                    const int64_t* __restrict__ chunk_start, int chunk_len,
-                                                   AdamScalars k, const int32_t* __restrict__ found_inf) {
+                                                   AdamScalars k, const int32_t* __restrict__ found_inf,
+                                                   const AdamScalars* __restrict__ kdev = nullptr) {
     if (found_inf && found_inf[0]) return;   // GradScaler.step skips the update on inf/nan
+    if (kdev) k = *kdev;                     // capturable form: scalars of the device-side step count
     const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
     const int64_t s0 = chunk_start[blockIdx.x];
     const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
@@ -407,6 +409,28 @@ __global__ __launch_bounds__(256) void adam_kernel(const ldm_tensor_slot* __rest
             sl.exp_avg_sq[i] = v;
             sl.param[i] = p;
         });
+}
+
+// Capturable step (hipGraph replay): the step count lives on the device and advances only on applied
+// steps (found_inf clear), and the derived scalars are formed from it exactly as the host form forms them
+// (double, one cast to fp32), so graphed and eager steps are bitwise equal.
+__global__ void adam_prep_kernel(float* step, const int32_t* found_inf, double lr, double beta1, double beta2,
+                                 double eps, double weight_decay, int decoupled, AdamScalars* out) {
+    if (found_inf && found_inf[0]) return;
+    const float st = step[0] + 1.f;
+    step[0] = st;
+    const double bc1 = 1.0 - pow(beta1, (double)st);
+    const double bc2 = 1.0 - pow(beta2, (double)st);
+    AdamScalars k;
+    k.one_m_beta1 = (float)(1.0 - beta1);
+    k.beta2 = (float)beta2;
+    k.one_m_beta2 = (float)(1.0 - beta2);
+    k.eps = (float)eps;
+    k.weight_decay = (float)weight_decay;
+    k.decay_mul = decoupled ? (float)(1.0 - lr * weight_decay) : 1.f;
+    k.step_size = (float)(lr / bc1);
+    k.bc2_sqrt = (float)sqrt(bc2);
+    *out = k;
 }
 
 // torch.amp.GradScaler._amp_update_scale_: backoff on inf, grow after growth_interval clean steps
@@ -579,6 +603,23 @@ extern "C" int ldm_adam_step(const ldm_tensor_slot* slots, const int32_t* chunk_
     k.bc2_sqrt = (float)std::sqrt(bc2);
     hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, slots, chunk_tensor, chunk_start,
                        chunk_len, k, found_inf);
+    LDM_CHECK_LAUNCH("adam_kernel");
+    return 0;
+}
+
+extern "C" int ldm_adam_step_dev(const ldm_tensor_slot* slots, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                                 int32_t nchunks, int32_t chunk_len, double lr, double beta1, double beta2, double eps,
+                                 double weight_decay, int32_t decoupled, float* step, const int32_t* found_inf,
+                                 float* scalars, void* stream) {
+    LDM_REQUIRE(slots && chunk_tensor && chunk_start && nchunks >= 0 && step && scalars, "adam_step_dev: bad argument");
+    static_assert(sizeof(AdamScalars) == 8 * sizeof(float), "AdamScalars is 8 floats");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step, found_inf, lr, beta1, beta2, eps, weight_decay,
+                       (int)decoupled, reinterpret_cast<AdamScalars*>(scalars));
+    LDM_CHECK_LAUNCH("adam_prep_kernel");
+    if (nchunks == 0) return 0;
+    hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, st, slots, chunk_tensor, chunk_start, chunk_len,
+                       AdamScalars{}, found_inf, reinterpret_cast<const AdamScalars*>(scalars));
     LDM_CHECK_LAUNCH("adam_kernel");
     return 0;
 }

@@ -142,6 +142,9 @@ SIGNATURES = {
     "ldm_unscale_check": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, c_fp, c_vp, c_vp]),
     "ldm_adam_step": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int32, c_int32, c_vp, c_vp]),
+    "ldm_adam_step_dev": (c_int32, [c_vp, c_vp, c_vp, c_int32, c_int32, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int32, c_fp, c_vp, c_fp,
+                                    c_vp]),
     "ldm_update_scale": (c_int32, [c_fp, c_vp, c_vp, c_float, c_float, c_int32, c_vp]),
 }
 

@@ -28,6 +28,8 @@ class _SlotTable:
 
     _cache = {}
     _maps = {}
+    _captured = []
+    _reserve = []
 
     def __new__(cls, params, grads, m, v):
         key = tuple((p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(), 0 if b is None else b.data_ptr(),
@@ -48,8 +50,18 @@ class _SlotTable:
             mp = (torch.from_numpy(ct).to(dev), torch.from_numpy(cs).to(dev), int(len(ct)))
             cls._maps[(dev, numels)] = mp
         self.chunk_tensor, self.chunk_start, self.nchunks = mp
-        host = torch.from_numpy(rows).pin_memory()        # caching host allocator: reused once the copy ran
         self.slots = torch.empty(rows.shape, dtype=torch.int64, device=dev)
+        if torch.cuda.is_current_stream_capturing():
+            # no host allocation may run inside a capture, and a captured copy re-reads its host buffer at
+            # every replay: take one of the pinned buffers reserved before the capture and keep it for good
+            if not cls._reserve or cls._reserve[-1].numel() < rows.size:
+                raise RuntimeError("ldm_amd.optim: call reserve_capture_buffers() before capturing an optimizer step")
+            host = cls._reserve.pop()[:rows.size].view(rows.shape)
+            host.copy_(torch.from_numpy(rows))
+            self._host = host
+            cls._captured.append(self)
+        else:
+            host = torch.from_numpy(rows).pin_memory()    # caching host allocator: reused once the copy ran
         self.slots.copy_(host, non_blocking=True)
         self.key = key
         if len(cls._cache) > 64:
@@ -59,6 +71,13 @@ class _SlotTable:
 
     def __init__(self, *args):
         pass
+
+
+def reserve_capture_buffers(n=4, words=1 << 14):
+    """Pinned host buffers for the slot tables built while a step is being captured into a hipGraph (one
+    per optimizer / unscale table in the step); call before torch.cuda.graph."""
+    while len(_SlotTable._reserve) < n:
+        _SlotTable._reserve.append(torch.empty(words, dtype=torch.int64, pin_memory=True))
 
 
 def scale_tensors_(tensors, factor):
@@ -91,7 +110,8 @@ class Adam(torch.optim.Optimizer):
 
     _decoupled = 0
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
+                 capturable=False):
         if amsgrad:
             raise NotImplementedError("ldm_amd.optim.Adam: amsgrad is not supported")
         if not 0.0 <= lr:
@@ -102,6 +122,9 @@ class Adam(torch.optim.Optimizer):
             raise ValueError(f"Invalid beta parameters: {betas}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
         self._tables = {}
+        # capturable (torch.optim.Adam(capturable=True)): the step count is a device tensor advanced by the
+        # kernel itself, so step() never reads it on the host and can be captured into a hipGraph
+        self.capturable = bool(capturable)
 
     @torch.no_grad()
     def step(self, closure=None, found_inf=None):
@@ -115,6 +138,10 @@ class Adam(torch.optim.Optimizer):
             if not params:
                 continue
             _check_params(params)
+            beta1, beta2 = group["betas"]
+            if self.capturable:
+                self._step_capturable(gi, group, params, found_inf, beta1, beta2)
+                continue
             # group the params by their step count (all equal unless params were added later)
             by_step = {}
             for p in params:
@@ -125,7 +152,6 @@ class Adam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
                 by_step.setdefault(int(st["step"].item()), []).append(p)
-            beta1, beta2 = group["betas"]
             for step, ps in by_step.items():
                 grads = [p.grad for p in ps]
                 tab = _SlotTable(ps, grads, [self.state[p]["exp_avg"] for p in ps],
@@ -144,13 +170,45 @@ class Adam(torch.optim.Optimizer):
         return loss
 
 
+    def _step_capturable(self, gi, group, params, found_inf, beta1, beta2):
+        """One launch pair for the group: ldm_adam_step_dev advances the group's device step count (shared
+        by its params' state["step"]) unless found_inf is set and forms the scalars from it on the device."""
+        dev = params[0].device
+        gstep = group.get("_ldm_step")
+        if gstep is None:
+            prev = [self.state[p]["step"] for p in params if len(self.state[p]) > 0]
+            init = float(prev[0]) if prev else 0.0
+            if any(float(s) != init for s in prev):
+                raise RuntimeError("ldm_amd.optim.Adam(capturable=True): params of a group at different steps")
+            gstep = torch.full((), init, dtype=torch.float32, device=dev)
+            group["_ldm_step"] = gstep
+            group["_ldm_scalars"] = torch.zeros(8, dtype=torch.float32, device=dev)
+        for p in params:
+            st = self.state[p]
+            if len(st) == 0 or "exp_avg" not in st:
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] = gstep
+        tab = _SlotTable(params, [p.grad for p in params], [self.state[p]["exp_avg"] for p in params],
+                         [self.state[p]["exp_avg_sq"] for p in params])
+        L.call("ldm_adam_step_dev", tab.slots.data_ptr(), tab.chunk_tensor.data_ptr(), tab.chunk_start.data_ptr(),
+               tab.nchunks, CHUNK, float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+               float(group["weight_decay"]), self._decoupled, gstep.data_ptr(),
+               None if found_inf is None else found_inf.data_ptr(), group["_ldm_scalars"].data_ptr(), stream_handle())
+        self._tables[(gi, "dev")] = tab
+        for p in params:
+            torch.autograd.graph.increment_version(p)
+
+
 class AdamW(Adam):
     """torch.optim.AdamW (decoupled weight decay, default 1e-2)."""
 
     _decoupled = 1
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
-        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad)
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
+                 capturable=False):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
+                         capturable=capturable)
 
 
 class GradScaler:
@@ -218,6 +276,9 @@ class GradScaler:
         self.unscale_(optimizer)
         for group in optimizer.param_groups:
             group.pop("_ldm_tabs", None)
+        if getattr(optimizer, "capturable", False):
+            # device-side skip: the kernel pair reads found_inf and leaves the step count alone on inf/nan
+            return optimizer.step(*args, found_inf=self._found_inf, **kwargs)
         # torch's GradScaler also syncs here (found_inf.item()) so that the optimiser's step counters
         # only advance on applied steps
         if int(self._found_inf.item()) == 0:

@@ -150,6 +150,13 @@ class LDMTrainer:
         # bfloat16 = BASELINE config 3); the HIP convs then round their operands to it (ldm_capi.h LDM_DT_*)
         self.autocast_dtype = None
         self.autocast_enabled = True
+        # graph_step = True: after graph_warmup eager steps, the whole step (forward, backward, unscale,
+        # optimizer, scaler update) is captured once into a hipGraph and replayed; the loss values are read
+        # after each replay.  Single-process only (the bucketed RCCL all-reduce stays eager).
+        self.graph_step = False
+        self.graph_warmup = 2
+        self._graph = None
+        self._graph_calls = 0
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", factor=0.5,
                                                                     patience=10)
         self.reducer = None
@@ -165,6 +172,12 @@ class LDMTrainer:
     def train_step(self, content_spec, style_spec, t=None, noise=None):
         """One step (reference train.py:163-208).  t / noise may be injected (parity tests); by default
         they are drawn like the reference (randint on the device; randn_like inside the scheduler)."""
+        if self.graph_step and self.device.type == "cuda" and self.reducer is None:
+            return self._graphed_step(content_spec, style_spec, t, noise)
+        return self._losses(self._step(content_spec, style_spec, t, noise))
+
+    def _step(self, content_spec, style_spec, t, noise):
+        """The step's device work; returns the four loss tensors (no host synchronisation)."""
         self.optimizer.zero_grad()
         content_spec = content_spec.float()
         style_spec = style_spec.float()
@@ -187,12 +200,42 @@ class LDMTrainer:
             self.reducer.finish()
         self.scaler.step(self.optimizer)
         self.scaler.update()
+        return compression_loss_, denoisinsg_loss, style_loss_, total_loss
+
+    @staticmethod
+    def _losses(t4):
+        c, d, s, tot = t4
         return {
-            "compression_loss": compression_loss_.item(),
-            "denoisinsg_loss": denoisinsg_loss.item(),
-            "style_loss": style_loss_.item(),
-            "total_loss": total_loss.item(),
+            "compression_loss": c.item(),
+            "denoisinsg_loss": d.item(),
+            "style_loss": s.item(),
+            "total_loss": tot.item(),
         }
+
+    def _graphed_step(self, content_spec, style_spec, t, noise):
+        """train_step as one hipGraph replay.  The optimizer runs its capturable form (device step count,
+        device-side inf/nan skip: ldm_adam_step_dev), so nothing in the step reads the device from the host;
+        t / noise are drawn inside the graph (torch's graph-safe Philox offsets) unless injected, in which
+        case every later call must inject them too (they are copied into the captured input buffers)."""
+        self.optimizer.capturable = True
+        args = (content_spec, style_spec, t, noise)
+        sig = tuple(None if a is None else (tuple(a.shape), a.dtype) for a in args)
+        if self._graph is None or self._graph_sig != sig:
+            if self._graph_calls < self.graph_warmup:
+                self._graph_calls += 1
+                return self._losses(self._step(*args))
+            static = [None if a is None else a.detach().clone() for a in args]
+            hoptim.reserve_capture_buffers()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs = self._step(*static)
+            self._graph, self._graph_in, self._graph_out, self._graph_sig = g, static, outs, sig
+        for dst, src in zip(self._graph_in, args):
+            if dst is not None:
+                dst.copy_(src)
+        self._graph.replay()
+        return self._losses(self._graph_out)
 
     def train_epoch(self, epoch):
         self.model.train()

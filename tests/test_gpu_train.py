@@ -322,6 +322,57 @@ def test_second_step_uses_updated_weights(cuda):
         assert abs(l2[k] - l1b[k]) <= 1e-5 * abs(l1b[k]), (k, l2[k], l1b[k])
 
 
+@pytest.mark.parametrize("autocast", [False, True])
+def test_graphed_train_step_equals_eager(cuda, autocast):
+    """LDMTrainer.graph_step: 2 eager warm-up steps, then the step captured into a hipGraph and replayed.
+    With injected t / noise the five steps' losses and the final parameters and BN buffers equal an eager
+    trainer's bitwise (same kernels; the capturable Adam forms its scalars from the device step count
+    exactly as the host form does); under autocast too."""
+    import models.model as M
+    import models.train as TR
+    content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 860)).to(cuda)
+    style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 861)).to(cuda)
+    t = torch.tensor([10, 150], device=cuda)
+    noise = torch.from_numpy(recipe.normal((2, 32, 16, 16), 862)).to(cuda)
+    res = []
+    for graph in (False, True):
+        m = M.LDM(32, pretrained_path="")
+        recipe.fill_module(m, seed=700)
+        m.feature_loss_net = _ZeroFeat()
+        m = m.to(cuda).train()
+        tr = TR.LDMTrainer(m, [], cuda, lr=1e-3)
+        tr.autocast_enabled = autocast
+        tr.graph_step = graph
+        losses = [tr.train_step(content, style, t=t, noise=noise) for _ in range(5)]
+        assert (tr._graph is not None) == graph
+        res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    (le, sde), (lg, sdg) = res
+    for a, b in zip(le, lg):
+        for k in a:
+            assert a[k] == b[k], (k, a[k], b[k])
+    for k in sde:
+        assert torch.equal(sde[k], sdg[k]), k
+
+
+def test_graphed_train_step_draws_t_and_noise(cuda):
+    """graph_step with t / noise drawn inside the graph: replays advance the RNG (losses differ step to
+    step) and training proceeds (finite, decreasing over 8 steps)."""
+    import models.model as M
+    import models.train as TR
+    torch.manual_seed(0)
+    m = M.LDM(32, pretrained_path="")
+    m.feature_loss_net = _ZeroFeat()
+    m = m.to(cuda).train()
+    tr = TR.LDMTrainer(m, [], cuda, lr=1e-3)
+    tr.graph_step = True
+    content = torch.rand(4, 1, 128, 128, device=cuda)
+    style = torch.rand(4, 1, 128, 128, device=cuda)
+    losses = [tr.train_step(content, style)["total_loss"] for _ in range(8)]
+    assert tr._graph is not None and all(np.isfinite(losses))
+    assert len(set(losses[2:])) == len(losses[2:])
+    assert np.mean(losses[-3:]) < np.mean(losses[:3])
+
+
 def test_trainer_step_runs_and_decreases_loss(cuda):
     """LDMTrainer.train_step end to end (GradScaler + Adam + autocast context) on random data."""
     import models.model as M
