@@ -9,7 +9,7 @@ mkdir -p "$ROOT/$OUT"
 cd /tmp && export TMPDIR=/tmp
 run() {
   timeout -s KILL 120 rocprofv3 --pmc $1 --output-format csv -d "$ROOT/$OUT/$2" -o p -- \
-    python3 "$ROOT/bench.py" --workload train --steps 2 --warmup 1 --no-cpu-baseline > "$ROOT/$OUT/$2.log" 2>&1 \
+    python3 "$ROOT/bench.py" --workload train --steps 2 --warmup 1 --no-cpu-baseline --train-eager > "$ROOT/$OUT/$2.log" 2>&1 \
     || { echo "pass $2 failed"; tail -5 "$ROOT/$OUT/$2.log"; exit 1; }
 }
 run "FETCH_SIZE" fetch

@@ -24,8 +24,9 @@ def load(d, name):
 
 
 def short(n):
-    n = re.sub(r"\(.*", "", n).replace("void ", "")
-    return re.sub(r"^ldm::(\(anonymous namespace\)::|wg::)?", "", n)
+    n = n.replace("void ", "").replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
+    return re.sub(r"^ldm::(wg::|tc::)?", "", n)
 
 
 def main(d):
