@@ -332,7 +332,6 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
 // MFMA maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j] and
 // B[k = 8h + j][col r]; D col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4h.
 // ------------------------------------------------------------------------------------------------------
-constexpr int kLQ = 32;    // positions per chunk
 constexpr int kLC = 32;    // gathered channels per block
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
@@ -358,12 +357,19 @@ struct LpArgs {
 };
 
 __host__ __device__ constexpr int lp_nb(int S, int KK) { return (3 + 7 * S + KK + 3) / 4; }   // b128 reads per k-step
-__host__ __device__ inline int lp_buf_floats(int bm, int pitch_c) { return bm * kLQ + (kLC * pitch_c + 255) / 256 * 256; }
-__host__ __device__ constexpr int lp_swz(int row) { return (row >> 1) & 7; }
+__host__ __device__ inline int lp_buf_floats(int bm, int qc, int pitch_c) {
+    return bm * qc + (kLC * pitch_c + 255) / 256 * 256;
+}
+// XOR swizzle of a Dense row's 16-B pieces (PPR per row): 16 consecutive rows' fragment reads land on
+// distinct bank groups
+template <int PPR>
+__host__ __device__ constexpr int lp_swz(int row) { return (row >> 1) & (PPR - 1); }
 
-template <int S, int KK, int BM, int WM, int DT>
+// QC positions per chunk: 32 (two k-steps), or 16 (one; the 2 x 8 planes of the UNet bottom)
+template <int S, int KK, int BM, int WM, int QC, int DT>
 __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
     constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp_nb(S, KK);
+    constexpr int PPR = QC / 4, RPI = 64 / PPR, NKS = QC / 16;   // pieces per row, rows per DMA instr, k-steps
     static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63;
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
     const int r = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.y * BM, c0 = blockIdx.x * kLC;
     const int HQ = a.Hq * a.Wq;
-    const int bufF = lp_buf_floats(BM, a.pitch_c);
+    const int bufF = lp_buf_floats(BM, QC, a.pitch_c);
     const int ch_begin = blockIdx.z * a.per_split;
     const int ch_end = min(a.nchunk, ch_begin + a.per_split);
     const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
@@ -388,14 +394,14 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
         if (a.cols == a.Wq) {
             qy0 = rr * a.rows, qx0 = 0;
         } else {
-            const int segs = a.Wq / kLQ;
-            qy0 = rr / segs, qx0 = (rr - qy0 * segs) * kLQ;
+            const int segs = a.Wq / QC;
+            qy0 = rr / segs, qx0 = (rr - qy0 * segs) * QC;
         }
         char* base = reinterpret_cast<char*>(smem + buf * bufF);
-        // Dense: BM rows x 8 pieces; one wave-instruction = 8 rows
-        for (int gi = wave; gi < BM / 8; gi += NW) {
-            const int row = gi * 8 + (lane >> 3);
-            const int sp = (lane & 7) ^ lp_swz(row);        // source piece landing in destination piece lane & 7
+        // Dense: BM rows x PPR pieces; one wave-instruction = RPI rows
+        for (int gi = wave; gi < BM / RPI; gi += NW) {
+            const int row = gi * RPI + lane / PPR;
+            const int sp = (lane % PPR) ^ lp_swz<PPR>(row);   // source piece landing in destination piece lane % PPR
             const int ql = sp * 4;
             const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
             const int m = m0 + row;
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
             const bool ok = pc < npiece && c < a.C && wrow < a.wr && (unsigned)iy < (unsigned)a.Hg &&
                             (unsigned)ix < (unsigned)a.Wg;
             const int voff = ok ? ((((b * a.C + c) * a.Hg + iy) * a.Wg + ix) * 4) : kOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + BM * kLQ * 4 + gi * 1024), 16, voff, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + BM * QC * 4 + gi * 1024), 16, voff, 0, 0, 0);
         }
     };
 
@@ -428,18 +434,18 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
             for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
 
     // per-lane LDS offsets (floats) inside a buffer for k-step ks: A pieces of fragment f, window run start
-    int aoff[2][MF][2], boff[2];
+    int aoff[NKS][MF][2], boff[NKS];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < NKS; ++ks) {
         const int q0 = ks * 16 + 8 * h;
         const int rl = q0 / a.cols, xl0 = q0 - rl * a.cols;
 #pragma unroll
         for (int f = 0; f < MF; ++f) {
             const int row = (wm * MF + f) * 32 + r;
 #pragma unroll
-            for (int u = 0; u < 2; ++u) aoff[ks][f][u] = row * kLQ + ((((q0 >> 2) + u) ^ lp_swz(row)) << 2);
+            for (int u = 0; u < 2; ++u) aoff[ks][f][u] = row * QC + ((((q0 >> 2) + u) ^ lp_swz<PPR>(row)) << 2);
         }
-        boff[ks] = BM * kLQ + r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S;
+        boff[ks] = BM * QC + r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S;
     }
 
     if (ch_begin < ch_end) issue(ch_begin, 0);
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
         if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
         const float* sb = smem + buf * bufF;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < NKS; ++ks) {
             floatx8 fa[MF];
 #pragma unroll
             for (int f = 0; f < MF; ++f) {
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
 }
 
 struct LpPlan {
-    int S, KK, BM, WM, splits, lds_bytes;
+    int S, KK, BM, WM, QC, splits, lds_bytes;
     LpArgs a;
 };
 
@@ -515,16 +521,21 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
         a.M = d.Cin, a.C = d.Cout, a.Hq = d.Hin, a.Wq = d.Win, a.Hg = d.Hout, a.Wg = d.Wout;
     }
     if (a.C < 16 || a.Wg % 4) return false;
-    if (a.Wq == 16) {
-        if (a.Hq % 2) return false;
+    int qc = 32;
+    if (a.Wq % 32 == 0) {
+        a.cols = 32, a.rows = 1;
+    } else if (a.Wq == 16 && a.Hq % 2 == 0) {
         a.cols = 16, a.rows = 2;
-    } else if (a.Wq % kLQ == 0) {
-        a.cols = kLQ, a.rows = 1;
+    } else if (a.Wq == 16) {
+        qc = 16, a.cols = 16, a.rows = 1;
+    } else if (a.Wq == 8 && a.Hq % 2 == 0) {
+        qc = 16, a.cols = 8, a.rows = 2;
     } else {
         return false;
     }
     const int S = d.stride, KK = d.kh;
-    a.cps = a.Hq * a.Wq / kLQ;
+    p.QC = qc;
+    a.cps = a.Hq * a.Wq / qc;
     a.nchunk = a.B * a.cps;
     a.wr = (a.rows - 1) * S + KK;
     a.wca = (3 + (a.cols - 1) * S + KK + 3) / 4 * 4;
@@ -534,7 +545,7 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     p.S = S, p.KK = KK;
     p.BM = a.M >= 128 ? 128 : (a.M > 32 ? 64 : 32);
     p.WM = p.BM == 128 ? 2 : 1;
-    p.lds_bytes = 2 * lp_buf_floats(p.BM, a.pitch_c) * 4;
+    p.lds_bytes = 2 * lp_buf_floats(p.BM, qc, a.pitch_c) * 4;
     if (p.lds_bytes > 160 * 1024) return false;
     const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + kLC - 1) / kLC);
     int s = 1;
@@ -545,9 +556,9 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     return true;
 }
 
-template <int S, int KK, int BM, int WM, int DT>
+template <int S, int KK, int BM, int WM, int QC, int DT>
 int launch_lp_dt(const LpPlan& p, hipStream_t st) {
-    auto kfn = wgrad_lp_kernel<S, KK, BM, WM, DT>;
+    auto kfn = wgrad_lp_kernel<S, KK, BM, WM, QC, DT>;
     static bool opted = false;
     if (!opted) {
         LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -558,21 +569,25 @@ int launch_lp_dt(const LpPlan& p, hipStream_t st) {
     LDM_CHECK_LAUNCH("wgrad_lp_kernel");
     return 0;
 }
-template <int S, int KK, int DT>
+template <int S, int KK, int QC, int DT>
 int launch_lp_bm(const LpPlan& p, hipStream_t st) {
     switch (p.BM) {
-        case 128: return launch_lp_dt<S, KK, 128, 2, DT>(p, st);
-        case 64: return launch_lp_dt<S, KK, 64, 1, DT>(p, st);
-        default: return launch_lp_dt<S, KK, 32, 1, DT>(p, st);
+        case 128: return launch_lp_dt<S, KK, 128, 2, QC, DT>(p, st);
+        case 64: return launch_lp_dt<S, KK, 64, 1, QC, DT>(p, st);
+        default: return launch_lp_dt<S, KK, 32, 1, QC, DT>(p, st);
     }
+}
+template <int S, int KK, int DT>
+int launch_lp_qc(const LpPlan& p, hipStream_t st) {
+    return p.QC == 16 ? launch_lp_bm<S, KK, 16, DT>(p, st) : launch_lp_bm<S, KK, 32, DT>(p, st);
 }
 template <int DT>
 int launch_lp(const LpPlan& p, hipStream_t st) {
     switch (p.S * 10 + p.KK) {
-        case 13: return launch_lp_bm<1, 3, DT>(p, st);
-        case 23: return launch_lp_bm<2, 3, DT>(p, st);
-        case 14: return launch_lp_bm<1, 4, DT>(p, st);
-        default: return launch_lp_bm<2, 4, DT>(p, st);
+        case 13: return launch_lp_qc<1, 3, DT>(p, st);
+        case 23: return launch_lp_qc<2, 3, DT>(p, st);
+        case 14: return launch_lp_qc<1, 4, DT>(p, st);
+        default: return launch_lp_qc<2, 4, DT>(p, st);
     }
 }
 

@@ -217,6 +217,10 @@ WGRAD_LP_CASES = {
     "k4s2_convT_m128": (2, 128, 16, 64, 64, 4, 2, 1, 0, True),     # decoder convT 128 -> 64, BM 128
     "k3s2_convT_op1": (2, 64, 8, 32, 32, 3, 2, 1, 1, True),        # UNet decoder convT (k3 s2 op1)
     "ragged_m40_c48": (3, 48, 8, 32, 40, 3, 1, 1, 0, False),       # M, C not multiples of the tiles
+    "k3s1_bottleneck_2x8": (4, 512, 2, 8, 512, 3, 1, 1, 0, False),  # 16-position chunks (2 rows of 8)
+    "k3s2_to_2x8": (4, 256, 4, 16, 512, 3, 2, 1, 0, False),         # UNet enc4: output 2 x 8
+    "k3s2_convT_from_2x8": (4, 512, 2, 8, 256, 3, 2, 1, 1, True),   # UNet dec4: input grid 2 x 8
+    "k3s2_wq16_odd_rows": (2, 64, 6, 32, 64, 3, 2, 1, 0, False),    # 3 x 16 output: one 16-wide row per chunk
 }
 
 
