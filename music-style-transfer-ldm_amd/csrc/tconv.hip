@@ -159,20 +159,21 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     float gv[2][16];
     gather(0, gv[0]);
     loadA(0, aset[0]);
-    if (nch > 1) loadA(1, aset[1]);
+    loadA(min(1, nch - 1), aset[1]);
     stage(0, gv[0]);
     __syncthreads();
-    if (nch > 1) gather(1, gv[0]);
+    gather(min(1, nch - 1), gv[0]);
     // step c (G = c % 2, A = c % 3, compile-time so every register set is named, never copied): chunk
     // c+2's weights and gather are issued, chunk c is multiplied, chunk c+1's gather (issued one step
     // earlier, in gv[G]) is staged; weights are consumed two steps after their loads, gathers one
     auto step = [&](int c, auto Gc, auto Ac) {
         constexpr int G = decltype(Gc)::value, A = decltype(Ac)::value;
         const int buf = c & 1;
-        if (c + 2 < nch) {
-            loadA(c + 2, aset[(A + 2) % 3]);
-            gather(c + 2, gv[G ^ 1]);
-        }
+        // unconditional (clamped past the end: a harmless re-load), so that every step issues the same
+        // loads and the waitcnt pass can count them exactly across the unrolled steps
+        const int c2 = min(c + 2, nch - 1);
+        loadA(c2, aset[(A + 2) % 3]);
+        gather(c2, gv[G ^ 1]);
         const unsigned short* bs = bt[buf];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -190,19 +191,26 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
                         acc[i][j] = mma<DT>(aset[A][i][s], bf[j], acc[i][j]);
                 }
         }
-        if (c + 1 < nch) stage(buf ^ 1, gv[G]);
+        stage(buf ^ 1, gv[G]);   // past the end it fills the idle buffer, which nothing reads
         __syncthreads();
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
-    for (int c = 0; c < nch; c += 6) {
+    // exits only right after a step, so the only path into a step is the one through the step before it
+    for (int c = 0;; c += 6) {
         step(c, I0{}, I0{});
-        if (c + 1 < nch) step(c + 1, I1{}, I1{});
-        if (c + 2 < nch) step(c + 2, I0{}, I2{});
-        if (c + 3 < nch) step(c + 3, I1{}, I0{});
-        if (c + 4 < nch) step(c + 4, I0{}, I1{});
-        if (c + 5 < nch) step(c + 5, I1{}, I2{});
+        if (c + 1 >= nch) break;
+        step(c + 1, I1{}, I1{});
+        if (c + 2 >= nch) break;
+        step(c + 2, I0{}, I2{});
+        if (c + 3 >= nch) break;
+        step(c + 3, I1{}, I0{});
+        if (c + 4 >= nch) break;
+        step(c + 4, I0{}, I1{});
+        if (c + 5 >= nch) break;
+        step(c + 5, I1{}, I2{});
+        if (c + 6 >= nch) break;
     }
 
     // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store
