@@ -1077,6 +1077,85 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
     }
 }
 
+// The same layer with two input rows per lane (four output rows x 8 columns): per input channel a lane
+// reads its four window rows as one 16-byte run plus the two border columns (12 loads for two rows instead
+// of 36 single-float gathers), and the channel loop keeps two channels of loads in flight.  Hin even.
+__global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
+    const int W4 = a.Win >> 2, H2 = a.Hin >> 1;
+    const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (idx >= a.B * H2 * W4) return;
+    const int r = a.fd_dwo.div(idx);   // fd_dwo = W4
+    const int qx0 = (idx - r * W4) * 4;
+    const int b = a.fd_dho.div(r);     // fd_dho = Hin / 2
+    const int qy0 = (r - b * H2) * 2;
+    const int HW = a.Hin * a.Win;
+    float acc[2][2][8];   // [input row][ry][2 jj + rx]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[u][i][j] = 0.f;
+    bool rok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rok[i] = (unsigned)(qy0 - 1 + i) < (unsigned)a.Hin;
+    const bool lok = qx0 > 0, hok = qx0 + 4 < a.Win;
+    const float* xp = a.x + (size_t)b * a.Cin * HW + (qy0 - 1) * a.Win + qx0;
+    auto load = [&](const float* p, float (&xr)[4][6]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float* row = p + i * a.Win;
+            const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
+            xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
+            xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+        }
+    };
+    auto mac = [&](const float (&xr)[4][6], const float* wq) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+                for (int rx = 0; rx < 2; ++rx)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int ia = t >> 1, ib = t & 1;
+                        const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
+                        const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
+                    }
+    };
+    float xa[4][6], xb[4][6];
+    int ci = 0;
+    for (; ci + 1 < a.Cin; ci += 2, xp += 2 * HW) {   // channel order kept: ci, then ci + 1
+        load(xp, xa);
+        load(xp + HW, xb);
+        mac(xa, a.w + ci * 16);
+        mac(xb, a.w + (ci + 1) * 16);
+    }
+    if (ci < a.Cin) {
+        load(xp, xa);
+        mac(xa, a.w + ci * 16);
+    }
+    const ChanEpi ce = chan_epi(a, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry) {
+            const size_t o = ((size_t)b * a.Hout + 2 * (qy0 + u) + ry) * a.Wout + 2 * qx0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[u][ry][4 * h + j]);
+                store4(a, o + 4 * h, v);
+            }
+        }
+}
+
 // ------------------------------------------------------------------------------------------------
 // weight packing into fragment order: packed[phase][chunk][Mpad][NLG][4], k = chunk*CK + NLG*j + lg
 // ------------------------------------------------------------------------------------------------
@@ -1400,6 +1479,13 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             d.out_pad == 0 && d.Win % 4 == 0 && a.pt.nphase == 4 && ((uintptr_t)y & 15) == 0 &&
             (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Win / 4);
+            if (d.Hin % 2 == 0) {
+                a.fd_dho = FastDiv::make(d.Hin / 2);
+                const int64_t lanes = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
+                hipLaunchKernelGGL(convT4_cout1_r2_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+                LDM_CHECK_LAUNCH("convT4_cout1_r2_kernel");
+                return 0;
+            }
             a.fd_dho = FastDiv::make(d.Hin);
             const int64_t lanes = (int64_t)d.B * d.Hin * (d.Win / 4);
             hipLaunchKernelGGL(convT4_cout1_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
