@@ -1,12 +1,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/g23; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_train.py tests/test_gpu_amp.py -q --timeout 200 --timeout-method thread > $O/t.log 2>&1; rc=$?
+O=gpurun_out/g24; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bench_config.py tests/test_gpu_step_kernels.py -q --timeout 200 --timeout-method thread > $O/t.log 2>&1; rc=$?
 tail -3 $O/t.log; grep "^FAILED" $O/t.log | head
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python -u tools/time_conv.py bf16 > $O/conv.log 2>&1 || { tail $O/conv.log; exit 1; }
-grep dec3 $O/conv.log
-for i in 1 2; do
-timeout -k 10 240 python -u bench.py --workload train --steps 20 --warmup 3 --no-cpu-baseline > $O/train$i.json 2> $O/train.err || { tail -20 $O/train.err; exit 1; }
-grep -o '"ms_per_step": [0-9.]*' $O/train$i.json
-done
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/bench.json')); print(d['value'], d['us_per_denoise_iteration'], {k: v['us'] for k, v in d['kernels'].items()})"
