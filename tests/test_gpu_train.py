@@ -354,6 +354,43 @@ def test_graphed_train_step_equals_eager(cuda, autocast):
         assert torch.equal(sde[k], sdg[k]), k
 
 
+def test_graphed_train_step_inf_skips_like_eager(cuda):
+    """GradScaler's inf/nan skip inside the graph: step 4 of 7 gets a non-finite noise target, so its
+    gradients are non-finite; Adam must skip it (capturable form: on the device, step count held) and the
+    scale back off once, exactly as the eager step with its host-side found_inf read.  Bitwise equal."""
+    import models.model as M
+    import models.train as TR
+    content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 870)).to(cuda)
+    style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 871)).to(cuda)
+    t = torch.tensor([30, 170], device=cuda)
+    noise = torch.from_numpy(recipe.normal((2, 32, 16, 16), 872)).to(cuda)
+    bad = noise.clone()
+    bad[0, 0, 0, 0] = float("inf")
+    seq = [noise, noise, noise, bad, noise, noise, noise]
+    res = []
+    for graph in (False, True):
+        m = M.LDM(32, pretrained_path="")
+        recipe.fill_module(m, seed=700)
+        m.feature_loss_net = _ZeroFeat()
+        m = m.to(cuda).train()
+        tr = TR.LDMTrainer(m, [], cuda, lr=1e-3)
+        tr.autocast_enabled = False
+        tr.graph_step = graph
+        losses = [tr.train_step(content, style, t=t, noise=nz) for nz in seq]
+        assert (tr._graph is not None) == graph
+        res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}, tr.scaler.get_scale()))
+    (le, sde, se), (lg, sdg, sg) = res
+    assert se == sg == 2.0 ** 15, (se, sg)
+    assert not np.isfinite(le[3]["total_loss"]) and all(np.isfinite(le[i]["total_loss"]) for i in (4, 5, 6))
+    for a, b in zip(le, lg):
+        for k in a:
+            assert a[k] == b[k] or (np.isnan(a[k]) and np.isnan(b[k])), (k, a[k], b[k])
+    for k in sde:   # (the non-finite step also reaches the BN running statistics, as in torch)
+        a, b = sde[k], sdg[k]
+        same = (a == b) | (torch.isnan(a) & torch.isnan(b)) if a.is_floating_point() else a == b
+        assert bool(same.all()), k
+
+
 def test_graphed_train_step_draws_t_and_noise(cuda):
     """graph_step with t / noise drawn inside the graph: replays advance the RNG (losses differ step to
     step) and training proceeds (finite, decreasing over 8 steps)."""
