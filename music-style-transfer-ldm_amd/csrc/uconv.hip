@@ -64,6 +64,11 @@ __host__ __device__ constexpr int tphase(int t) { return (tky(t) != 1 ? 2 : 0) +
 #ifndef UCONV_DIAG
 #define UCONV_DIAG 0
 #endif
+// cache policy of the activation (B operand) loads: 0 default; experiment builds set 2 (nt: streamed, so that
+// they do not push the layer weights out of the XCD's L2 between iterations)
+#ifndef UCONV_XAUX
+#define UCONV_XAUX 0
+#endif
 #if (UCONV_DIAG & 4)
 __device__ unsigned long long g_uconv_stamps[4096][5];
 #define UCONV_STAMP(k)                                                                                 \
@@ -184,7 +189,7 @@ void uconv_kernel(UArgs a) {
             for (int ni = 0; ni < TN; ++ni)
                 fb[bf][i][ni] = (UCONV_DIAG & 2) ? floatx4{(float)vt[t][ni], 1.f, 2.f, 3.f}
                                                  : __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                                   xr, vt[t][ni], sb0 + cc * 64, 0));
+                                                                                   xr, vt[t][ni], sb0 + cc * 64, UCONV_XAUX));
             __builtin_amdgcn_sched_barrier(0);        // chunks issue in consumption order
         });
     };
