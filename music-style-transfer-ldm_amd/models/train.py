@@ -219,7 +219,11 @@ class LDMTrainer:
         case every later call must inject them too (they are copied into the captured input buffers)."""
         self.optimizer.capturable = True
         args = (content_spec, style_spec, t, noise)
-        sig = tuple(None if a is None else (tuple(a.shape), a.dtype) for a in args)
+        # host scalars the capture bakes into the graph (the optimizer's hyper-parameters: ReduceLROnPlateau
+        # moves lr between epochs; the style-loss weight): a change re-captures
+        hyper = tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in self.optimizer.param_groups)
+        sig = tuple(None if a is None else (tuple(a.shape), a.dtype) for a in args) + (
+            hyper, self.style_loss_weight, self.autocast_enabled, self.autocast_dtype)
         if self._graph is None or self._graph_sig != sig:
             if self._graph_calls < self.graph_warmup:
                 self._graph_calls += 1

@@ -325,9 +325,9 @@ def test_second_step_uses_updated_weights(cuda):
 @pytest.mark.parametrize("autocast", [False, True])
 def test_graphed_train_step_equals_eager(cuda, autocast):
     """LDMTrainer.graph_step: 2 eager warm-up steps, then the step captured into a hipGraph and replayed.
-    With injected t / noise the five steps' losses and the final parameters and BN buffers equal an eager
+    With injected t / noise the eight steps' losses and the final parameters and BN buffers equal an eager
     trainer's bitwise (same kernels; the capturable Adam forms its scalars from the device step count
-    exactly as the host form does); under autocast too."""
+    exactly as the host form does); under autocast too; a learning-rate change after step 5 re-captures."""
     import models.model as M
     import models.train as TR
     content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 860)).to(cuda)
@@ -345,6 +345,9 @@ def test_graphed_train_step_equals_eager(cuda, autocast):
         tr.graph_step = graph
         losses = [tr.train_step(content, style, t=t, noise=noise) for _ in range(5)]
         assert (tr._graph is not None) == graph
+        # a learning-rate change (ReduceLROnPlateau between epochs) must reach the graphed step too
+        tr.optimizer.param_groups[0]["lr"] *= 0.5
+        losses += [tr.train_step(content, style, t=t, noise=noise) for _ in range(3)]
         res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
     (le, sde), (lg, sdg) = res
     for a, b in zip(le, lg):

@@ -1,8 +1,6 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/g27; mkdir -p $O
-for v in "" _nt "" _nt; do
-  LDM_AMD_LIB=$PWD/music-style-transfer-ldm_amd/lib/libldm_amd$v.so timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench$v.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-  python -c "
-import json; d=json.load(open('$O/bench$v.json')); print('lib$v', d['value'], d['us_per_denoise_iteration'], {k: v['us'] for k, v in d['kernels'].items()})"
-done
+O=gpurun_out/g28; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_train.py -q -k "graphed or second_step" --timeout 200 --timeout-method thread > $O/t.log 2>&1; rc=$?
+tail -3 $O/t.log; grep "^FAILED\|^E  " $O/t.log | head
+exit $rc
