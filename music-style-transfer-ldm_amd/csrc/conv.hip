@@ -970,7 +970,9 @@ __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float 
 template <int K>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
+    __shared__ ChanEpi es[64];   // per-channel epilogue constants, formed once per block (not per lane and channel)
     for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = a.w[i];   // [co][ky*K + kx]
+    for (int i = threadIdx.x; i < a.Cout; i += blockDim.x) es[i] = chan_epi(a, i);
     __syncthreads();
     const int W4 = a.Wout >> 2;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1007,7 +1009,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[j] = fmaf(win[ky][kx + 2 * j], w, acc[j]);
             }
-        const ChanEpi ce = chan_epi(a, co);
+        const ChanEpi ce = es[co];
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[j]);

@@ -12,6 +12,7 @@ from ldm_amd import ops  # noqa: E402
 from time_wgrad import LAYERS, time_ms  # noqa: E402
 
 EXTRA = [("vae_dec3 convT k4 64->1", 32, 64, 64, 256, 1, 4, 2, 1, 0, True),
+         ("vae_enc1 k3s2 1->64", 32, 1, 128, 512, 64, 3, 2, 1, 0, False),
          ("style_enc5 k3s2 256->256", 32, 256, 8, 32, 256, 3, 2, 1, 0, False)]
 
 
