@@ -1,10 +1,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/g29; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_train.py tests/test_gpu_tiled.py -q --timeout 200 --timeout-method thread > $O/t.log 2>&1; rc=$?
-tail -2 $O/t.log; grep "^FAILED\|^E  " $O/t.log | head
+O=gpurun_out/g30; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
+tail -2 $O/gpu_tests.log; grep "^FAILED\|^E  " $O/gpu_tests.log | head
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python -u tools/time_conv.py bf16 > $O/conv.log 2>&1 || { tail $O/conv.log; exit 1; }
-grep "enc1 k3s2 1\|dec3" $O/conv.log
-timeout -k 10 240 python -u bench.py --workload train --steps 20 --warmup 3 --no-cpu-baseline > $O/train.json 2> $O/train.err || { tail -20 $O/train.err; exit 1; }
-grep -o '"ms_per_step": [0-9.]*' $O/train.json
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+bash tools/gpu_workloads.sh workloads_r02d > gpurun_out/workloads_r02d.log 2>&1 || { tail -5 gpurun_out/workloads_r02d.log; exit 1; }
+echo done
