@@ -641,13 +641,22 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
 #define LDM_ATTF(LP, SP, D, LT, EQV, NWV)                                                                \
     if (d == D && E == EQV && L <= LP && S <= SP) {                                                      \
         const size_t lds = ((size_t)NWV * LT * (SP + 1) + (size_t)D * (SP + 1)) * sizeof(float);       \
+        if (lds > 64 * 1024) {                                                                           \
+            static bool opted = false;                                                                   \
+            if (!opted) {                                                                                \
+                LDM_HIP_TRY(hipFuncSetAttribute(                                                         \
+                    (const void*)attention_mfma_kernel<2, LP, SP, D, LT, true, EQV, NWV>,                  \
+                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                            \
+                opted = true;                                                                            \
+            }                                                                                            \
+        }                                                                                                \
         hipLaunchKernelGGL((attention_mfma_kernel<2, LP, SP, D, LT, true, EQV, NWV>), dim3(B * heads * (LP / LT)), \
                            dim3(64 * NWV), lds, st, z, kv, out, E, heads, L, S, 1.0f, kf, bf);           \
         LDM_CHECK_LAUNCH("attention_mfma_kernel (folded)");                                              \
         return 0;                                                                                        \
     }
     LDM_ATTF(16, 16, 128, 16, 512, 8)
-    LDM_ATTF(64, 64, 64, 16, 256, 8)
+    LDM_ATTF(64, 64, 64, 16, 256, 16)
     LDM_ATTF(32, 32, 64, 16, 256, 8)
     LDM_ATTF(32, 32, 128, 16, 512, 8)
     LDM_ATTF(16, 16, 64, 16, 256, 4)
