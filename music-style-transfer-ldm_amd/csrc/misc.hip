@@ -189,8 +189,8 @@ __global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __
     const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
 
     // stage V [D][S] -> LDS [D][SP+1]: every load of this thread issues before any LDS store
-    if (S == SP && (D * SP) % (256 * NW) == 0) {   // full rows: 16-byte loads
-        constexpr int NV4 = D * SP / (256 * NW);
+    if (S == SP && (D * SP) % (256 * NW) == 0 && D * SP >= 256 * NW) {   // full rows: 16-byte loads
+        constexpr int NV4 = D * SP >= 256 * NW ? D * SP / (256 * NW) : 1;
         float4 v[NV4];
 #pragma unroll
         for (int u = 0; u < NV4; ++u) v[u] = reinterpret_cast<const float4*>(vb)[u * 64 * NW + (int)threadIdx.x];
