@@ -1,10 +1,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/g36; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
-tail -2 $O/gpu_tests.log; grep "^FAILED\|^E  " $O/gpu_tests.log | head
+O=gpurun_out/g37; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bench_config.py -q --timeout 200 --timeout-method thread > $O/t.log 2>&1; rc=$?
+tail -2 $O/t.log; grep "^FAILED\|^E  " $O/t.log | head
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-bash tools/gpu_final.sh final_r02e > gpurun_out/final_r02e.log 2>&1 || { tail -5 gpurun_out/final_r02e.log; exit 1; }
-echo done
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench$i.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/bench$i.json')); print(d['value'], d['us_per_denoise_iteration'], {k: v['us'] for k, v in d['kernels'].items() if 'attn' in k})"
+done
