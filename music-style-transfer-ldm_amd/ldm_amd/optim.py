@@ -60,6 +60,7 @@ class _SlotTable:
             host.copy_(torch.from_numpy(rows))
             self._host = host
             cls._captured.append(self)
+            self._captured_key = (dev, key)
         else:
             host = torch.from_numpy(rows).pin_memory()    # caching host allocator: reused once the copy ran
         self.slots.copy_(host, non_blocking=True)
@@ -75,9 +76,25 @@ class _SlotTable:
 
 def reserve_capture_buffers(n=4, words=1 << 14):
     """Pinned host buffers for the slot tables built while a step is being captured into a hipGraph (one
-    per optimizer / unscale table in the step); call before torch.cuda.graph."""
+    per optimizer / unscale table in the step); call before torch.cuda.graph.  Returns the list that will
+    hold the tables the capture builds: pass it to release_captured() when the graph is dropped."""
     while len(_SlotTable._reserve) < n:
         _SlotTable._reserve.append(torch.empty(words, dtype=torch.int64, pin_memory=True))
+    _SlotTable._captured = []
+    return _SlotTable._captured
+
+
+def release_captured(tables):
+    """Forget the slot tables (and their pinned host rows) of a captured graph that is being replaced: they
+    leave the table cache, so the pinned buffers and device tables die with the graph."""
+    if not tables:
+        return
+    for tab in tables:
+        k = getattr(tab, "_captured_key", None)
+        if k is not None and _SlotTable._cache.get(k) is tab:
+            del _SlotTable._cache[k]
+    tables.clear()
+    _SlotTable._reserve.clear()
 
 
 def scale_tensors_(tensors, factor):
@@ -142,6 +159,10 @@ class Adam(torch.optim.Optimizer):
             if self.capturable:
                 self._step_capturable(gi, group, params, found_inf, beta1, beta2)
                 continue
+            if "_ldm_step" in group:
+                # leaving the capturable form: every param gets its own host step count again (the shared
+                # device count must not be advanced once per param by the eager loop below)
+                self._unshare_steps(group)
             # group the params by their step count (all equal unless params were added later)
             by_step = {}
             for p in params:
@@ -169,6 +190,47 @@ class Adam(torch.optim.Optimizer):
                     torch.autograd.graph.increment_version(p)
         return loss
 
+
+    _GROUP_PRIVATE = ("_ldm_step", "_ldm_scalars", "_ldm_tabs")
+
+    def _unshare_steps(self, group):
+        gstep = group.pop("_ldm_step")
+        group.pop("_ldm_scalars", None)
+        n = float(gstep)
+        for p in group["params"]:
+            st = self.state.get(p)
+            if st and st.get("step") is gstep:
+                st["step"] = torch.tensor(n)
+
+    def state_dict(self):
+        """torch.optim state_dict, with every param's 'step' a CPU tensor of its own (the capturable form
+        shares one device count per group) and without this class's private per-group device tensors, so
+        that it loads into torch.optim.Adam or into an eager / capturable instance of this class alike."""
+        sd = super().state_dict()
+        for g in sd["param_groups"]:
+            for k in self._GROUP_PRIVATE:
+                g.pop(k, None)
+        state = {}
+        for idx, st in sd["state"].items():
+            st = dict(st)
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"] = torch.tensor(float(st["step"]))
+            state[idx] = st
+        sd["state"] = state
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        for g in self.param_groups:
+            for k in self._GROUP_PRIVATE:
+                g.pop(k, None)
+            for p in g["params"]:
+                st = self.state.get(p)
+                if st and "step" in st and torch.is_tensor(st["step"]):
+                    st["step"] = torch.tensor(float(st["step"]))
+        self._tables.clear()
+        # a captured train step holds the old state tensors: LDMTrainer re-captures when this moves
+        self.state_epoch = getattr(self, "state_epoch", 0) + 1
 
     def _step_capturable(self, gi, group, params, found_inf, beta1, beta2):
         """One launch pair for the group: ldm_adam_step_dev advances the group's device step count (shared

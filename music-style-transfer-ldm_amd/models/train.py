@@ -144,6 +144,7 @@ class LDMTrainer:
         self.device = torch.device(device) if not isinstance(device, torch.device) else device
         self.style_loss_weight = style_loss_weight
         trainable_params = [p for p in model.parameters() if p.requires_grad]
+        self._trainable = trainable_params
         self.optimizer = hoptim.Adam(trainable_params, lr=lr)
         self.scaler = hoptim.GradScaler("cuda")
         # dtype of the train step's autocast region (train.py:174 uses the device default: fp16 on a GPU;
@@ -195,6 +196,9 @@ class LDMTrainer:
             compression_loss_ = compression_loss(content_spec, reconstructed, z_0, self.model.feature_loss_net)
             style_loss_ = style_loss(reconstructed, style_spec, self.model.feature_loss_net)
             total_loss = compression_loss_ + denoisinsg_loss + self.style_loss_weight * style_loss_
+        # the step's reconstruction (a static buffer of the graph when the step is replayed): for callers that
+        # inspect the step's output, e.g. the parity tests; nothing in the step reads it
+        self.last_outputs = {"reconstructed": reconstructed.detach()}
         self.scaler.scale(total_loss).backward()
         if self.reducer is not None:
             self.reducer.finish()
@@ -223,22 +227,36 @@ class LDMTrainer:
         # moves lr between epochs; the style-loss weight): a change re-captures
         hyper = tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in self.optimizer.param_groups)
         sig = tuple(None if a is None else (tuple(a.shape), a.dtype) for a in args) + (
-            hyper, self.style_loss_weight, self.autocast_enabled, self.autocast_dtype)
+            hyper, self.style_loss_weight, self.autocast_enabled, self.autocast_dtype,
+            getattr(self.optimizer, "state_epoch", 0))
         if self._graph is None or self._graph_sig != sig:
             if self._graph_calls < self.graph_warmup:
                 self._graph_calls += 1
                 return self._losses(self._step(*args))
             static = [None if a is None else a.detach().clone() for a in args]
-            hoptim.reserve_capture_buffers()
+            if self._graph is not None:
+                hoptim.release_captured(self._graph_tables)
+                self._graph = None
+            tables = hoptim.reserve_capture_buffers()
+            # new versions for the capture: every weight pack of the step misses the version-keyed caches and
+            # is recorded into the graph (a cache hit would bake a pack made outside it into every replay)
+            for p in self._trainable:
+                torch.autograd.graph.increment_version(p)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 outs = self._step(*static)
             self._graph, self._graph_in, self._graph_out, self._graph_sig = g, static, outs, sig
+            self._graph_tables = tables
         for dst, src in zip(self._graph_in, args):
             if dst is not None:
                 dst.copy_(src)
         self._graph.replay()
+        # the replay rewrote the parameters on the device, but their autograd versions moved only once, at
+        # capture: move them again so that version-keyed caches (packed conv weights, the UNet engine's bound
+        # weights) never serve pre-replay values to a later eager forward or to a re-capture
+        for p in self._trainable:
+            torch.autograd.graph.increment_version(p)
         return self._losses(self._graph_out)
 
     def train_epoch(self, epoch):

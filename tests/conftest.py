@@ -59,16 +59,28 @@ def cuda():
     return torch.device("cuda:0")
 
 
-def adam_step_err(new, ref_new, grad_ref, lr, rel=1e-3):
-    """Parity of one Adam/AdamW first step.  The first step moves each element by ~lr * g / (|g| + eps):
-    elements whose reference gradient is below `rel` x max|g| sit inside fp32 gradient noise and may move
-    the other way, so they are only held to 2 lr; the rest must agree to the returned rel_err."""
+def adam_step_err(new, ref_new, grad_ref, lr, rel=1e-3, grad=None):
+    """Parity of one Adam/AdamW first step, which moves each element by ~lr * sign(g).
+
+    grad (our gradient, recommended): where its sign agrees with the reference gradient's, the update must
+    agree too, however small g is; a sign disagreement is allowed only inside the fp32 gradient noise
+    (|g_ref| <= rel x max|g_ref|), and only there may an element move the other way (held to 2 lr).
+    Without grad, every element below the noise level is held to 2 lr only.  Returns the rel_err of the
+    elements that must agree."""
     new = np.asarray(new, dtype=np.float64)
     ref_new = np.asarray(ref_new, dtype=np.float64)
-    g = np.abs(np.asarray(grad_ref, dtype=np.float64))
-    big = g > rel * g.max()
-    small_ok = bool(np.all(np.abs(new - ref_new)[~big] <= 2.0 * lr * (1 + 1e-3) + 1e-7))
+    gr = np.asarray(grad_ref, dtype=np.float64)
+    big = np.abs(gr) > rel * np.abs(gr).max()
+    must = big
+    if grad is not None:
+        g = np.asarray(grad, dtype=np.float64)
+        # (|g| well above Adam's eps = 1e-8, where the step is lr * sign(g) whatever the magnitude)
+        agree = (np.sign(g) == np.sign(gr)) & (np.minimum(np.abs(g), np.abs(gr)) > 1e-6)
+        assert not np.any(~agree & big), "a gradient above the noise level has the wrong sign"
+        must = big | agree
+    free = ~must
+    small_ok = bool(np.all(np.abs(new - ref_new)[free] <= 2.0 * lr * (1 + 1e-3) + 1e-7))
     assert small_ok, "an element moved by more than one Adam step"
-    if not big.any():
+    if not must.any():
         return 0.0
-    return float(np.abs(new - ref_new)[big].max() / max(np.abs(ref_new).max(), 1e-30))
+    return float(np.abs(new - ref_new)[must].max() / max(np.abs(ref_new).max(), 1e-30))

@@ -4,6 +4,7 @@
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r2     # ref_goldens_r2.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp    # ref_goldens_amp.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --vggish # ref_goldens_vggish.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r3     # ref_goldens_r3.npz
 
 Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
 stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
@@ -375,6 +376,62 @@ def vggish():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays", {k: float(v) for k, v in G.items()})
 
 
+R3_B, R3_H, R3_W = 32, 128, 512
+
+
+def r3_inputs():
+    """Config 3's benchmarked shape: batch 32, 1x128x512 content / style mels, t, injected q_sample noise."""
+    content = torch.from_numpy(recipe.uniform01((R3_B, 1, R3_H, R3_W), 760))
+    style = torch.from_numpy(recipe.uniform01((R3_B, 1, R3_H, R3_W), 761))
+    t = torch.from_numpy(recipe.timesteps(R3_B, 762))
+    noise = torch.from_numpy(recipe.normal((R3_B, 32, R3_H // 8, R3_W // 8), 763))
+    return content, style, t, noise
+
+
+def round3():
+    """(11) LDMTrainer.train_step's arithmetic at config 3's benchmarked shape -> ref_goldens_r3.npz: batch 32,
+    1x128x512 mels, LDM(32, pretrained_path='') with recipe weights (seed 700) and every module in train mode
+    (the bench's model: the encoder is trainable too, its BN uses batch statistics), loss = MSE(recon, x) +
+    0.01 KL(z0) + MSE(eps_pred, eps) (LPIPS / VGGish left out: remote weights), q_sample noise injected.  Once
+    in fp32 and once with forward + losses under torch.autocast("cpu", bfloat16) (train.py:174's region),
+    backward outside.  Stored: the loss terms, reconstructed samples 0 and 31, the ten TRAIN_GRAD_KEYS
+    gradients (in_proj rows 0..255)."""
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+    content, style, t, noise = r3_inputs()
+    G["r3_t"] = t.numpy()
+    for name, dt in (("fp32", None), ("bf16", torch.bfloat16)):
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.train()
+        real_randn_like = torch.randn_like
+        torch.randn_like = lambda x, *a, **k: noise.clone()
+        try:
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=dt is not None):
+                out = ldm(content, style, t)
+                dl = L.diffusion_loss(out["noise_pred"], out["noise"])
+                mse = torch.nn.MSELoss()(out["reconstructed"], content)
+                kl = L.kl_regularization_loss(out["z_0"])
+                comp = mse + 0.01 * kl
+                total = comp + dl
+        finally:
+            torch.randn_like = real_randn_like
+        total.backward()
+        G[f"r3_{name}_compression"] = np32(comp.float())
+        G[f"r3_{name}_diffusion"] = np32(dl.float())
+        G[f"r3_{name}_total"] = np32(total.float())
+        G[f"r3_{name}_recon_0_31"] = np32(out["reconstructed"].float()[[0, R3_B - 1]])
+        named = dict(ldm.named_parameters())
+        for k in TRAIN_GRAD_KEYS:
+            g = named[k].grad
+            G[f"r3_{name}_grad_" + k] = np32(g[:256] if g.dim() == 2 and g.shape[0] > 256 else g)
+        print(name, float(total), flush=True)
+    path = os.path.join(HERE, "ref_goldens_r3.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
 TRAIN_GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
                    "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
                    "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
@@ -388,6 +445,8 @@ AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.enco
 if __name__ == "__main__":
     if "--r2" in sys.argv:
         round2()
+    elif "--r3" in sys.argv:
+        round3()
     elif "--amp" in sys.argv:
         amp()
     elif "--vggish" in sys.argv:

@@ -267,7 +267,8 @@ def test_trainer_world2_syncbn_equals_world1(cuda):
     for k in KEYS:
         for r in range(world):
             assert rel_err(res[r]["grad/" + k], ref["grad/" + k]) < TOL, (r, k)
-            assert adam_step_err(res[r]["param/" + k], ref["param/" + k], ref["grad/" + k], 5e-4) < 1e-5, (r, k)
+            assert adam_step_err(res[r]["param/" + k], ref["param/" + k], ref["grad/" + k], 5e-4,
+                                 grad=res[r]["grad/" + k]) < 1e-5, (r, k)
     for k in BUFS:
         for r in range(world):
             assert rel_err(res[r]["buf/" + k], ref["buf/" + k]) < TOL, (r, k)

@@ -1,0 +1,248 @@
+"""Config 3 at its benchmarked shape: LDMTrainer.train_step (reference train.py:163-208) at batch 32 on
+1x128x512 mels, built exactly like bench.py's train line (LDM(32, pretrained_path=''), every module in train
+mode, the B=32 tuned plans of tuned_plans.json, GradScaler + Adam(lr=1e-4), graph_step on) with t and the
+q_sample noise injected, against the REFERENCE run at the same shape (tests/golden/ref_goldens_r3.npz,
+make_goldens.py --r3: recipe weights, train-mode model, loss = MSE + 0.01 KL + diffusion MSE).
+
+The two warm-up steps run at lr = 0 (weights unchanged; Adam's moments and step count advance), so the
+captured-and-replayed third step sees the recipe weights the goldens were made from.  Checked after the
+replay: the three reported loss terms, reconstructed samples 0 and 31, the ten TRAIN_GRAD_KEYS gradients,
+and the Adam update (moments to 1e-6; parameters to 2 fp32 ulps + 1e-3 lr against float64 Adam applied to
+the step's own gradients from the snapshot of the moments taken before it).
+
+Tolerances: fp32 (LDM_AMD_DTYPE=fp32, the bench's --dtype fp32): max|y - y_ref| <= 1e-4 max|y_ref|
+(north_star).  bf16 (the bench default): per quantity within 2 e + 1e-3 of both the fp32 and the bf16
+reference, e = the reference's own bf16-vs-fp32 distance (the rule of test_gpu_amp.py).
+
+test_config3_every_conv_instance re-runs every conv forward / data-gradient / weight-gradient call of one
+bf16 step at its B=32 geometry (whatever kernel instance the plan picks: tconv_kernel, conv_mfma_kernel,
+wgrad_lp_kernel, the Cin = 1 and Cout = 1 kernels ...) on random operands against float64 of the operands
+(rounded to bf16 where the instance rounds; 1e-5).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import recipe
+from conftest import ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+
+GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
+             "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
+             "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
+             "style_encoder.enc1.weight")
+B, H, W = 32, 128, 512
+
+
+@pytest.fixture(scope="module")
+def g3():
+    return np.load(os.path.join(ROOT, "tests", "golden", "ref_goldens_r3.npz"))
+
+
+def _inputs(cuda):
+    content = torch.from_numpy(recipe.uniform01((B, 1, H, W), 760)).to(cuda)
+    style = torch.from_numpy(recipe.uniform01((B, 1, H, W), 761)).to(cuda)
+    t = torch.from_numpy(recipe.timesteps(B, 762)).to(cuda)
+    noise = torch.from_numpy(recipe.normal((B, 32, H // 8, W // 8), 763)).to(cuda)
+    return content, style, t, noise
+
+
+def npy(t):
+    return t.detach().double().cpu().numpy()
+
+
+def _bench_trainer(cuda, dtype):
+    """The bench's train line (bench.py run_train) on recipe weights."""
+    import models.model as M
+    import models.train as TR
+    m = M.LDM(32, pretrained_path="")
+    recipe.fill_module(m, seed=700)
+    m = m.to(cuda).train()
+    tr = TR.LDMTrainer(m, None, cuda, lr=1e-4)
+    tr.autocast_dtype = None if dtype == "fp32" else torch.bfloat16
+    tr.graph_step = True
+    return m, tr
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_config3_graphed_step_matches_reference(g3, cuda, dtype, monkeypatch):
+    if dtype == "fp32":
+        monkeypatch.setenv("LDM_AMD_DTYPE", "fp32")
+    m, tr = _bench_trainer(cuda, dtype)
+    content, style, t, noise = _inputs(cuda)
+    assert np.array_equal(t.cpu().numpy(), g3["r3_t"])
+    lr = 1e-4
+    tr.optimizer.param_groups[0]["lr"] = 0.0
+    for _ in range(2):
+        tr.train_step(content, style, t=t, noise=noise)
+    assert tr._graph is None
+    named = dict(m.named_parameters())
+    snap = {}
+    for k in GRAD_KEYS:
+        st = tr.optimizer.state[named[k]]
+        snap[k] = (st["exp_avg"].double().cpu(), st["exp_avg_sq"].double().cpu(), named[k].detach().double().cpu())
+    tr.optimizer.param_groups[0]["lr"] = lr
+    losses = tr.train_step(content, style, t=t, noise=noise)
+    assert tr._graph is not None, "the third step must be the captured graph's replay"
+    torch.cuda.synchronize()
+
+    rec = tr.last_outputs["reconstructed"][[0, B - 1]]
+    grads = {}
+    for k in GRAD_KEYS:
+        g = named[k].grad
+        grads[k] = g[:256] if g.dim() == 2 and g.shape[0] > 256 else g
+    pairs = [("compression", np.float64(losses["compression_loss"]), "compression"),
+             ("diffusion", np.float64(losses["denoisinsg_loss"]), "diffusion"),
+             ("total", np.float64(losses["total_loss"]), "total"),
+             ("recon", npy(rec), "recon_0_31")] + [(k, npy(grads[k]), "grad_" + k) for k in GRAD_KEYS]
+    assert losses["style_loss"] == 0.0
+    rows, bad = [], []
+    for name, ours, key in pairs:
+        f32, bf = g3[f"r3_fp32_{key}"], g3[f"r3_bf16_{key}"]
+        to32 = rel_err(np.asarray(ours).reshape(np.shape(f32)), f32)
+        if dtype == "fp32":
+            rows.append(f"{name}: {to32:.2e}")
+            if to32 > 1e-4:
+                bad.append(name)
+        else:
+            e = rel_err(bf, f32)
+            tobf = rel_err(np.asarray(ours).reshape(np.shape(bf)), bf)
+            rows.append(f"{name}: ref bf16-vs-fp32 {e:.2e}, ours-vs-fp32 {to32:.2e}, ours-vs-bf16 {tobf:.2e}")
+            if to32 > 2 * e + 1e-3 or tobf > 2 * e + 1e-3:
+                bad.append(name)
+    print("\n".join(rows))
+    assert not bad, (bad, rows)
+
+    # Adam (step 3) from the snapshot of the moments, applied to this step's own (unscaled) gradients
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    for k in GRAD_KEYS:
+        p = named[k]
+        g = p.grad.double().cpu()
+        m2, v2, p2 = snap[k]
+        m3 = b1 * m2 + (1 - b1) * g
+        v3 = b2 * v2 + (1 - b2) * g * g
+        st = tr.optimizer.state[p]
+        assert rel_err(npy(st["exp_avg"]), m3.numpy()) < 1e-6, k
+        assert rel_err(npy(st["exp_avg_sq"]), v3.numpy()) < 1e-6, k
+        p3 = p2 - (lr / (1 - b1 ** 3)) * m3 / (v3.sqrt() / math.sqrt(1 - b2 ** 3) + eps)
+        err = (p.detach().double().cpu() - p3).abs()
+        bound = 2 * np.finfo(np.float32).eps * p3.abs() + 1e-3 * lr
+        assert bool((err <= bound).all()), (k, float(err.max()))
+        assert float((p.detach().double().cpu() - p2).abs().max()) > 0.5 * lr, k   # the update was applied
+
+
+class _Recorder:
+    """Records the conv calls of one train step: ('fwd'|'dgrad'|'wgrad', desc fields, dtype, act)."""
+
+    def __init__(self, ops, monkeypatch):
+        self.calls = []
+        self.seen = set()
+        fwd, dgrad, wgrad = ops.conv_forward, ops.conv_backward_data, ops.conv_backward_weight
+
+        def key(desc):
+            return (desc.B, desc.Cin, desc.Hin, desc.Win, desc.Cout, desc.kh, desc.kw, desc.stride, desc.pad,
+                    desc.out_pad, desc.transposed)
+
+        def add(kind, d, dt, extra=()):
+            k = (kind, key(d), int(dt)) + tuple(extra)
+            if k not in self.seen:
+                self.seen.add(k)
+                self.calls.append(k)
+
+        def conv_forward(x, weight, bias=None, **kw):
+            y = fwd(x, weight, bias, **kw)
+            if kw.get("plan") is None:
+                d = ops.make_desc(x.shape[0], x.shape[1], x.shape[2], x.shape[3], y.shape[1],
+                                  weight.shape[2], weight.shape[3], kw.get("stride", 1), kw.get("padding", 1),
+                                  kw.get("output_padding", 0), kw.get("transposed", False))
+                dt = ops.autocast_dt() if kw.get("dtype") is None else kw["dtype"]
+                add("fwd", d, dt, (kw.get("bcast") is not None, kw.get("skip") is not None))
+            return y
+
+        def conv_backward_data(dy, weight, desc, wkey=None, dtype=0):
+            add("dgrad", desc, dtype)
+            return dgrad(dy, weight, desc, wkey, dtype)
+
+        def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
+            add("wgrad", desc, dtype)
+            return wgrad(x, dy, desc, dw, accumulate, dtype)
+
+        monkeypatch.setattr(ops, "conv_forward", conv_forward)
+        monkeypatch.setattr(ops, "conv_backward_data", conv_backward_data)
+        monkeypatch.setattr(ops, "conv_backward_weight", conv_backward_weight)
+
+
+def _ref_conv(x, w, d):
+    if d[10]:
+        return F.conv_transpose2d(x, w, stride=d[7], padding=d[8], output_padding=d[9])
+    return F.conv2d(x, w, stride=d[7], padding=d[8])
+
+
+def test_config3_every_conv_instance(cuda, monkeypatch):
+    """Every conv forward / data gradient / weight gradient of one bf16 config-3 step, at its B=32 geometry."""
+    from ldm_amd import ops
+    m, tr = _bench_trainer(cuda, "bf16")
+    tr.graph_step = False
+    content, style, t, noise = _inputs(cuda)
+    rec = _Recorder(ops, monkeypatch)
+    tr.train_step(content, style, t=t, noise=noise)
+    monkeypatch.undo()
+    torch.cuda.synchronize()
+    assert len(rec.calls) >= 20, rec.calls
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    g = torch.Generator().manual_seed(5)
+    bad, rows = [], []
+    for call in rec.calls:
+        kind, d, dt = call[0], call[1], call[2]
+        Bc, Cin, Hin, Win, Cout, kh, kw, stride, pad, op, tr_ = d
+        wshape = (Cin, Cout, kh, kw) if tr_ else (Cout, Cin, kh, kw)
+        w = torch.randn(wshape, generator=g) / math.sqrt(Cin * kh * kw)
+        x = torch.rand((Bc, Cin, Hin, Win), generator=g) * 2 - 1
+        desc = ops.make_desc(Bc, Cin, Hin, Win, Cout, kh, kw, stride, pad, op, tr_)
+        rnd = (lambda a: a.bfloat16().double()) if dt == 2 else (lambda a: a.half().double()) if dt == 1 \
+            else (lambda a: a.double())
+        xd, wd = x.to(cuda), w.to(cuda)
+        yshape = (Bc, Cout, desc.Hout, desc.Wout)
+        if kind == "fwd":
+            # an epilogue with a broadcast add or a skip runs another kernel family: keep them (zero-valued)
+            has_bc, has_sk = call[3], call[4]
+            y = ops.conv_forward(xd, wd, None, stride=stride, padding=pad, transposed=bool(tr_), output_padding=op,
+                                 bcast=torch.zeros((Bc, Cout), device=cuda) if has_bc else None,
+                                 skip=torch.zeros(yshape, device=cuda) if has_sk else None, dtype=dt)
+            ys = npy(y[[0, Bc - 1]])
+
+            def ref(f):
+                return _ref_conv(f(x[[0, Bc - 1]]), f(w), d).numpy()
+        elif kind == "dgrad":
+            dy = torch.rand(yshape, generator=g) * 2 - 1
+            gx = ops.conv_backward_data(dy.to(cuda), wd, desc, dtype=dt)
+            ys = npy(gx[[0, Bc - 1]])
+
+            def ref(f):
+                xr = torch.zeros((2, Cin, Hin, Win), dtype=torch.float64, requires_grad=True)
+                (_ref_conv(xr, f(w), d) * f(dy[[0, Bc - 1]])).sum().backward()
+                return xr.grad.numpy()
+        else:
+            dy = torch.rand(yshape, generator=g) * 2 - 1
+            dw = ops.conv_backward_weight(xd, dy.to(cuda), desc, dtype=dt)
+            ys = npy(dw)
+
+            def ref(f):
+                wr = w.double().requires_grad_(True)
+                (_ref_conv(f(x), wr, d) * f(dy)).sum().backward()
+                return wr.grad.numpy()
+        # float64 of the operands as the instance sees them: rounded to the region's dtype, or fp32 for the
+        # instances that keep fp32 operands (the Cin = 1 / Cout = 1 / direct kernels)
+        err = rel_err(ys, ref(rnd))
+        if err > 1e-5 and dt != 0:
+            err = min(err, rel_err(ys, ref(lambda a: a.double())))
+        rows.append(f"{kind} {d} dt={dt}: {err:.2e}")
+        if err > 1e-5:
+            bad.append(rows[-1])
+    print("\n".join(rows))
+    assert not bad, bad
