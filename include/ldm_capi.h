@@ -179,6 +179,13 @@ int ldm_fold_conv_proj(const ldm_conv_desc* d, const float* w_conv, const float*
                        const float* b_proj, int32_t Cmid, float* w_out, float* pos_bias_out, void* stream);
 int ldm_attention_core(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads,
                        int32_t L, int32_t S, float scale, void* stream);
+/* Width-general form (flash.hip; any L, S, head dim 64 or 128 — the UNet's token counts grow with the mel
+ * width, model.py:140-153): KV-tiled online softmax, channel-major q / out as ldm_attention_core, plus
+ * lse [B,heads,L] = the log-sum-exp of each query's scaled scores for ldm_attention_backward_flash.
+ * ldm_attention_core itself hands over to this kernel when L or S exceeds its LDS-resident instances. */
+int ldm_attention_flash_supported(int32_t E, int32_t heads);
+int ldm_attention_forward_lse(const float* q, const float* kv, float* out, float* lse, int32_t B, int32_t E,
+                              int32_t heads, int32_t L, int32_t S, float scale, void* stream);
 
 /* ---- DDPM forward noising q_sample (ForwardDiffusion.forward, model.py:102-115) ----------------
  * z_t = sqrt(ab[t_b]) * x0 + sqrt(1-ab[t_b]) * eps.  coef_table [T,2] = {sqrt(ab), sqrt(1-ab)} per
@@ -356,6 +363,12 @@ int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x
 /* Backward of ldm_attention_core: dq [B,E,L], dkv [B,2E,S] (dK then dV). */
 int ldm_attention_backward(const float* q, const float* kv, const float* dout, float* dq, float* dkv, int32_t B,
                            int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream);
+/* The same backward for any L, S (flash.hip), from the forward's out and lse (ldm_attention_forward_lse):
+ * delta = rowsum(dO * O) into delta_ws [B,heads,L], then dK/dV (64 keys per block, q and dO streamed) and
+ * dQ (64 queries per block, K and V streamed), deterministic. */
+int ldm_attention_backward_flash(const float* q, const float* kv, const float* out, const float* lse,
+                                 const float* dout, float* dq, float* dkv, float* delta_ws, int32_t B, int32_t E,
+                                 int32_t heads, int32_t L, int32_t S, float scale, void* stream);
 
 /* ---- VGGish feature / style loss (loss.py:52-101, VGGishFeatureLoss.forward) ----
  * The conv stack runs on ldm_conv_forward (ReLU fused: each conv launch yields one feature tap).

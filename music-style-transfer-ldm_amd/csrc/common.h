@@ -161,6 +161,12 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
 int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, int32_t E, int32_t heads, int32_t L,
                       int32_t S, float scale, bool tok, hipStream_t st);
 
+// flash.hip: KV-tiled online-softmax attention for any L, S (head dim 64 or 128); lse [B,heads,L] (channel-major
+// q only) or NULL
+bool attention_flash_supported(int E, int heads);
+int attention_flash(const float* q, const float* kv, float* out, float* lse, int32_t B, int32_t E, int32_t heads,
+                    int32_t L, int32_t S, float scale, bool tok, hipStream_t st);
+
 int attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out, int32_t B,
                      int32_t E, int32_t heads, int32_t L, int32_t S, hipStream_t st);
 int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,

@@ -1,0 +1,493 @@
+// Width-general cross-attention (CrossAttention, model.py:126-160) for any number of query tokens L and
+// key tokens S: KV-tiled online-softmax forward and the matching two-kernel backward, on the exact-fp32
+// v_mfma_f32_16x16x4_f32.  The UNet's attention tokens grow linearly with the mel width (L = S = H*W/16
+// for CA2, H*W/64 for CA1: 64 / 16 at the canonical 16x64 latent, 128 / 32 at 16x128, 4096 / 1024 for
+// SURVEY's stress shape S), so the LDS-resident instances of misc.hip (L, S <= 64) hand over to these.
+//
+// One block = 4 waves = 64 query rows (forward, dQ) or 64 key columns (dK/dV) of one (batch, head); each
+// wave owns 16 of them as the N (or M) side of its MFMA tiles.  K / V (forward, dQ) or q / dO (dK/dV)
+// stream through LDS in tiles of 64 tokens, staged by all four waves, pitch D+4 / 68 floats (= 4 mod 64:
+// the 16 lanes of one b128 read and the 64 lanes of one b32 read hit distinct banks).
+//
+// The products are laid out so that no fragment is ever transposed through LDS: the scores are computed
+// transposed (S^T = K (q*scale)^T, M = key, N = query), whose accumulator layout — lane (col, lg) holds
+// keys 4 lg + r of query col — is exactly the B operand of O^T = V P^T (K index s = 16 st + 4 lg + r), and
+// the softmax statistics of query col live in the lanes that accumulate its output column.  Row max / sum
+// take two xor-shuffles across the lane groups.  Deterministic: fixed tile order, no atomics.
+//
+// Layouts: kv [B, 2E, S] channel-major (K rows then V rows, as the K/V projection writes them); q / out
+// [B, E, L] channel-major or token-major [B, L, E] (TOK, the UNet engine's NHWC activations); lse / delta
+// [B, heads, L].
+#include <cmath>
+
+#include "common.h"
+
+namespace ldm {
+namespace fa {
+
+constexpr int kTok = 64;            // tokens per block and per streamed tile
+constexpr int kKP = kTok + 4;       // LDS pitch of a channel-major [c][s] tile
+
+__device__ __forceinline__ floatx4 mma(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// [D][64] tile of a channel-major slab (row c at src + c*n, tokens t0 .. t0+63, zero past n) -> LDS
+// [D][kKP]; every load of the thread in flight before its first store.
+template <int D>
+__device__ __forceinline__ void stage_cs(const float* __restrict__ src, int n, int t0, float* __restrict__ dst) {
+    constexpr int NIT = D * (kTok / 4) / 256;
+    float4 v[NIT];
+    const bool vec = (n & 3) == 0 && t0 + kTok <= n;
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+        const int e = u * 256 + (int)threadIdx.x;
+        const int c = e / (kTok / 4), t = t0 + 4 * (e % (kTok / 4));
+        const float* p = src + (size_t)c * n + t;
+        if (vec) {
+            v[u] = *reinterpret_cast<const float4*>(p);
+        } else {
+            v[u].x = t + 0 < n ? p[0] : 0.f;
+            v[u].y = t + 1 < n ? p[1] : 0.f;
+            v[u].z = t + 2 < n ? p[2] : 0.f;
+            v[u].w = t + 3 < n ? p[3] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+        const int e = u * 256 + (int)threadIdx.x;
+        *reinterpret_cast<float4*>(dst + (e / (kTok / 4)) * kKP + 4 * (e % (kTok / 4))) = v[u];
+    }
+}
+
+// [D][64] channel-major tile (tokens t0..) -> LDS token-major [64][D+4], times mul; zero past n.
+template <int D>
+__device__ __forceinline__ void stage_tc(const float* __restrict__ src, int n, int t0, float mul, float* __restrict__ dst) {
+    constexpr int NIT = D * (kTok / 4) / 256, P = D + 4;
+    float4 v[NIT];
+    const bool vec = (n & 3) == 0 && t0 + kTok <= n;
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+        const int e = u * 256 + (int)threadIdx.x;
+        const int c = e / (kTok / 4), t = t0 + 4 * (e % (kTok / 4));
+        const float* p = src + (size_t)c * n + t;
+        if (vec) {
+            v[u] = *reinterpret_cast<const float4*>(p);
+        } else {
+            v[u].x = t + 0 < n ? p[0] : 0.f;
+            v[u].y = t + 1 < n ? p[1] : 0.f;
+            v[u].z = t + 2 < n ? p[2] : 0.f;
+            v[u].w = t + 3 < n ? p[3] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+        const int e = u * 256 + (int)threadIdx.x;
+        const int c = e / (kTok / 4), tl = 4 * (e % (kTok / 4));
+        dst[(tl + 0) * P + c] = v[u].x * mul;
+        dst[(tl + 1) * P + c] = v[u].y * mul;
+        dst[(tl + 2) * P + c] = v[u].z * mul;
+        dst[(tl + 3) * P + c] = v[u].w * mul;
+    }
+}
+
+// The 16 query rows' fragment a lane holds as the N operand: frag[jj][i] = x[l][16 jj + 4 lg + i] * mul.
+template <int D, bool TOK>
+__device__ __forceinline__ void load_qfrag(const float* __restrict__ base, int E, int L, int l, int lg, float mul,
+                                           float (&f)[D / 16][4]) {
+    if constexpr (TOK) {
+        const float* p = base + (size_t)l * E + 4 * lg;
+#pragma unroll
+        for (int jj = 0; jj < D / 16; ++jj) {
+            const float4 v = *reinterpret_cast<const float4*>(p + 16 * jj);
+            f[jj][0] = v.x * mul;
+            f[jj][1] = v.y * mul;
+            f[jj][2] = v.z * mul;
+            f[jj][3] = v.w * mul;
+        }
+    } else {
+        const float* p = base + (size_t)(4 * lg) * L + l;
+#pragma unroll
+        for (int jj = 0; jj < D / 16; ++jj)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[jj][i] = p[(size_t)(16 * jj + i) * L] * mul;
+    }
+}
+
+// ---- forward ---------------------------------------------------------------------------------------
+template <int D, bool TOK, bool LSE>
+__global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                        float* __restrict__ out, float* __restrict__ lse, int E,
+                                                        int heads, int L, int S, float scale) {
+    constexpr int NJ = D / 16;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ks = sm;              // [D][kKP]
+    float* Vs = sm + D * kKP;    // [D][kKP]
+    const int nqt = (L + kTok - 1) / kTok;
+    const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
+    const int h = bh % heads, b = bh / heads;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, lg = lane >> 4;
+    const int l = qt * kTok + wave * 16 + col;
+    const bool lok = l < L;
+    const int lc = lok ? l : L - 1;
+
+    // q_scaled = q * sqrt(1/d) (the reference's elementwise product), N operand of S^T
+    float qf[NJ][4];
+    const float* qb = TOK ? q + (size_t)b * L * E + (size_t)h * D : q + ((size_t)b * E + (size_t)h * D) * L;
+    load_qfrag<D, TOK>(qb, E, L, lc, lg, scale, qf);
+
+    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
+    const float* vb = kb + (size_t)E * S;
+    floatx4 o[NJ];
+#pragma unroll
+    for (int ct = 0; ct < NJ; ++ct) o[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+
+    for (int s0 = 0; s0 < S; s0 += kTok) {
+        __syncthreads();
+        stage_cs<D>(kb, S, s0, Ks);
+        stage_cs<D>(vb, S, s0, Vs);
+        __syncthreads();
+        // S^T[s][l] for the tile's 64 keys (4 tiles of 16): lane holds keys s0 + 16 st + 4 lg + r of query l
+        floatx4 sc[4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            sc[st] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sc[st] = mma(Ks[(16 * jj + 4 * lg + i) * kKP + 16 * st + col], qf[jj][i], sc[st]);
+        }
+        // online softmax over s (the 4 lanes of query col share its statistics)
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (s0 + 16 * st + 4 * lg + r < S) tmax = fmaxf(tmax, sc[st][r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = expf(m - mnew);
+        float p[4][4], tsum = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                p[st][r] = s0 + 16 * st + 4 * lg + r < S ? expf(sc[st][r] - mnew) : 0.f;
+                tsum += p[st][r];
+            }
+        tsum += __shfl_xor(tsum, 16);
+        tsum += __shfl_xor(tsum, 32);
+        lsum = lsum * alpha + tsum;
+        m = mnew;
+        // O^T[c][l] = alpha O^T + sum_s V[c][s] P[l][s]
+#pragma unroll
+        for (int ct = 0; ct < NJ; ++ct) {
+            o[ct] *= alpha;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const float4 va = *reinterpret_cast<const float4*>(Vs + (16 * ct + col) * kKP + 16 * st + 4 * lg);
+                o[ct] = mma(va.x, p[st][0], o[ct]);
+                o[ct] = mma(va.y, p[st][1], o[ct]);
+                o[ct] = mma(va.z, p[st][2], o[ct]);
+                o[ct] = mma(va.w, p[st][3], o[ct]);
+            }
+        }
+    }
+    if (!lok) return;
+    // lane holds O[l][c] for c = 16 ct + 4 lg + r
+    if constexpr (TOK) {
+        float* ob = out + ((size_t)b * L + l) * E + (size_t)h * D + 4 * lg;
+#pragma unroll
+        for (int ct = 0; ct < NJ; ++ct)
+            *reinterpret_cast<float4*>(ob + 16 * ct) =
+                make_float4(o[ct][0] / lsum, o[ct][1] / lsum, o[ct][2] / lsum, o[ct][3] / lsum);
+    } else {
+        float* ob = out + ((size_t)b * E + (size_t)h * D + 4 * lg) * L + l;
+#pragma unroll
+        for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ob[(size_t)(16 * ct + r) * L] = o[ct][r] / lsum;
+    }
+    if (LSE && lg == 0) lse[(size_t)bh * L + l] = m + logf(lsum);
+}
+
+// ---- backward ----------------------------------------------------------------------------------------
+// delta[b,h,l] = sum_c dO[c][l] O[c][l] over the head's channels (= rowsum(P * dP), channel-major)
+__global__ __launch_bounds__(256) void flash_delta_kernel(const float* __restrict__ out, const float* __restrict__ dout,
+                                                          float* __restrict__ delta, int E, int heads, int L, int D,
+                                                          int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int l = (int)(i % L);
+    const int64_t bh = i / L;
+    const int h = (int)(bh % heads);
+    const int64_t b = bh / heads;
+    const size_t base = ((size_t)b * E + (size_t)h * D) * L + l;
+    float acc = 0.f;
+    for (int c = 0; c < D; ++c) acc = fmaf(dout[base + (size_t)c * L], out[base + (size_t)c * L], acc);
+    delta[i] = acc;
+}
+
+// dK, dV for 64 keys per block (wave: 16 keys, the N side), streaming q*scale and dO through LDS:
+//   S = qs K^T, P = exp(S - lse), dP = dO V^T, dS = P (dP - delta);  dV^T += dO^T P, dK^T += qs^T dS
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_dkv_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                            const float* __restrict__ dout, const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, float* __restrict__ dkv,
+                                                            int E, int heads, int L, int S, float scale) {
+    constexpr int NJ = D / 16, P = D + 4;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Qs = sm;                  // [64][D+4]  q * scale, token-major
+    float* Os = Qs + kTok * P;       // [64][D+4]  dO
+    float* Ls = Os + kTok * P;       // [64] lse (+inf past L: P = 0)
+    float* Ds = Ls + kTok;           // [64] delta
+    const int nkt = (S + kTok - 1) / kTok;
+    const int kt = blockIdx.x % nkt, bh = blockIdx.x / nkt;
+    const int h = bh % heads, b = bh / heads;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, lg = lane >> 4;
+    const int s = kt * kTok + wave * 16 + col;
+    const bool sok = s < S;
+    const int sc = sok ? s : S - 1;
+    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
+    const float* vb = kb + (size_t)E * S;
+    float kf[NJ][4], vf[NJ][4];   // B operands: K[c][s], V[c][s] for c = 16 jj + 4 lg + i
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            kf[jj][i] = kb[(size_t)(16 * jj + 4 * lg + i) * S + sc];
+            vf[jj][i] = vb[(size_t)(16 * jj + 4 * lg + i) * S + sc];
+        }
+    const float* qb = q + ((size_t)b * E + (size_t)h * D) * L;
+    const float* ob = dout + ((size_t)b * E + (size_t)h * D) * L;
+    const float* lb = lse + (size_t)bh * L;
+    const float* db = delta + (size_t)bh * L;
+    floatx4 dk[NJ], dv[NJ];
+#pragma unroll
+    for (int ct = 0; ct < NJ; ++ct) dk[ct] = dv[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int l0 = 0; l0 < L; l0 += kTok) {
+        __syncthreads();
+        stage_tc<D>(qb, L, l0, scale, Qs);
+        stage_tc<D>(ob, L, l0, 1.f, Os);
+        if (threadIdx.x < kTok) {
+            const int l = l0 + (int)threadIdx.x;
+            Ls[threadIdx.x] = l < L ? lb[l] : INFINITY;
+            Ds[threadIdx.x] = l < L ? db[l] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int lt = 0; lt < 4; ++lt) {
+            // S[l][s], dP[l][s]: lane holds queries l0 + 16 lt + 4 lg + r of key s
+            floatx4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+            const float* qrow = Qs + (16 * lt + col) * P + 4 * lg;
+            const float* orow = Os + (16 * lt + col) * P + 4 * lg;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const float4 a = *reinterpret_cast<const float4*>(qrow + 16 * jj);
+                const float4 g = *reinterpret_cast<const float4*>(orow + 16 * jj);
+                sv = mma(a.x, kf[jj][0], sv);
+                sv = mma(a.y, kf[jj][1], sv);
+                sv = mma(a.z, kf[jj][2], sv);
+                sv = mma(a.w, kf[jj][3], sv);
+                dp = mma(g.x, vf[jj][0], dp);
+                dp = mma(g.y, vf[jj][1], dp);
+                dp = mma(g.z, vf[jj][2], dp);
+                dp = mma(g.w, vf[jj][3], dp);
+            }
+            float pv[4], ds[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int li = 16 * lt + 4 * lg + r;
+                pv[r] = expf(sv[r] - Ls[li]);
+                ds[r] = pv[r] * (dp[r] - Ds[li]);
+            }
+            // dV^T[c][s] += sum_l dO[l][c] P[l][s];  dK^T[c][s] += sum_l qs[l][c] dS[l][s]
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int li = 16 * lt + 4 * lg + r;
+                    dv[ct] = mma(Os[li * P + 16 * ct + col], pv[r], dv[ct]);
+                    dk[ct] = mma(Qs[li * P + 16 * ct + col], ds[r], dk[ct]);
+                }
+        }
+    }
+    if (!sok) return;
+    float* dkb = dkv + ((size_t)b * 2 * E + (size_t)h * D) * S + s;
+    float* dvb = dkb + (size_t)E * S;
+#pragma unroll
+    for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            dkb[(size_t)(16 * ct + 4 * lg + r) * S] = dk[ct][r];
+            dvb[(size_t)(16 * ct + 4 * lg + r) * S] = dv[ct][r];
+        }
+}
+
+// dQ for 64 queries per block (wave: 16 queries, the N side), streaming K and V through LDS:
+//   S^T = K qs^T, dP^T = V dO^T, dS = P (dP - delta);  dQ^T += K dS^T, times scale
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                           const float* __restrict__ dout, const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, float* __restrict__ dq,
+                                                           int E, int heads, int L, int S, float scale) {
+    constexpr int NJ = D / 16;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ks = sm;              // [D][kKP]
+    float* Vs = sm + D * kKP;    // [D][kKP]
+    const int nqt = (L + kTok - 1) / kTok;
+    const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
+    const int h = bh % heads, b = bh / heads;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, lg = lane >> 4;
+    const int l = qt * kTok + wave * 16 + col;
+    const bool lok = l < L;
+    const int lc = lok ? l : L - 1;
+    const float* qb = q + ((size_t)b * E + (size_t)h * D) * L;
+    const float* ob = dout + ((size_t)b * E + (size_t)h * D) * L;
+    float qf[NJ][4], of[NJ][4];
+    load_qfrag<D, false>(qb, E, L, lc, lg, scale, qf);
+    load_qfrag<D, false>(ob, E, L, lc, lg, 1.f, of);
+    const float ll = lse[(size_t)bh * L + lc], dl = delta[(size_t)bh * L + lc];
+    const float* kb = kv + ((size_t)b * 2 * E + (size_t)h * D) * S;
+    const float* vb = kb + (size_t)E * S;
+    floatx4 acc[NJ];
+#pragma unroll
+    for (int ct = 0; ct < NJ; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int s0 = 0; s0 < S; s0 += kTok) {
+        __syncthreads();
+        stage_cs<D>(kb, S, s0, Ks);
+        stage_cs<D>(vb, S, s0, Vs);
+        __syncthreads();
+        float ds[4][4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            floatx4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int a = (16 * jj + 4 * lg + i) * kKP + 16 * st + col;
+                    sv = mma(Ks[a], qf[jj][i], sv);
+                    dp = mma(Vs[a], of[jj][i], dp);
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool ok = s0 + 16 * st + 4 * lg + r < S;
+                const float pv = ok ? expf(sv[r] - ll) : 0.f;
+                ds[st][r] = pv * (dp[r] - dl);
+            }
+        }
+#pragma unroll
+        for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const float4 ka = *reinterpret_cast<const float4*>(Ks + (16 * ct + col) * kKP + 16 * st + 4 * lg);
+                acc[ct] = mma(ka.x, ds[st][0], acc[ct]);
+                acc[ct] = mma(ka.y, ds[st][1], acc[ct]);
+                acc[ct] = mma(ka.z, ds[st][2], acc[ct]);
+                acc[ct] = mma(ka.w, ds[st][3], acc[ct]);
+            }
+    }
+    if (!lok) return;
+    float* db = dq + ((size_t)b * E + (size_t)h * D + 4 * lg) * L + l;
+#pragma unroll
+    for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) db[(size_t)(16 * ct + r) * L] = acc[ct][r] * scale;
+}
+
+template <class K>
+static int opt_in_lds(K kernel, size_t bytes) {
+    if (bytes > 64 * 1024) LDM_HIP_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)bytes));
+    return 0;
+}
+
+template <int D, bool TOK, bool LSE>
+static int fwd_launch(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
+                      float scale, hipStream_t st) {
+    const size_t lds = 2 * (size_t)D * kKP * sizeof(float);
+    static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE>, lds);
+    if (opted) return opted;
+    const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
+    hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E, heads, L, S,
+                       scale);
+    LDM_CHECK_LAUNCH("flash_fwd_kernel");
+    return 0;
+}
+
+template <int D>
+static int bwd_launch(const float* q, const float* kv, const float* out, const float* lse, const float* dout, float* dq,
+                      float* dkv, float* delta, int B, int E, int heads, int L, int S, float scale, hipStream_t st) {
+    const int64_t n = (int64_t)B * heads * L;
+    hipLaunchKernelGGL(flash_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, dout, delta, E, heads,
+                       L, D, n);
+    LDM_CHECK_LAUNCH("flash_delta_kernel");
+    const size_t lds_kv = (2 * (size_t)kTok * (D + 4) + 2 * kTok) * sizeof(float);
+    static int o1 = opt_in_lds(flash_bwd_dkv_kernel<D>, lds_kv);
+    if (o1) return o1;
+    hipLaunchKernelGGL(flash_bwd_dkv_kernel<D>, dim3((unsigned)B * heads * ((S + kTok - 1) / kTok)), dim3(256), lds_kv,
+                       st, q, kv, dout, lse, delta, dkv, E, heads, L, S, scale);
+    LDM_CHECK_LAUNCH("flash_bwd_dkv_kernel");
+    const size_t lds_q = 2 * (size_t)D * kKP * sizeof(float);
+    static int o2 = opt_in_lds(flash_bwd_dq_kernel<D>, lds_q);
+    if (o2) return o2;
+    hipLaunchKernelGGL(flash_bwd_dq_kernel<D>, dim3((unsigned)B * heads * ((L + kTok - 1) / kTok)), dim3(256), lds_q, st,
+                       q, kv, dout, lse, delta, dq, E, heads, L, S, scale);
+    LDM_CHECK_LAUNCH("flash_bwd_dq_kernel");
+    return 0;
+}
+
+}  // namespace fa
+
+bool attention_flash_supported(int E, int heads) {
+    if (heads <= 0 || E % heads) return false;
+    const int d = E / heads;
+    return d == 64 || d == 128;
+}
+
+int attention_flash(const float* q, const float* kv, float* out, float* lse, int32_t B, int32_t E, int32_t heads,
+                    int32_t L, int32_t S, float scale, bool tok, hipStream_t st) {
+    LDM_REQUIRE(q && kv && out && B > 0 && L > 0 && S > 0, "attention (flash): bad argument");
+    LDM_REQUIRE(attention_flash_supported(E, heads), "attention (flash): head dim must be 64 or 128");
+    LDM_REQUIRE(!(tok && lse), "attention (flash): lse output with channel-major q only");
+    const int d = E / heads;
+#define LDM_FA(D)                                                                                   \
+    if (d == D) {                                                                                   \
+        if (tok) return fa::fwd_launch<D, true, false>(q, kv, out, nullptr, B, E, heads, L, S, scale, st); \
+        if (lse) return fa::fwd_launch<D, false, true>(q, kv, out, lse, B, E, heads, L, S, scale, st);     \
+        return fa::fwd_launch<D, false, false>(q, kv, out, nullptr, B, E, heads, L, S, scale, st);         \
+    }
+    LDM_FA(64)
+    LDM_FA(128)
+#undef LDM_FA
+    return fail(3, "attention (flash): no instance");
+}
+
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" int ldm_attention_forward_lse(const float* q, const float* kv, float* out, float* lse, int32_t B, int32_t E,
+                                         int32_t heads, int32_t L, int32_t S, float scale, void* stream) {
+    LDM_REQUIRE(lse, "attention_forward_lse: null lse");
+    return attention_flash(q, kv, out, lse, B, E, heads, L, S, scale, false, (hipStream_t)stream);
+}
+
+extern "C" int ldm_attention_backward_flash(const float* q, const float* kv, const float* out, const float* lse,
+                                            const float* dout, float* dq, float* dkv, float* delta_ws, int32_t B,
+                                            int32_t E, int32_t heads, int32_t L, int32_t S, float scale, void* stream) {
+    LDM_REQUIRE(q && kv && out && lse && dout && dq && dkv && delta_ws && B > 0 && L > 0 && S > 0,
+                "attention_backward_flash: bad argument");
+    LDM_REQUIRE(attention_flash_supported(E, heads), "attention_backward_flash: head dim must be 64 or 128");
+    const int d = E / heads;
+    if (d == 64)
+        return fa::bwd_launch<64>(q, kv, out, lse, dout, dq, dkv, delta_ws, B, E, heads, L, S, scale, (hipStream_t)stream);
+    return fa::bwd_launch<128>(q, kv, out, lse, dout, dq, dkv, delta_ws, B, E, heads, L, S, scale, (hipStream_t)stream);
+}
+
+extern "C" int ldm_attention_flash_supported(int32_t E, int32_t heads) { return attention_flash_supported(E, heads) ? 1 : 0; }

@@ -702,6 +702,8 @@ int attention_core_ex(const float* q, const float* kv, float* out, int32_t B, in
         LDM_ATT(2, 64, 64, 128, 16)
 #undef LDM_ATT
     }
+    // wider maps (L or S > 64: mels wider than 512 frames, SURVEY's shape S): KV-tiled online softmax
+    if (attention_flash_supported(E, heads)) return attention_flash(q, kv, out, nullptr, B, E, heads, L, S, scale, tok, st);
     // generic VALU fallback (head dims not a multiple of the MFMA tile)
     LDM_REQUIRE(!tok, "attention: token-major layout needs an MFMA instance for this head size");
     const size_t lds = ((size_t)d * kAttnLT + 2 * (size_t)d * S + (size_t)kAttnLT * S) * sizeof(float);

@@ -105,6 +105,11 @@ SIGNATURES = {
     "ldm_sinusoid_embed": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_vp]),
     "ldm_time_mlp_forward": (c_int32, [c_vp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_attention_core": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_vp]),
+    "ldm_attention_flash_supported": (c_int32, [c_int32, c_int32]),
+    "ldm_attention_forward_lse": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                            c_float, c_vp]),
+    "ldm_attention_backward_flash": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32,
+                                               c_int32, c_int32, c_int32, c_float, c_vp]),
     "ldm_attention_fold_keys": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_float, c_fp, c_fp,
                                           c_vp]),
     "ldm_attention_folded": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,

@@ -72,6 +72,21 @@ class UNetEngine:
         ps += [tm[1].weight, tm[1].bias, tm[3].weight, tm[3].bias]
         return ps
 
+    @staticmethod
+    def supports(channels):
+        """The fused engine keeps the UNet's activations NHWC, which its MFMA conv instances need 8-aligned
+        channel counts for (enc1's input, dec1's output); other latent widths (UNet(1, 1) on a raw mel, the
+        VAE's default latent_dim=4) run the per-layer path (UNet._layerwise, NCHW kernels)."""
+        return channels % 8 == 0 and channels >= 16
+
+    @staticmethod
+    def fold_applies(shape):
+        """The folded cross-attentions re-associate the scores' contraction from d to E per head: that pays
+        while the key count S stays below ~E/3 (the saved Q projection is L*E*E, the extra score work
+        (heads-1)*L*S*E), and its LDS-resident instances cover S <= 64 (CA2) / 32 (CA1).  Wider latents (mels
+        beyond 512 frames) run the literal loop with the KV-tiled attention (flash.hip)."""
+        return shape.H * shape.W <= 1024
+
     def weights(self, shape):
         """UNetWeights for this shape, re-packing only the parameters whose _version moved."""
         skey = (shape.B, shape.C, shape.H, shape.W, shape.nf)
@@ -131,7 +146,7 @@ class UNetEngine:
             w.ca_bkv[j] = ipb.data_ptr() + E * 4
             w.ca_bo[j] = a.out_proj.bias.data_ptr()
         folded = {}
-        if self.fold:
+        if self.fold and self.fold_applies(shape):
             # enc4 o out_proj(CA2) and bottleneck o out_proj(CA1), packed with those layers' plans
             for j, (layer, conv, ca) in enumerate(((3, u.enc4, u.cross_attention2), (4, u.bottleneck, u.cross_attention1))):
                 a = ca.multihead_attn

@@ -281,9 +281,14 @@ def _kl_backward(ctx, g):
 
 def attention_core(q, kv, heads):
     def fwd(store, q_, kv_):
+        store["heads"] = heads
+        if store["grad"] and ops.attention_uses_flash(q_.shape[1], heads, q_.shape[2], kv_.shape[2]):
+            # wide maps: the KV-tiled kernels, whose backward needs the output and the per-query log-sum-exp
+            out, lse = ops.attention_forward_lse(q_, kv_, heads)
+            store["saved"] = (q_, kv_, out, lse)
+            return out
         out = ops.attention_core(q_, kv_, heads)
         store["saved"] = (q_, kv_)
-        store["heads"] = heads
         return out
 
     return hip_apply("attention_core", fwd, q, kv)
@@ -291,6 +296,10 @@ def attention_core(q, kv, heads):
 
 @register_backward("attention_core")
 def _attention_backward(ctx, gout):
-    q, kv = ctx.saved_tensors
+    saved = ctx.saved_tensors
+    if len(saved) == 4:
+        q, kv, out, lse = saved
+        return ops.attention_backward_flash(q, kv, out, lse, gout, ctx.store["heads"])
+    q, kv = saved
     dq, dkv = ops.attention_backward(q, kv, gout, ctx.store["heads"])
     return dq, dkv

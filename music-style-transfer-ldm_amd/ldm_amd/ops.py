@@ -524,6 +524,38 @@ def attention_core(q, kv, heads):
     return out
 
 
+def attention_uses_flash(E, heads, Lq, S):
+    """True when the KV-tiled kernels (flash.hip) carry the attention: L or S beyond the LDS-resident
+    instances of ldm_attention_core (64 tokens)."""
+    return max(Lq, S) > 64 and bool(L.load().ldm_attention_flash_supported(int(E), int(heads)))
+
+
+def attention_forward_lse(q, kv, heads):
+    """q [B,E,L], kv [B,2E,S] -> (out [B,E,L], lse [B,heads,L]) on the KV-tiled online-softmax kernel."""
+    require_device(q, kv)
+    B, E, Lq = q.shape
+    S = kv.shape[2]
+    out = torch.empty_like(q)
+    lse = torch.empty((B, heads, Lq), device=q.device, dtype=torch.float32)
+    scale = float(math.sqrt(1.0 / float(E // heads)))
+    L.call("ldm_attention_forward_lse", q.data_ptr(), kv.data_ptr(), out.data_ptr(), lse.data_ptr(), B, E, heads, Lq, S,
+           scale, stream_handle())
+    return out, lse
+
+
+def attention_backward_flash(q, kv, out, lse, dout, heads):
+    q, kv, out, dout = f32c(q), f32c(kv), f32c(out), f32c(dout)
+    B, E, Lq = q.shape
+    S = kv.shape[2]
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    delta = torch.empty((B, heads, Lq), device=q.device, dtype=torch.float32)
+    scale = float(math.sqrt(1.0 / float(E // heads)))
+    L.call("ldm_attention_backward_flash", q.data_ptr(), kv.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(),
+           dq.data_ptr(), dkv.data_ptr(), delta.data_ptr(), B, E, heads, Lq, S, scale, stream_handle())
+    return dq, dkv
+
+
 _COEF_CACHE = IdCache()
 
 

@@ -291,7 +291,7 @@ class UNet(nn.Module):
 
     def forward(self, z, t, style_embedding: dict = None):
         s5, s6 = style_embedding["s5"], style_embedding["s6"]
-        if HF._needs_grad(z, s5, s6, *self.parameters()):
+        if HF._needs_grad(z, s5, s6, *self.parameters()) or not UNetEngine.supports(z.shape[1]):
             return self._layerwise(z, t, s5, s6)
         return engine_for(self).forward(z, t, s5, s6)
 
@@ -388,8 +388,15 @@ class LDM(nn.Module):
         eps_logs = torch.empty_like(x0_logs)
         s5 = ops.f32c(style_embedding["s5"])
         s6 = ops.f32c(style_embedding["s6"])
+        coefs = coefs.to(dev)
         with torch.no_grad():
-            engine_for(self.unet).ddim_loop(x, s5, s6, t_table, coefs.to(dev), float(eta), x0_logs, eps_logs)
+            if UNetEngine.supports(x.shape[1]):
+                engine_for(self.unet).ddim_loop(x, s5, s6, t_table, coefs, float(eta), x0_logs, eps_logs)
+            else:   # latent widths the fused engine does not take: per-layer UNet + the DDIM update kernel
+                emb = {"s5": s5, "s6": s6}
+                for i in range(n):
+                    eps = self.unet(x, t_table[i], emb)
+                    ops.ddim_step_(x, eps, coefs[i].contiguous(), float(eta), x0_logs[i], eps_logs[i])
         logs["timesteps"] = [int(v) for v in times[:-1]]
         logs["pred_x0"] = list(x0_logs.unbind(0))
         logs["noise_pred"] = list(eps_logs.unbind(0))

@@ -47,7 +47,9 @@ def sinusoid(t, dim=128):
 
 
 def time_mlp(sd, p, t):
-    h = F.linear(sinusoid(t), _g(sd, p + "time_mlp.1.weight"), _g(sd, p + "time_mlp.1.bias"))
+    w1 = _g(sd, p + "time_mlp.1.weight")
+    # the embedding is fp32 in the reference (model.py:239-246); a float64 restatement widens it afterwards
+    h = F.linear(sinusoid(t).to(w1.dtype), w1, _g(sd, p + "time_mlp.1.bias"))
     h = F.gelu(h)
     return F.linear(h, _g(sd, p + "time_mlp.3.weight"), _g(sd, p + "time_mlp.3.bias"))
 

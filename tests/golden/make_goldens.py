@@ -395,7 +395,7 @@ def round3():
     0.01 KL(z0) + MSE(eps_pred, eps) (LPIPS / VGGish left out: remote weights), q_sample noise injected.  Once
     in fp32 and once with forward + losses under torch.autocast("cpu", bfloat16) (train.py:174's region),
     backward outside.  Stored: the loss terms, reconstructed samples 0 and 31, the ten TRAIN_GRAD_KEYS
-    gradients (in_proj rows 0..255)."""
+    gradients (in_proj rows 0..255); and all of it again with the reference model in float64."""
     torch.set_num_threads(8)
     M, L = import_reference()
     G = {}
@@ -427,6 +427,57 @@ def round3():
             g = named[k].grad
             G[f"r3_{name}_grad_" + k] = np32(g[:256] if g.dim() == 2 and g.shape[0] > 256 else g)
         print(name, float(total), flush=True)
+    # the same step in float64 (LDM.forward casts its inputs to fp32, model.py:357, so the reference cannot run
+    # it in float64 itself): the oracle's restatement (oracle/ldm_torch_cpu.py, pinned to the fp32 golden by
+    # tests/test_oracle_golden.py) on float64 recipe weights -- the reference's own fp32 error, per quantity
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import ldm_torch_cpu as TC
+    ldm = M.LDM(32, pretrained_path="")
+    recipe.fill_module(ldm, seed=700)
+    sd = {k: v.detach().double().clone() for k, v in ldm.state_dict().items()}
+    for k, v in sd.items():
+        if v.is_floating_point() and "running_" not in k and not k.startswith("noise_scheduler"):
+            v.requires_grad_(True)
+    ab = M.ForwardDiffusion(200).alpha_bar_t.double()
+    o = TC.ldm_forward(sd, content.double(), style.double(), t, noise.double(), ab, train_decoder=True,
+                       train_encoder=True, state={})
+    dl = torch.mean((o["noise_pred"] - o["noise"]) ** 2)
+    comp = torch.mean((o["reconstructed"] - content.double()) ** 2) + 0.01 * TC.kl_loss(o["z_0"])
+    (comp + dl).backward()
+    G["r3_fp64_compression"] = comp.detach().numpy()
+    G["r3_fp64_diffusion"] = dl.detach().numpy()
+    G["r3_fp64_total"] = (comp + dl).detach().numpy()
+    G["r3_fp64_recon_0_31"] = o["reconstructed"].detach()[[0, R3_B - 1]].numpy()
+    for k in TRAIN_GRAD_KEYS:
+        g = sd[k].grad
+        G["r3_fp64_grad_" + k] = (g[:256] if g.dim() == 2 and g.shape[0] > 256 else g).numpy()
+
+    # (12) width-general attention: the UNet on a latent wider than 64 tokens per cross-attention --
+    # [1,32,16,128] (a 1x128x1024 mel: CA2 L = S = 128, CA1 32) -- forward and a 5-step DDIM (eta 0); and
+    # a reduced SURVEY shape S: UNet(1, 1, 64) straight on a [1,1,64,256] mel with s5 [1,256,16,64] and
+    # s6 [1,512,8,32] (CA2 L = S = 1024, CA1 256).
+    with torch.no_grad():
+        unet = M.UNet(32, 32, 64)
+        recipe.fill_module(unet, seed=100)
+        z = torch.from_numpy(recipe.normal((1, 32, 16, 128), 770))
+        s5 = torch.from_numpy(recipe.uniform01((1, 256, 4, 32), 771))
+        s6 = torch.from_numpy(recipe.uniform01((1, 512, 2, 16), 772))
+        t = torch.tensor([117])
+        G["w128_unet_out"] = np32(unet(z, t, {"s5": s5, "s6": s6}))
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.eval()
+        style = torch.from_numpy(recipe.uniform01((1, 1, 128, 1024), 773))
+        emb = ldm.style_encoder(style)
+        zT = torch.from_numpy(recipe.normal((1, 32, 16, 128), 774))
+        x, _ = ldm.style_conditioned_ddim_sample(zT, emb, timesteps=5, eta=0.0)
+        G["w128_ddim5_x"] = np32(x)
+        us = M.UNet(1, 1, 64)
+        recipe.fill_module(us, seed=101)
+        zs = torch.from_numpy(recipe.normal((1, 1, 64, 256), 775))
+        s5s = torch.from_numpy(recipe.uniform01((1, 256, 16, 64), 776))
+        s6s = torch.from_numpy(recipe.uniform01((1, 512, 8, 32), 777))
+        G["shapeS_unet_out"] = np32(us(zs, torch.tensor([42]), {"s5": s5s, "s6": s6s}))
     path = os.path.join(HERE, "ref_goldens_r3.npz")
     np.savez_compressed(path, **G)
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")

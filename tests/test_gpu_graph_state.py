@@ -9,6 +9,8 @@
   entries): it loads into torch.optim.Adam and into the eager form, and the next step there matches
   torch.optim.Adam continuing from the same state (1e-6).
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -132,7 +134,7 @@ def test_capturable_adam_state_dict_round_trip(cuda, target):
         other = torch.optim.Adam(qs, lr=5e-4)
     else:
         other = hoptim.Adam(qs, lr=5e-4, capturable=(target == "capturable"))
-    other.load_state_dict(sd)
+    other.load_state_dict(copy.deepcopy(sd))   # (load_state_dict keeps same-device tensors by reference)
     for i, (a, b) in enumerate(zip(ps_ref, qs)):
         g = _rand(a.shape, 900 + i)
         a.grad = g.clone()

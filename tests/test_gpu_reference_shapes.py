@@ -134,3 +134,24 @@ def test_unet_dimensions(cuda, grad):
     assert z.requires_grad == grad
     ref = TC.unet(sd, x, t, style["s5"], style["s6"])
     assert rel_err(z.detach().cpu().numpy(), ref.numpy()) < TOL
+
+
+def test_ldm_latent_dim4_sampling(cuda):
+    """A latent width the fused engine does not take (the VAE's default latent_dim=4, model.py:14): the UNet
+    runs per layer and the reverse loop is the per-step UNet + DDIM-update kernel.  3 DDIM steps (eta 1)
+    against the oracle's reverse loop on the same weights, 1e-4."""
+    import models.model as M
+    from oracle import ldm_torch_cpu as TC
+    torch.manual_seed(7)
+    ldm = M.LDM(4, pretrained_path="").eval()
+    sd = _sd(ldm)
+    ldm = ldm.to(cuda)
+    style = torch.rand((2, 1, 64, 64), generator=torch.Generator().manual_seed(17))
+    zT = _randn((2, 4, 8, 8), 18)
+    with torch.no_grad():
+        emb = ldm.style_encoder(style.to(cuda))
+        x, logs = ldm.style_conditioned_ddim_sample(zT.to(cuda), emb, timesteps=4, eta=1.0)
+        embr = TC.style_encoder(sd, style)
+        xr = TC.reverse_loop(sd, TC.schedule(200)[2], zT, embr["s5"], embr["s6"], TC.ddim_times(200, 4), 1.0)
+    assert logs["timesteps"] == TC.ddim_times(200, 4)[:-1].tolist()
+    assert rel_err(x.cpu().numpy(), xr.numpy()) < TOL

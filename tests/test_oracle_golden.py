@@ -238,3 +238,60 @@ def test_vggish_feature_loss(goldens_vgg, case):
     out = TC.vggish_feature_loss(sd, p, t)
     assert rel_err(out.numpy(), goldens_vgg[f"vgg_{case}_loss"]) < 2e-6
 
+
+
+# ---- round 3: config 3's shape, wide latents (ref_goldens_r3.npz) ----------------------------------------
+@pytest.fixture(scope="module")
+def goldens3():
+    import os
+    from conftest import ROOT
+    return np.load(os.path.join(ROOT, "tests", "golden", "ref_goldens_r3.npz"))
+
+
+def test_wide_latent_unet_and_ddim(M, ldm_sd, goldens3):
+    """UNet on a [1,32,16,128] latent (CA2 L = S = 128) and a 5-step DDIM there; UNet(1, 1, 64) on a
+    [1,1,64,256] mel (reduced SURVEY shape S: CA2 L = S = 1024)."""
+    sd = sd_for(lambda: M.UNet(32, 32, 64), 100)
+    z = torch.from_numpy(recipe.normal((1, 32, 16, 128), 770))
+    s5 = torch.from_numpy(recipe.uniform01((1, 256, 4, 32), 771))
+    s6 = torch.from_numpy(recipe.uniform01((1, 512, 2, 16), 772))
+    with torch.no_grad():
+        y = TC.unet(sd, z, torch.tensor([117]), s5, s6, p="")
+        assert rel_err(y.numpy(), goldens3["w128_unet_out"]) < 2e-6
+        ab = TC.schedule(200)[2]
+        style = torch.from_numpy(recipe.uniform01((1, 1, 128, 1024), 773))
+        emb = TC.style_encoder(ldm_sd, style)
+        zT = torch.from_numpy(recipe.normal((1, 32, 16, 128), 774))
+        x = TC.reverse_loop(ldm_sd, ab, zT, emb["s5"], emb["s6"], TC.ddim_times(200, 5), 0.0)
+        assert rel_err(x.numpy(), goldens3["w128_ddim5_x"]) < 1e-5
+        sds = sd_for(lambda: M.UNet(1, 1, 64), 101)
+        zs = torch.from_numpy(recipe.normal((1, 1, 64, 256), 775))
+        s5s = torch.from_numpy(recipe.uniform01((1, 256, 16, 64), 776))
+        s6s = torch.from_numpy(recipe.uniform01((1, 512, 8, 32), 777))
+        ys = TC.unet(sds, zs, torch.tensor([42]), s5s, s6s, p="")
+        assert rel_err(ys.numpy(), goldens3["shapeS_unet_out"]) < 2e-6
+
+
+def test_config3_train_step(M, goldens3):
+    """The restated train step at config 3's shape (batch 32, 1x128x512, every module in train mode) against
+    the reference's fp32 golden: losses, reconstructed samples 0 / 31, two gradients."""
+    sd = sd_for(lambda: M.LDM(32, pretrained_path=""), 700)
+    trained = [k for k in sd if sd[k].is_floating_point() and "running_" not in k and "num_batches" not in k]
+    for k in trained:
+        sd[k].requires_grad_(True)
+    B = 32
+    content = torch.from_numpy(recipe.uniform01((B, 1, 128, 512), 760))
+    style = torch.from_numpy(recipe.uniform01((B, 1, 128, 512), 761))
+    t = torch.from_numpy(recipe.timesteps(B, 762))
+    noise = torch.from_numpy(recipe.normal((B, 32, 16, 64), 763))
+    assert np.array_equal(t.numpy(), goldens3["r3_t"])
+    ab = TC.schedule(200)[2]
+    o = TC.ldm_forward(sd, content, style, t, noise, ab, train_decoder=True, train_encoder=True, state={})
+    dl = torch.mean((o["noise_pred"] - o["noise"]) ** 2)
+    comp = torch.mean((o["reconstructed"] - content) ** 2) + 0.01 * TC.kl_loss(o["z_0"])
+    (comp + dl).backward()
+    assert rel_err(comp.detach().numpy(), goldens3["r3_fp32_compression"]) < 1e-5
+    assert rel_err(dl.detach().numpy(), goldens3["r3_fp32_diffusion"]) < 1e-5
+    assert rel_err(o["reconstructed"].detach()[[0, B - 1]].numpy(), goldens3["r3_fp32_recon_0_31"]) < 1e-5
+    for k in ("unet.dec1.weight", "decoder.decoder.6.weight"):
+        assert rel_err(sd[k].grad.numpy(), goldens3["r3_fp32_grad_" + k]) < 1e-4, k
