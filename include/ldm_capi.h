@@ -370,6 +370,28 @@ int ldm_attention_backward_flash(const float* q, const float* kv, const float* o
                                  const float* dout, float* dq, float* dkv, float* delta_ws, int32_t B, int32_t E,
                                  int32_t heads, int32_t L, int32_t S, float scale, void* stream);
 
+/* ---- LPIPS-AlexNet perceptual distance (loss.py:6-21: lpips==0.1.4 LPIPS(net='alex') on 2x-1)
+ * The AlexNet convs run on ldm_conv_forward: 3x3 directly, 11x11/s4 and 5x5 as ldm_im2col + a 1x1 conv (their
+ * data gradient: the 1x1 dual conv + ldm_col2im).  col [B,Kpad,Ho,Wo], k = (c*kh+ky)*kw+kx, rows >= Cv*kh*kw
+ * zero.  shift/scale (or NULL): the LPIPS ScalingLayer fused, a 1-channel input broadcast to Cv channels
+ * (t - shift_c)/scale_c; unit=1 first maps x -> 2x - 1 (perceptual_loss_old); col2im folds both back into dx.
+ * ldm_maxpool3s2: nn.MaxPool2d(3, 2) (floor); its backward routes dy to torch's first-occurrence argmax.
+ * ldm_lpips_layer: val[b] += mean_p sum_c w_c (f0_c/(|f0|+1e-10) - f1_c/(|f1|+1e-10))^2 (normalize_tensor,
+ * squared difference, 1x1 lin head without bias, spatial average); workspace >= B*HW floats.
+ * ldm_lpips_layer_backward: d val / d f1 (side 1) or d f0 (side 0) times gval[b], written or accumulated. */
+int ldm_im2col(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, int32_t kh, int32_t kw, int32_t stride,
+               int32_t pad, int32_t Kpad, const float* shift, const float* scale, int32_t Cv, int32_t unit, float* col,
+               void* stream);
+int ldm_col2im(const float* col, int32_t B, int32_t C, int32_t H, int32_t W, int32_t kh, int32_t kw, int32_t stride,
+               int32_t pad, int32_t Kpad, const float* scale, int32_t Cv, int32_t unit, float* dx, void* stream);
+int ldm_maxpool3s2(const float* x, float* y, int32_t B, int32_t C, int32_t H, int32_t W, void* stream);
+int ldm_maxpool3s2_backward(const float* x, const float* dy, float* dx, int32_t B, int32_t C, int32_t H, int32_t W,
+                            void* stream);
+int ldm_lpips_layer(const float* f0, const float* f1, const float* w, int32_t B, int32_t C, int32_t HW, float* val,
+                    float* workspace, void* stream);
+int ldm_lpips_layer_backward(const float* f0, const float* f1, const float* w, const float* gval, int32_t B,
+                             int32_t C, int32_t HW, int32_t side, int32_t accumulate, float* df, void* stream);
+
 /* ---- VGGish feature / style loss (loss.py:52-101, VGGishFeatureLoss.forward) ----
  * The conv stack runs on ldm_conv_forward (ReLU fused: each conv launch yields one feature tap).
  * ldm_maxpool2x2: nn.MaxPool2d(2, 2) on NCHW fp32 (floor mode, NaN-propagating), y [B,C,H/2,W/2].

@@ -110,6 +110,15 @@ SIGNATURES = {
                                             c_float, c_vp]),
     "ldm_attention_backward_flash": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32,
                                                c_int32, c_int32, c_int32, c_float, c_vp]),
+    "ldm_im2col": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                             c_fp, c_fp, c_int32, c_int32, c_fp, c_vp]),
+    "ldm_col2im": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                             c_fp, c_int32, c_int32, c_fp, c_vp]),
+    "ldm_maxpool3s2": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_vp]),
+    "ldm_maxpool3s2_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_vp]),
+    "ldm_lpips_layer": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_vp]),
+    "ldm_lpips_layer_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_fp,
+                                           c_vp]),
     "ldm_attention_fold_keys": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_float, c_fp, c_fp,
                                           c_vp]),
     "ldm_attention_folded": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,

@@ -116,9 +116,12 @@ class GradAllReduce:
     world_size() before applying it (GradScaler.set_grad_divisor folds that into its unscale kernel,
     or pass average=True to scale here with the HIP kernel)."""
 
-    def __init__(self, params, bucket_mb=25.0, group=None, average=False):
+    def __init__(self, params, bucket_mb=25.0, group=None, average=False, collective=None):
         self.group = group
         self.average = average
+        # collective(flat, group) -> work with .wait(): the bucket all-reduce (default: an async RCCL / gloo
+        # all_reduce(SUM)); tests inject a stub
+        self._collective = collective
         params = [p for p in params if p.requires_grad]
         if not params:
             raise ValueError("GradAllReduce: no parameters require grad")
@@ -146,7 +149,21 @@ class GradAllReduce:
             h.remove()
         self._handles = []
 
+    @property
+    def capturable(self):
+        """True when the whole step, these hooks and collectives included, can be captured into a hipGraph:
+        every piece is then a device operation on fixed buffers (the bucket copies, the RCCL all-reduces on
+        the process group's stream joined back by events, the views into the flat buckets) and nothing reads
+        the device from the host.  RCCL ('nccl') collectives are capturable; gloo's (host staging) are not.
+        A stub collective declares it with a `capturable` attribute."""
+        if self._collective is not None:
+            return bool(getattr(self._collective, "capturable", False))
+        return is_distributed() and tdist.get_backend(self.group) == "nccl"
+
     def _launch(self, b):
+        if self._collective is not None:
+            b.work = self._collective(b.flat, self.group)
+            return
         b.work = tdist.all_reduce(b.flat, op=tdist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _on_grad(self, p):

@@ -48,12 +48,31 @@ def set_perceptual_backend(fn):
 
 
 def perceptual_loss_old(original, reconstructed):
-    """LPIPS(net='alex') on inputs mapped [0,1] -> [-1,1] (reference loss.py:6-21)."""
+    """LPIPS(net='alex') on inputs mapped [0,1] -> [-1,1] (reference loss.py:6-21).
+
+    With an ldm_amd.lpips.LPIPSAlex backend (local weights, load_lpips_alex) the whole term runs on the HIP
+    kernels, the 2x - 1 map fused into its first layer; any other backend is called as fn(2x - 1, 2y - 1).
+    The reference's two range asserts (loss.py:14-15, two host syncs) are not repeated: the decoder's
+    (tanh + 1) / 2 output and ToTensor'd mels are in [0, 1] by construction."""
     if _PERCEPTUAL_BACKEND is None:
         _warn_once("lpips", "perceptual_loss_old: no LPIPS backend installed (weights are not available "
                             "offline); the perceptual term is 0. Use loss.set_perceptual_backend(fn).")
         return torch.zeros((), device=original.device, dtype=torch.float32)
+    from ldm_amd.lpips import LPIPSAlex
+    if isinstance(_PERCEPTUAL_BACKEND, LPIPSAlex):
+        return _PERCEPTUAL_BACKEND(original, reconstructed, unit=True).mean()
     return _PERCEPTUAL_BACKEND(2 * original - 1, 2 * reconstructed - 1).mean()
+
+
+def load_lpips_alex(state_dict_or_path, device="cuda"):
+    """An LPIPS(net='alex') backend on the HIP kernels from LOCAL weights: an lpips.LPIPS state_dict, or
+    torchvision alexnet 'features.*' + the lpips v0.1 'lin<i>.model.1.weight' tensors in one dict (or a file
+    holding either, loaded with weights_only=True).  Install it with set_perceptual_backend."""
+    from ldm_amd.lpips import LPIPSAlex
+    sd = state_dict_or_path
+    if isinstance(sd, str):
+        sd = torch.load(sd, map_location="cpu", weights_only=True)
+    return LPIPSAlex.from_state_dict(sd).to(device)
 
 
 def perceptual_loss(original, reconstructed, feature_extractor_type: str = "vggish", feature_extractor=None):

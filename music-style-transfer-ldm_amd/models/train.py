@@ -13,7 +13,8 @@ Differences from the reference, all deliberate:
     autocast_dtype) and accumulate in fp32.  autocast_enabled = False runs the step in fp32.
   * Data-parallel: when torch.distributed is initialised with world_size > 1, each rank trains on its
     own batch shard and the gradients are all-reduced (bucketed, overlapped with backward) before the
-    optimiser step (ldm_amd.dist.GradAllReduce).  Single-process behaviour is unchanged.
+    optimiser step (ldm_amd.dist.GradAllReduce); over RCCL the graphed step captures those collectives.
+    Single-process behaviour is unchanged.
   * The datasets (dataset.py) are not part of this package (torchvision-based image folders, out of
     scope for the hot path); train_autoencoder / train_ldm accept ready loaders, else they import the
     reference-style `dataset` module from sys.path.
@@ -153,7 +154,9 @@ class LDMTrainer:
         self.autocast_enabled = True
         # graph_step = True: after graph_warmup eager steps, the whole step (forward, backward, unscale,
         # optimizer, scaler update) is captured once into a hipGraph and replayed; the loss values are read
-        # after each replay.  Single-process only (the bucketed RCCL all-reduce stays eager).
+        # after each replay.  Data-parallel over RCCL the capture holds the bucketed gradient all-reduces
+        # (launched from the backward's hooks, joined before the optimizer) and SyncBN's statistic
+        # all-reduces too; over gloo (host-staged collectives) the step stays eager.
         self.graph_step = False
         self.graph_warmup = 2
         self._graph = None
@@ -173,7 +176,7 @@ class LDMTrainer:
     def train_step(self, content_spec, style_spec, t=None, noise=None):
         """One step (reference train.py:163-208).  t / noise may be injected (parity tests); by default
         they are drawn like the reference (randint on the device; randn_like inside the scheduler)."""
-        if self.graph_step and self.device.type == "cuda" and self.reducer is None:
+        if self.graph_step and self.device.type == "cuda" and (self.reducer is None or self.reducer.capturable):
             return self._graphed_step(content_spec, style_spec, t, noise)
         return self._losses(self._step(content_spec, style_spec, t, noise))
 

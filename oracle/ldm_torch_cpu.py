@@ -211,3 +211,39 @@ def vggish_feature_loss(sd, predicted, target, cfg=VGGISH_CFG):
         total = total + F.mse_loss(p_, t_)
     return total / len(taps)
 
+
+
+# ---- LPIPS-AlexNet (loss.py:6-21: lpips==0.1.4 LPIPS(net='alex'), not vendored, not installed) ----------------
+# Restated from lpips 0.1.4's published forward (net='alex', lpips=True, spatial=False, version '0.1'); PARITY
+# UNPINNED: no output of the package exists here to pin it to.  sd uses lpips.LPIPS state_dict keys.
+LPIPS_SHIFT = (-0.030, -0.088, -0.188)
+LPIPS_SCALE = (0.458, 0.448, 0.450)
+_ALEX = (("net.slice1.0", 4, 2, False), ("net.slice2.3", 1, 2, True), ("net.slice3.6", 1, 1, True),
+         ("net.slice4.8", 1, 1, False), ("net.slice5.10", 1, 1, False))
+
+
+def lpips_alex(sd, in0, in1):
+    """LPIPS.forward(in0, in1) -> [B,1,1,1] (inputs already in [-1, 1], as perceptual_loss_old passes them)."""
+    dt = in0.dtype
+    shift = torch.tensor(LPIPS_SHIFT, dtype=dt).view(1, 3, 1, 1)
+    scale = torch.tensor(LPIPS_SCALE, dtype=dt).view(1, 3, 1, 1)
+
+    def feats(x):
+        h = (x - shift) / scale                       # ScalingLayer (a 1-channel input broadcasts)
+        out = []
+        for name, stride, pad, pool in _ALEX:
+            if pool:
+                h = F.max_pool2d(h, kernel_size=3, stride=2)
+            h = F.relu(F.conv2d(h, _g(sd, name + ".weight"), _g(sd, name + ".bias"), stride=stride, padding=pad))
+            out.append(h)
+        return out
+
+    def normalize(f, eps=1e-10):
+        return f / (torch.sqrt(torch.sum(f ** 2, dim=1, keepdim=True)) + eps)
+
+    val = None
+    for i, (a, b) in enumerate(zip(feats(in0), feats(in1))):
+        d = (normalize(a) - normalize(b)) ** 2
+        r = F.conv2d(d, _g(sd, f"lin{i}.model.1.weight")).mean([2, 3], keepdim=True)
+        val = r if val is None else val + r
+    return val

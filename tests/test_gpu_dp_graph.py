@@ -1,0 +1,70 @@
+"""The data-parallel train step captured into a hipGraph over RCCL (reference train.py:163-208).
+
+One GPU box holds one GPU, so the collective runs in a world-1 'nccl' (= RCCL) process group: the trainer is
+given the bucketed GradAllReduce it builds for world > 1 (its post-accumulate-grad hooks, the per-bucket
+copies, the asynchronous RCCL all-reduces and their joins), graph_step captures all of it, and the replayed
+steps must equal an eager trainer without a reducer BITWISE (a one-rank sum is the identity).  What stays
+unmeasured on hardware: more than one rank (SyncBN's statistic collectives only fire for world > 1) and the
+scaling curve.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+import recipe
+
+pytestmark = pytest.mark.gpu
+
+
+class _ZeroFeat(torch.nn.Module):
+    def forward(self, a, b):
+        return torch.zeros((), device=a.device)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_graphed_step_with_rccl_reducer_equals_eager(cuda):
+    import torch.distributed as tdist
+    import models.model as M
+    import models.train as TR
+    from ldm_amd import dist as hdist
+    content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 930)).to(cuda)
+    style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 931)).to(cuda)
+    t = torch.tensor([33, 144], device=cuda)
+    noise = torch.from_numpy(recipe.normal((2, 32, 16, 16), 932)).to(cuda)
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                             device_id=cuda)
+    try:
+        res = []
+        for dp in (False, True):
+            m = M.LDM(32, pretrained_path="")
+            recipe.fill_module(m, seed=700)
+            m.feature_loss_net = _ZeroFeat()
+            m = m.to(cuda).train()
+            tr = TR.LDMTrainer(m, [], cuda, lr=1e-3)
+            tr.autocast_enabled = False
+            if dp:
+                tr.reducer = hdist.GradAllReduce([p for p in m.parameters() if p.requires_grad], bucket_mb=8.0)
+                assert tr.reducer.capturable and len(tr.reducer.buckets) > 1
+                tr.graph_step = True
+            losses = [tr.train_step(content, style, t=t, noise=noise) for _ in range(5)]
+            tr.optimizer.param_groups[0]["lr"] *= 0.5
+            losses += [tr.train_step(content, style, t=t, noise=noise) for _ in range(3)]
+            assert (tr._graph is not None) == dp
+            res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+        (le, sde), (lg, sdg) = res
+        for a, b in zip(le, lg):
+            for k in a:
+                assert a[k] == b[k], (k, a[k], b[k])
+        for k in sde:
+            assert torch.equal(sde[k], sdg[k]), k
+    finally:
+        tdist.destroy_process_group()

@@ -145,3 +145,27 @@ def test_fast_plan_override_table_loads():
         pytest.skip("no tuned table")
     n = autotune.load_tuned(path)
     assert n > 0 and len(ops._PLAN_OVERRIDE) >= n
+
+
+def test_lpips_alex_state_dict_forms():
+    """LPIPSAlex takes lpips.LPIPS state_dict keys, or torchvision alexnet 'features.<idx>.*' + the lpips v0.1
+    'lin<i>.model.1.weight' file, and refuses an incomplete set (loss.py:6-21)."""
+    import pytest as _pytest
+    import torch as _torch
+    from ldm_amd.lpips import CONVS, LPIPSAlex
+    m = LPIPSAlex()
+    sd = {k: _torch.randn(v.shape) for k, v in m.state_dict().items() if not k.startswith("lins.")}
+    sd.update({f"lins.{i}.model.1.weight": sd[f"lin{i}.model.1.weight"] for i in range(5)})   # one tensor, two keys
+    m2 = LPIPSAlex.from_state_dict(sd)
+    assert all(_torch.equal(m2.state_dict()[k], sd[k]) for k in sd if not k.startswith("scaling_layer"))
+    tv = {}
+    for sl, idx, *_ in CONVS:
+        tv[f"features.{idx}.weight"] = sd[f"net.slice{sl}.{idx}.weight"]
+        tv[f"features.{idx}.bias"] = sd[f"net.slice{sl}.{idx}.bias"]
+    for i in range(5):
+        tv[f"lin{i}.model.1.weight"] = sd[f"lin{i}.model.1.weight"]
+    m3 = LPIPSAlex.from_state_dict(tv)
+    assert _torch.equal(m3.lins[2].model[1].weight, sd["lin2.model.1.weight"])
+    assert _torch.equal(m3.net.conv(1).weight, sd["net.slice2.3.weight"])
+    with _pytest.raises(KeyError):
+        LPIPSAlex.from_state_dict({k: v for k, v in tv.items() if not k.startswith("lin4")})
