@@ -105,7 +105,10 @@ def _graph_time_us(fn, reps):
 STEP_LAYERS = [  # (name, Cin, Cout, mode 0 conv s1 / 1 conv s2 / 2 convT s2, input scale divisor)
     ("enc1", 32, 64, 0, 1), ("enc2", 64, 128, 1, 1), ("enc3", 128, 256, 1, 2), ("enc4", 256, 512, 1, 4),
     ("bottleneck", 512, 512, 0, 8), ("dec4", 512, 256, 2, 8), ("dec3", 256, 128, 2, 4), ("dec2", 128, 64, 2, 2)]
-USTEP_LAYERS = (0, 5, 7)   # csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip
+USTEP_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_USTEP_LAYERS", "0x81"), 0) >> l) & 1)
+# ^ csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip (enc1, dec2)
+KS_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_UCONV_KS", "0x7c"), 0) >> l) & 1)
+# ^ csrc/uconv.hip ks_on(): the layers that run the K-split step kernel (enc3, enc4, bottleneck, dec4, dec3)
 
 
 def time_step_layers(engine, B, H, W, dev, reps=50):
@@ -128,7 +131,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         sk = torch.randn(B, hout, wout, cout, device=dev) if mode == 2 else None
         dt = int(w.step_dtype)
         v3 = int(w.use_step) == 2 and dt == 0 and layer in USTEP_LAYERS and B % 4 == 0 and (H, W) == (16, 64)
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else 0
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else int(lib.ldm_step_workspace_floats(B, H, W))
         ws = torch.zeros(max(1, nws), device=dev)
         args = (x.data_ptr(), w.step_w[layer], bias, None if bc is None else bc.data_ptr(),
                 None if sk is None else sk.data_ptr(), y.data_ptr())
@@ -137,7 +140,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
             stp = torch.cuda.current_stream().cuda_stream
             if v3:
                 return lib.ldm_ustep_conv(layer, B, *args, ws.data_ptr() if nws else None, stp)
-            return lib.ldm_step_conv_dt(layer, B, H, W, *args, dt, stp)
+            return lib.ldm_step_conv_ws(layer, B, H, W, *args, dt, ws.data_ptr() if nws else None, stp)
 
         L.check(run(), name)
         us = _graph_time_us(run, reps)
@@ -145,7 +148,8 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         fl = 2.0 * B * cout * hout * wout * cin * taps
         by = 4.0 * (cin * cout * 9 + B * cin * hin * win + B * cout * hout * wout)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else "uconv_kernel")
+                     "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else
+                                                          ("uconv_kernel (K split)" if layer in KS_LAYERS else "uconv_kernel"))
                      + ("" if dt == 0 else (" fp16 operands" if dt == 1 else " bf16 operands"))}
     # the folded cross-attentions of the loop
     for name, E, Lt in (("attn2_folded", 256, H * W // 16), ("attn1_folded", 512, H * W // 64)):

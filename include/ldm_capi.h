@@ -311,6 +311,16 @@ int64_t ldm_step_packed_floats(int32_t layer);
 int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream);
 int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                   const float* bias, const float* bcast, const float* skip, float* y, void* stream);
+/* The step kernels of the deep layers (enc3, enc4, bottleneck, dec4, dec3) also come in a K-split form: a
+ * 32x32 block tile with K split over 2-8 blocks (write-through partial tiles, the last block of a tile sums
+ * them in split order), half the operand bytes per block.  It runs when a workspace is given (and
+ * LDM_UCONV_KS, a layer bit mask, selects the layer; default all five): ldm_step_workspace_floats(B, H, W)
+ * floats, zero-filled once (its counters return to zero after every launch); launches on one stream may
+ * share it.  ldm_step_conv / ldm_step_conv_dt run the single-block form. */
+int64_t ldm_step_workspace_floats(int32_t B, int32_t H, int32_t W);
+int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                     const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
+                     float* workspace, void* stream);
 /* ldm_step_conv with an operand precision LDM_DT_* (ldm_step_conv = LDM_DT_F32). */
 int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                      const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype, void* stream);

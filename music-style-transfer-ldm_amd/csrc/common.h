@@ -186,8 +186,10 @@ struct StepConv {
     float* x0_log;        // dec1: NCHW logs (or NULL)
     float* eps_log;
     int dtype;            // operand precision: LDM_DT_F32 / LDM_DT_F16 / LDM_DT_BF16 (uconv.hip)
+    float* ws;            // split-K workspace (step_ws_floats; zero-filled once) for the K-split layers
 };
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
+int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats = nullptr);
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
 // ustep.hip: the LDS-staged step kernels at the canonical latent (16 x 64, batch a multiple of 4)
 bool ustep_supported(int B, int H, int W);

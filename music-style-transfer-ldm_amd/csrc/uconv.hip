@@ -23,6 +23,8 @@
 // A[row = l & 15][k] and B[k][col = l & 15] for its lane group lg = l >> 4; within a 16-channel chunk,
 // MFMA step j uses k-local channel 4*lg + j.  D: row 4*lg + r, col l & 15.
 // Summation order differs from torch's (K blocked over waves, fixed order), well inside 1e-4.
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -50,7 +52,9 @@ struct UArgs {
     int32_t B, Hin, Win, Hout, Wout;
     int32_t Hq, Wq, Nq;   // column grid: output pixels (conv) or input pixels (transposed)
     int32_t nMt, nNt, order;
-    FastDiv fd_hw, fd_w, fd_mt, fd_nt;
+    FastDiv fd_hw, fd_w, fd_mt, fd_nt, fd_tiles;
+    float* slab;          // KS > 1: partial tiles [tile][KS][NFR][64] float4 (write-through)
+    int32_t* cnt;         // KS > 1: arrival counter per tile (zero between launches)
 };
 
 // (ky, kx) of tap t and the conv input offset / the transposed conv's output parity
@@ -92,7 +96,7 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT>
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS = 1>
 __global__ __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu((WN * WK + 3) / 4, (WN * WK + 3) / 4)))
 void uconv_kernel(UArgs a) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
@@ -100,7 +104,7 @@ void uconv_kernel(UArgs a) {
     constexpr int CPC = 9;                        // chunks per channel chunk (the 9 taps)
     static_assert(NCH % S == 0 && NCH % CPC == 0, "stage / chunk structure");
     static_assert(CIN % 16 == 0 && COUT % (16 * TM) == 0, "channel tiling");
-    static_assert((9 * CIN / 16) == NCH * WK, "the block's waves cover K exactly once");
+    static_assert((9 * CIN / 16) == NCH * WK * KS, "the grid's waves cover K exactly once");
     // a lone accumulator chain of 16x16x4 (40-cycle dependent latency, 32-cycle issue) alternates two
     constexpr int NACC2 = (NPH * TM * TN == 1) ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -111,10 +115,16 @@ void uconv_kernel(UArgs a) {
     const int wn = wave % WN, wk = wave / WN;
     const int col = lane & 15, lg = lane >> 4;
 
-    // block -> (M tile, N tile)
-    int mt, nt;
+    // block -> (K split ks, M tile, N tile).  The KS blocks of one tile are tiles apart, so with a tile count
+    // that is a multiple of 8 they share an XCD (round-robin placement): the last one reads the others'
+    // partials from its own L2.
+    int mt, nt, ks = 0;
     {
-        const int bid = blockIdx.x;
+        int bid = blockIdx.x;
+        if constexpr (KS > 1) {
+            ks = a.fd_tiles.div(bid);
+            bid -= ks * (a.nMt * a.nNt);
+        }
         const int q1 = a.fd_mt.div(bid), q2 = a.fd_nt.div(bid);
         mt = a.order == 0 ? bid - q1 * a.nMt : q2;
         nt = a.order == 0 ? q1 : bid - q2 * a.nNt;
@@ -159,8 +169,9 @@ void uconv_kernel(UArgs a) {
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, WBYTES, 0x00020000);
     const int va = (m0 + col) * 64 + lg * 16;                 // A: row m0+col, k-local 4*lg .. +3
-    const int sa0 = uni(wk * NCH * COUT * 64);                 // first chunk of this wave
-    const int sb0 = uni(wk * (NCH / CPC) * 64);                // its first channel chunk (16 ch x 4 B)
+    const int kw0 = ks * WK + wk;                              // this wave's slice of K
+    const int sa0 = uni(kw0 * NCH * COUT * 64);                // first chunk of this wave
+    const int sb0 = uni(kw0 * (NCH / CPC) * 64);               // its first channel chunk (16 ch x 4 B)
 
     floatx4 acc[NACC2][NPH][TM][TN];
 #pragma unroll
@@ -307,19 +318,64 @@ void uconv_kernel(UArgs a) {
         __syncthreads();
     }
     UCONV_STAMP(3);
+    floatx4 vv[NMY];
     static_for<0, NMY>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         const int f = frag(k);
-        floatx4 v;
         if constexpr (WK > 1) {
             const int fc = f < NFR ? f : NFR - 1;
-            v = red[((0 * WN + wn) * NFR + fc) * 64 + lane];
+            floatx4 v = red[((0 * WN + wn) * NFR + fc) * 64 + lane];
 #pragma unroll
             for (int k2 = 1; k2 < WK; ++k2) v = v + red[((k2 * WN + wn) * NFR + fc) * 64 + lane];
+            vv[k] = v;
         } else {
             constexpr int p = k / (TM * TN), mi = (k / TN) % TM, ni = k % TN;
-            v = acc[0][p][mi][ni];
+            vv[k] = acc[0][p][mi][ni];
         }
+    });
+    if constexpr (KS > 1) {
+        // ---- K split over blocks: write-through (sc1) partial tile, arrival counter, the last block of the
+        //      tile sums the KS partials in split order (deterministic) and runs the epilogue ---------------
+        static_assert(WN == 1, "one wave column per block under a K split");
+        const int tile = mt + nt * a.nMt;
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.slab), (short)0, 0x7fffffff, 0x00020000);
+        auto slab_off = [&](int kk, int f) { return (((tile * KS + kk) * NFR + f) * 64 + lane) * 16; };
+        static_for<0, NMY>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int f = frag(k);
+            if (f < NFR)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vv[k]),
+                                                       sr, slab_off(ks, f), 0, 16);
+        });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);
+        if (threadIdx.x == 0) {
+            const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == KS - 1;
+            if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        static_for<0, NMY>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int f = frag(k);
+            const int fc = f < NFR ? f : NFR - 1;
+            floatx4 part[KS];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                part[kk] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(sr, slab_off(kk, fc), 0, 16));
+            floatx4 sum = ks == 0 ? vv[k] : part[0];
+#pragma unroll
+            for (int kk = 1; kk < KS; ++kk) sum = sum + (kk == ks ? vv[k] : part[kk]);
+            vv[k] = sum;
+        });
+    }
+    static_for<0, NMY>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int f = frag(k);
+        const floatx4 v = vv[k];
         const Out ot = out_of(f);
         if (!ot.ok) return;
         const floatx4 bias = pre_b[k];
@@ -405,27 +461,45 @@ struct LayerGeo {
     int mode, cin, cout, tm, tn, wn, wk;
 };
 
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT>
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS>
 static int launch_dt(const UArgs& a, hipStream_t st) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
-    const int blocks = a.nMt * a.nNt;
-    const size_t lds = WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0;
-    auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT>;
+    const int blocks = a.nMt * a.nNt * KS;
+    const size_t lds = std::max<size_t>(WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0, KS > 1 ? 16 : 0);
+    auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * WN * WK), lds, st, a);
     LDM_CHECK_LAUNCH("uconv_kernel");
     return 0;
 }
 
 // operand precision (StepConv::dtype) -> instance
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI>
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int KS = 1>
 static int launch(const UArgs& a, int dtype, hipStream_t st) {
     switch (dtype) {
-        case LDM_DT_F32: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 0>(a, st);
-        case LDM_DT_F16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 1>(a, st);
-        case LDM_DT_BF16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 2>(a, st);
+        case LDM_DT_F32: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 0, KS>(a, st);
+        case LDM_DT_F16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 1, KS>(a, st);
+        case LDM_DT_BF16: return launch_dt<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, 2, KS>(a, st);
         default: return fail(2, "step conv: unknown operand precision");
     }
 }
+
+// The K-split form of the deep layers (variant 1): a 32 x 32 block tile (2 x 2 MFMA tiles per wave) instead of
+// 16 x 16, so a block pulls half the operand bytes per MFMA, with K split over KS blocks to keep 256 blocks
+// (write-through partial tiles, last arriver sums in split order).  {tm, tn, wk, ks}; ks 0 = no variant.
+struct KsGeo {
+    int tm, tn, wk, ks;
+};
+constexpr KsGeo kKs[9] = {
+    {0, 0, 0, 0},   // enc1
+    {0, 0, 0, 0},   // enc2
+    {2, 2, 4, 2},   // enc3        128 tiles x 2
+    {2, 2, 4, 4},   // enc4        64 tiles x 4
+    {2, 2, 8, 4},   // bottleneck  64 tiles x 4, 8 waves
+    {2, 2, 4, 8},   // dec4        32 tiles x 8
+    {2, 2, 4, 4},   // dec3        64 tiles x 4
+    {0, 0, 0, 0},   // dec2
+    {0, 0, 0, 0},   // dec1
+};
 
 constexpr LayerGeo kGeo[9] = {
     {0, 32, 64, 2, 1, 4, 1},     // enc1        conv3x3 s1
@@ -447,13 +521,54 @@ int64_t step_packed_floats(int layer) {
     return (int64_t)9 * uc::kGeo[layer].cin * uc::kGeo[layer].cout;
 }
 
+namespace uc {
+// Layers that run the K-split variant: bit l of LDM_UCONV_KS (read once; default kKsDefault).
+constexpr int kKsDefault = (1 << 2) | (1 << 3) | (1 << 4) | (1 << 5) | (1 << 6);
+static int ks_mask() {
+    static const int m = [] {
+        const char* e = std::getenv("LDM_UCONV_KS");
+        return e ? (int)std::strtol(e, nullptr, 0) : kKsDefault;
+    }();
+    return m;
+}
+static bool ks_on(int layer) { return kKs[layer].ks > 1 && ((ks_mask() >> layer) & 1); }
+// spatial size divisor of each layer's input (model.py:178-194)
+constexpr int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
+static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& slab_floats) {
+    const LayerGeo& g = kGeo[layer];
+    const KsGeo& k = kKs[layer];
+    const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
+    const int64_t nq = (int64_t)B * (g.mode == 1 ? (Hin / 2) * (Win / 2) : Hin * Win);
+    tiles = (int64_t)(g.cout / (16 * k.tm)) * ((nq + 16 * k.tn - 1) / (16 * k.tn));
+    slab_floats = tiles * k.ks * (g.mode == 2 ? 4 : 1) * k.tm * k.tn * 256;
+}
+}  // namespace uc
+
+// Split-K workspace of the step kernels at this shape: arrival counters (one int32 per tile, zero between
+// launches) sized for the layer with the most tiles, then the largest layer's partial slabs.
+int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
+    using namespace uc;
+    int64_t mt = 0, ms = 0;
+    for (int l = 0; l < 9; ++l) {
+        if (!ks_on(l)) continue;
+        int64_t t, sf;
+        ks_tiles(l, B, H, W, t, sf);
+        mt = std::max(mt, t);
+        ms = std::max(ms, sf);
+    }
+    if (!mt) return 0;
+    const int64_t c = (mt + 63) / 64 * 64;
+    if (cnt_floats) *cnt_floats = c;
+    return c + ms;
+}
+
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st) {
     using namespace uc;
     LDM_REQUIRE(layer >= 0 && layer <= 8, "step conv: layer index");
     LDM_REQUIRE(B > 0 && H % 8 == 0 && W % 8 == 0, "step conv: latent H, W must be multiples of 8");
-    const LayerGeo& g = kGeo[layer];
-    // spatial size of each layer's input (model.py:178-194)
-    static const int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
+    const bool ksv = ks_on(layer) && s.ws;   // without a split-K workspace the single-block form runs
+    LayerGeo g = kGeo[layer];
+    if (ksv) g.tm = kKs[layer].tm, g.tn = kKs[layer].tn, g.wn = 1, g.wk = kKs[layer].wk;
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     UArgs a{};
     a.x = s.x;
@@ -489,9 +604,34 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
     a.fd_w = FastDiv::make(a.Wq);
     a.fd_mt = FastDiv::make(a.nMt);
     a.fd_nt = FastDiv::make(a.nNt);
+    a.fd_tiles = FastDiv::make(a.nMt * a.nNt);
+    if (ksv) {
+        int64_t cnt = 0;
+        const int64_t wsf = step_ws_floats(B, H, W, &cnt);
+        int64_t tiles, sf;
+        ks_tiles(layer, B, H, W, tiles, sf);
+        LDM_REQUIRE(tiles == (int64_t)a.nMt * a.nNt && wsf >= cnt + sf && (cnt + sf) * 4 < 0x7fffffffLL,
+                    "step conv: split-K workspace geometry");
+        a.cnt = reinterpret_cast<int32_t*>(s.ws);
+        a.slab = s.ws + cnt;
+    }
     LDM_REQUIRE((int64_t)B * Hin * Win * g.cin * 4 < 0x7ff00000LL && (int64_t)B * a.Hout * a.Wout * g.cout * 4 < 0x7ff00000LL,
                 "step conv: tensor too large for 32-bit buffer offsets");
     LDM_REQUIRE(s.x && s.w && s.bias, "step conv: null operand");
+    if (ksv) {
+        switch (layer) {
+            case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 2, 1, 4, 9, 9, EPI_RELU, 2>(a, s.dtype, st);
+            case 3: LDM_REQUIRE(s.y, "enc4: y");
+                return launch<1, 256, 512, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_POSB, 4>(a, s.dtype, st);
+            case 4: LDM_REQUIRE(s.y, "bottleneck: y");
+                return launch<0, 512, 512, 2, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB, 4>(a, s.dtype, st);
+            case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
+                return launch<2, 512, 256, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, 8>(a, s.dtype, st);
+            case 6: LDM_REQUIRE(s.y && s.skip, "dec3: y, skip");
+                return launch<2, 256, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, 4>(a, s.dtype, st);
+            default: return fail(2, "step conv: no K-split variant for this layer");
+        }
+    }
     switch (layer) {
         case 0: LDM_REQUIRE(s.y, "enc1: y"); return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 1: LDM_REQUIRE(s.y && s.bcast, "enc2: y, t_emb");
@@ -547,6 +687,27 @@ extern "C" int ldm_step_pack_weight(int32_t layer, const float* w, float* packed
 extern "C" int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                              const float* bias, const float* bcast, const float* skip, float* y, void* stream) {
     return ldm_step_conv_dt(layer, B, H, W, x, packed, bias, bcast, skip, y, LDM_DT_F32, stream);
+}
+
+extern "C" int64_t ldm_step_workspace_floats(int32_t B, int32_t H, int32_t W) {
+    if (B <= 0 || H % 8 || W % 8) return -1;
+    return step_ws_floats(B, H, W, nullptr);
+}
+
+extern "C" int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
+                                const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
+                                float* workspace, void* stream) {
+    StepConv s{};
+    s.dtype = dtype;
+    s.x = x;
+    s.w = packed;
+    s.bias = bias;
+    s.bcast = bcast;
+    s.skip = skip;
+    s.y = y;
+    s.ws = workspace;
+    LDM_REQUIRE(layer != 8, "ldm_step_conv: dec1 runs fused with the DDIM update (ldm_ddim_sample)");
+    return step_conv(layer, B, H, W, s, (hipStream_t)stream);
 }
 
 extern "C" int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,

@@ -3,6 +3,7 @@
 // ~16 launches per denoising step, no host synchronisation, no allocation — the Python layer
 // captures the full loop into a single hipGraph.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -96,6 +97,7 @@ struct UNetWs {
     float *kf2, *bf2, *kf1, *bf1;   // folded keys of both cross-attentions (reverse loop, use_fold)
     float* xs;                      // the sampler state in NHWC (reverse loop with the step kernels)
     float* ustep;                   // split-K counters + slabs of the LDS-staged step kernels (zero-filled)
+    float* uks;                     // split-K counters + slabs of the K-split step kernels (uconv.hip)
     int64_t total;
 };
 
@@ -122,7 +124,13 @@ static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
 // Layers that run on ustep.hip under use_step 2: measured in the reverse loop (rocprofv3, B=8), the
 // LDS-staged form wins for enc1, dec4 and dec2 and loses where it has to split K across blocks or where the
 // register-direct form already streams well (profiles/r02/README.md).
-static bool ustep_layer(int l) { return l == 0 || l == 5 || l == 7; }
+static bool ustep_layer(int l) {
+    static const int m = [] {
+        const char* e = std::getenv("LDM_USTEP_LAYERS");   // bit l: layer l on ustep.hip (A/B timing)
+        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0) | (1 << 7);
+    }();
+    return (m >> l) & 1;
+}
 
 static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* w) {
     if (!use_ustep(s, w)) return 0;
@@ -170,6 +178,7 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.bf1 = take(B * 4 * L1);
     w.xs = take(B * (int64_t)s.C * HW);
     w.ustep = take(ustep_ws_floats(s, wts));
+    w.uks = take(wts && wts->use_step ? step_ws_floats(s.B, s.H, s.W) : 0);
     w.total = off;
     return w;
 }
@@ -303,6 +312,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
         c.bcast = bcast;
         c.skip = skip;
         c.dtype = w.step_dtype;
+        c.ws = ws.uks;
         return v3 && ustep_layer(layer) ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
     };
     LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
@@ -325,6 +335,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     c.x0_log = fuse.x0_log;
     c.eps_log = fuse.eps_log;
     c.dtype = w.step_dtype;
+    c.ws = ws.uks;
     return v3 && ustep_layer(8) ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
 }
 

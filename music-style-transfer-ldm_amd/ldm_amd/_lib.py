@@ -82,6 +82,9 @@ SIGNATURES = {
     "ldm_step_conv_dt": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
                                    c_vp]),
     "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
+    "ldm_step_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_step_conv_ws": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
+                                   c_fp, c_vp]),
     "ldm_mel_quantize": (c_int32, [c_fp, c_fp, c_int64, ctypes.c_float, c_vp]),
     "ldm_mel_dequantize": (c_int32, [c_fp, c_fp, c_int64, ctypes.c_float, c_vp]),
     "ldm_u8_to_unit": (c_int32, [c_fp, c_fp, c_int64, c_vp]),

@@ -34,11 +34,14 @@ def _case(variant, layer, shape):
 
 @pytest.mark.parametrize("variant,layer,shape",
                          [_case("uconv", l, s) for l in range(8) for s in [(8, 16, 64), (2, 16, 16), (3, 8, 24)]] +
-                         [_case("ustep", l, s) for l in range(8) for s in [(8, 16, 64), (4, 16, 64), (12, 16, 64)]])
+                         [_case("ustep", l, s) for l in range(8) for s in [(8, 16, 64), (4, 16, 64), (12, 16, 64)]] +
+                         [_case("ksplit", l, s) for l in (2, 3, 4, 5, 6) for s in [(8, 16, 64), (2, 16, 16), (3, 8, 24),
+                                                                                  (5, 16, 64)]])
 def test_step_layer_vs_float64(cuda, variant, layer, shape):
-    """uconv: ldm_step_conv (register-direct, any latent with H, W multiples of 8); ustep: ldm_ustep_conv
-    (LDS-staged, latent 16 x 64, B a multiple of 4), run twice on one workspace: bitwise-equal results
-    (the split-K sum is in slot order) and the counters left zero."""
+    """uconv: ldm_step_conv (register-direct, any latent with H, W multiples of 8); ksplit: ldm_step_conv_ws
+    (the same kernel with 32x32 tiles and K split over blocks); ustep: ldm_ustep_conv (LDS-staged, latent
+    16 x 64, B a multiple of 4).  The split forms run twice on one workspace: bitwise-equal results (the
+    split-K sum is in slot order) and the counters left zero."""
     from ldm_amd import _lib as L
     B, H, W = shape
     Cin, Cout, mode = LAYERS[layer]
@@ -67,6 +70,16 @@ def test_step_layer_vs_float64(cuda, variant, layer, shape):
     if variant == "uconv":
         L.call("ldm_step_conv", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp,
                y.data_ptr(), st)
+    elif variant == "ksplit":   # the K-split form (32x32 tiles, K over 2-8 blocks, last arriver sums)
+        nws = int(lib.ldm_step_workspace_floats(B, H, W))
+        assert nws > 0
+        ws = torch.zeros(nws, device=cuda)
+        for yy in (y, y2 := torch.full_like(y, float("nan"))):
+            L.call("ldm_step_conv_ws", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp,
+                   yy.data_ptr(), 0, ws.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+        assert int(ws[:64].view(torch.int32).abs().sum()) == 0
     else:
         nws = int(lib.ldm_ustep_workspace_floats(layer, B))
         assert nws >= 0
