@@ -321,6 +321,12 @@ int64_t ldm_step_workspace_floats(int32_t B, int32_t H, int32_t W);
 int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                      const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
                      float* workspace, void* stream);
+/* dec1 with the fused DDIM update, as the reverse loop runs it: d2 [B,H,W,64] NHWC, xs [B,H,W,32] NHWC sampler
+ * state updated in place, coef [4] {sqrt(ab_t), sqrt(1-ab_t), sqrt(ab_next), sqrt(1-ab_next)}, x0_log /
+ * eps_log NCHW [B,32,H,W] or NULL (model.py:442-463). */
+int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const float* packed, const float* bias,
+                       const float* coef, float eta, float* xs, float* x0_log, float* eps_log, int32_t dtype,
+                       void* stream);
 /* ldm_step_conv with an operand precision LDM_DT_* (ldm_step_conv = LDM_DT_F32). */
 int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                      const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype, void* stream);

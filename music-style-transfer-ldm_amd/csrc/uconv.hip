@@ -710,6 +710,23 @@ extern "C" int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, 
     return step_conv(layer, B, H, W, s, (hipStream_t)stream);
 }
 
+extern "C" int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const float* packed, const float* bias,
+                                  const float* coef, float eta, float* xs, float* x0_log, float* eps_log, int32_t dtype,
+                                  void* stream) {
+    LDM_REQUIRE(d2 && packed && bias && coef && xs, "ldm_step_dec1_ddim: null argument");
+    StepConv s{};
+    s.dtype = dtype;
+    s.x = d2;
+    s.w = packed;
+    s.bias = bias;
+    s.coef = coef;
+    s.eta = eta;
+    s.xs = xs;
+    s.x0_log = x0_log;
+    s.eps_log = eps_log;
+    return step_conv(8, B, H, W, s, (hipStream_t)stream);
+}
+
 extern "C" int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                                 const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
                                 void* stream) {

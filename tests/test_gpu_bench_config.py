@@ -8,9 +8,13 @@ pinned to the reference's own outputs by tests/test_oracle_golden.py) run on the
 
   * timestep list bit-exact (model.py:420);
   * final x, the first pred_x0 log and the last noise_pred log within 1e-4 relative (north_star);
-  * every conv/projection layer of the step, launched alone with the exact plan and layouts the bench
-    uses, against float64 F.conv2d / conv_transpose2d (1e-5 relative): this covers every kernel
-    instance that appears in the bench's rocprof summary.
+  * every step kernel the bench's loop launches (test_bench_config_step_kernels): each of the nine convs on
+    the instance the loop picks for it (ustep.hip for enc1 / dec2, the K-split uconv.hip form for enc3, enc4,
+    the bottleneck, dec4, dec3, uconv.hip for enc2; dec1 with its fused DDIM update and both logs), with the
+    engine's packed step weights, the folded out-projections and position biases, on NHWC operands at
+    B = 8, 16 x 64, against float64 torch (1e-5 relative);
+  * the general-kernel (conv.hip) plans of the same layers, which ldm_unet_forward (single UNet calls) runs
+    (test_bench_config_every_layer_instance).
 
 Reference: /root/reference/models/model.py:409-465 (the loop), :163-231 (the UNet).
 """
@@ -87,9 +91,83 @@ def _from_layout(y, shape, nhwc):
     return y.view(B, H, W, C).permute(0, 3, 1, 2) if nhwc else y.view(B, C, H, W)
 
 
+def test_bench_config_step_kernels(bench_objects, cuda):
+    """The loop's nine step-kernel launches at the bench geometry, each on the instance the loop uses."""
+    import os
+    from ldm_amd import _lib as L
+    eng, ldm = bench_objects["eng"], bench_objects["ldm"]
+    B, H, W = 8, 16, 64
+    shape = eng.shape(B, 32, H, W)
+    w = eng.weights(shape)
+    assert int(w.use_step) == 2 and int(w.step_dtype) == 0
+    u = ldm.unet
+    lib = L.load()
+    st = torch.cuda.current_stream().cuda_stream
+    ustep_layers = int(os.environ.get("LDM_USTEP_LAYERS", "0x81"), 0)
+    LAYERS = [(32, 64, 0, 1), (64, 128, 1, 1), (128, 256, 1, 2), (256, 512, 1, 4), (512, 512, 0, 8),
+              (512, 256, 2, 8), (256, 128, 2, 4), (128, 64, 2, 2)]
+    convs = [u.enc1, u.enc2, u.enc3, u.enc4, u.bottleneck, u.dec4, u.dec3, u.dec2, u.dec1]
+    g = torch.Generator().manual_seed(78)
+    sws = torch.zeros(max(1, int(lib.ldm_step_workspace_floats(B, H, W))), device=cuda)
+    for layer, (cin, cout, mode, div) in enumerate(LAYERS):
+        hin, win = H // div, W // div
+        hout, wout = (hin, win) if mode == 0 else ((hin // 2, win // 2) if mode == 1 else (2 * hin, 2 * win))
+        x = torch.randn(B, cin, hin, win, generator=g)
+        xd = x.permute(0, 2, 3, 1).contiguous().to(cuda)
+        y = torch.full((B, hout, wout, cout), float("nan"), device=cuda)
+        bc = torch.randn(B, cout, generator=g) if layer == 1 else None
+        sk = torch.randn(B, cout, hout, wout, generator=g) if mode == 2 else None
+        bcd = None if bc is None else bc.to(cuda)
+        skd = None if sk is None else sk.permute(0, 2, 3, 1).contiguous().to(cuda)
+        bias = w.step_pb[layer - 3] if layer in (3, 4) else w.conv_b[layer]
+        args = (xd.data_ptr(), w.step_w[layer], bias, None if bcd is None else bcd.data_ptr(),
+                None if skd is None else skd.data_ptr(), y.data_ptr())
+        if (ustep_layers >> layer) & 1:
+            nws = int(lib.ldm_ustep_workspace_floats(layer, B))
+            uws = torch.zeros(max(1, nws), device=cuda)
+            L.call("ldm_ustep_conv", layer, B, *args, uws.data_ptr() if nws else None, st)
+        else:
+            L.call("ldm_step_conv_ws", layer, B, H, W, *args, 0, sws.data_ptr(), st)
+        torch.cuda.synchronize()
+        conv = convs[layer]
+        x64 = x.double()
+        if layer in (3, 4):   # the folded out-projection: conv(out_proj(a)) with out_proj's bias inside
+            a = (u.cross_attention2, u.cross_attention1)[layer - 3].multihead_attn
+            x64 = torch.einsum("oc,bchw->bohw", a.out_proj.weight.detach().double().cpu(), x64) + \
+                a.out_proj.bias.detach().double().cpu()[None, :, None, None]
+        w64, b64 = conv.weight.detach().double().cpu(), conv.bias.detach().double().cpu()
+        if mode == 2:
+            ref = F.conv_transpose2d(x64, w64, b64, stride=2, padding=1, output_padding=1)
+        else:
+            ref = F.conv2d(x64, w64, b64, stride=1 if mode == 0 else 2, padding=1)
+        ref = ref.clamp_min(0)
+        if bc is not None:
+            ref = ref + bc.double()[:, :, None, None]
+        if sk is not None:
+            ref = ref + sk.double()
+        assert rel_err(npy(y.permute(0, 3, 1, 2)), ref.numpy()) < 1e-5, layer
+    # dec1 + the fused DDIM update (model.py:442-463) with both logs
+    d2 = torch.randn(B, 64, H, W, generator=g)
+    xs = torch.randn(B, 32, H, W, generator=g)
+    coef = torch.tensor([0.6, 0.8, 0.7, 0.71414284], dtype=torch.float32)
+    xsd = xs.permute(0, 2, 3, 1).contiguous().to(cuda)
+    x0l = torch.full((B, 32, H, W), float("nan"), device=cuda)
+    epl = torch.full_like(x0l, float("nan"))
+    L.call("ldm_step_dec1_ddim", B, H, W, d2.permute(0, 2, 3, 1).contiguous().to(cuda).data_ptr(), w.step_w[8],
+           w.conv_b[8], coef.to(cuda).data_ptr(), 0.3, xsd.data_ptr(), x0l.data_ptr(), epl.data_ptr(), 0, st)
+    torch.cuda.synchronize()
+    eps = F.conv2d(d2.double(), u.dec1.weight.detach().double().cpu(), u.dec1.bias.detach().double().cpu(), padding=1)
+    c = coef.double()
+    x0 = (xs.double() - c[1] * eps) / c[0]
+    xn = c[2] * x0 + c[3] * eps + 0.3 * (c[3] * eps - c[1] * eps)
+    assert rel_err(npy(epl), eps.numpy()) < 1e-5
+    assert rel_err(npy(x0l), x0.numpy()) < 1e-5
+    assert rel_err(npy(xsd.permute(0, 3, 1, 2)), xn.numpy()) < 1e-5
+
+
 def test_bench_config_every_layer_instance(bench_objects, cuda):
-    """Each of the step's conv / projection launches, with the bench's plan, layouts and (for enc4 and
-    the bottleneck) folded weights + position-dependent bias, against float64 torch on the CPU."""
+    """Each conv / projection of a single UNet call (ldm_unet_forward: conv.hip's general kernel) with the
+    engine's B=8 plans and layouts, and (for enc4 and the bottleneck) the folded weights, against float64."""
     from ldm_amd import _lib as L
     eng, ldm = bench_objects["eng"], bench_objects["ldm"]
     B = 8
