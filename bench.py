@@ -105,10 +105,10 @@ def _graph_time_us(fn, reps):
 STEP_LAYERS = [  # (name, Cin, Cout, mode 0 conv s1 / 1 conv s2 / 2 convT s2, input scale divisor)
     ("enc1", 32, 64, 0, 1), ("enc2", 64, 128, 1, 1), ("enc3", 128, 256, 1, 2), ("enc4", 256, 512, 1, 4),
     ("bottleneck", 512, 512, 0, 8), ("dec4", 512, 256, 2, 8), ("dec3", 256, 128, 2, 4), ("dec2", 128, 64, 2, 2)]
-USTEP_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_USTEP_LAYERS", "0x81"), 0) >> l) & 1)
-# ^ csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip (enc1, dec2)
-KS_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_UCONV_KS", "0x7c"), 0) >> l) & 1)
-# ^ csrc/uconv.hip ks_on(): the layers that run the K-split step kernel (enc3, enc4, bottleneck, dec4, dec3)
+USTEP_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_USTEP_LAYERS", "0xa1"), 0) >> l) & 1)
+# ^ csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip (enc1, dec4, dec2)
+KS_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_UCONV_KS", "0x18"), 0) >> l) & 1)
+# ^ csrc/uconv.hip ks_on(): the layers that run the K-split step kernel (enc4, bottleneck)
 
 
 def time_step_layers(engine, B, H, W, dev, reps=50):

@@ -523,7 +523,9 @@ int64_t step_packed_floats(int layer) {
 
 namespace uc {
 // Layers that run the K-split variant: bit l of LDM_UCONV_KS (read once; default kKsDefault).
-constexpr int kKsDefault = (1 << 2) | (1 << 3) | (1 << 4) | (1 << 5) | (1 << 6);
+// Measured in the loop's chain timing (bench.py kernels, B = 8): the split form gains 0.4 us on the bottleneck
+// and 0.2 us on enc4, and loses 0.9-1.5 us on enc3, dec4 and dec3 (their single-block forms stay).
+constexpr int kKsDefault = (1 << 3) | (1 << 4);
 static int ks_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS");

@@ -127,7 +127,7 @@ static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
 static bool ustep_layer(int l) {
     static const int m = [] {
         const char* e = std::getenv("LDM_USTEP_LAYERS");   // bit l: layer l on ustep.hip (A/B timing)
-        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0) | (1 << 7);
+        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0) | (1 << 5) | (1 << 7);
     }();
     return (m >> l) & 1;
 }

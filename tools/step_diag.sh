@@ -12,7 +12,7 @@ for k in "$@"; do
 done
 wait
 others=""
-for s in capi.cpp conv.hip misc.hip unet.hip backward.hip reduce.hip uconv.hip ustep.hip; do
+for s in $(sed -n 's/^SRCS := //p' Makefile); do
   [ "$s" = "$f.hip" ] || others="$others ../build/$s.o"
 done
 for k in "$@"; do
