@@ -386,6 +386,17 @@ int ldm_attention_backward_flash(const float* q, const float* kv, const float* o
                                  const float* dout, float* dq, float* dkv, float* delta_ws, int32_t B, int32_t E,
                                  int32_t heads, int32_t L, int32_t S, float scale, void* stream);
 
+/* ---- multi-tensor weight re-pack (the train step refreshes every packed trainable conv weight after the
+ * optimizer step in one launch instead of one per weight; pack.hip).  ldm_pack_many_prepare fills
+ * n * ldm_pack_job_bytes() bytes of host_jobs with the jobs for (descs[i], plans[i]) reading the torch-layout
+ * weight w[i] into out[i] (the buffer ldm_conv_pack_weight would fill, kinds 1-3) and returns the launch
+ * size; copy the table to device memory once, then ldm_pack_many(table, n, launch_size, stream) re-packs
+ * them all (same values as ldm_conv_pack_weight). */
+int64_t ldm_pack_job_bytes(void);
+int ldm_pack_many_prepare(const ldm_conv_desc* descs, const ldm_conv_plan* plans, const float* const* w,
+                          void* const* out, int32_t n, void* host_jobs, int64_t* launch_size);
+int ldm_pack_many(const void* device_jobs, int32_t n, int64_t launch_size, void* stream);
+
 /* ---- LPIPS-AlexNet perceptual distance (loss.py:6-21: lpips==0.1.4 LPIPS(net='alex') on 2x-1)
  * The AlexNet convs run on ldm_conv_forward: 3x3 directly, 11x11/s4 and 5x5 as ldm_im2col + a 1x1 conv (their
  * data gradient: the 1x1 dual conv + ldm_col2im).  col [B,Kpad,Ho,Wo], k = (c*kh+ky)*kw+kx, rows >= Cv*kh*kw

@@ -120,6 +120,22 @@ struct PhaseTable {
 
 int build_phase_table(const ldm_conv_desc& d, PhaseTable& pt);
 
+// One weight re-pack of a multi-tensor pack launch (pack.hip): the packed layout of a conv.hip MFMA plan
+// (kind 1 / 2: fp32, CK = 8 / 16 channels per fragment) or of a tconv.hip plan (kind 3: 16-bit, 32-channel
+// chunks), read from the torch-layout weight w.
+struct PackJob {   // one weight of a multi-tensor re-pack (pack.hip); filled by conv_pack_job / tconv_pack_job
+    const float* w;
+    void* out;
+    int64_t first_block, total;   // this job's first block of the launch; its element count (< 2^31)
+    int32_t kind, dt, Cin, Cout, KK, transposed, Mpad, nphase;
+    int32_t ntap[kMaxPhase];
+    int64_t wofs[kMaxPhase];
+    int32_t kk[kMaxPhase][kMaxTap];
+    FastDiv fd_mpad, fd_cin, fd_ntap[kMaxPhase];
+};
+int conv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j);    // kinds 1, 2 (conv.hip)
+int tconv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j);   // kind 3 (tconv.hip)
+
 // tconv.hip: the LDS-staged 16-bit-operand implicit GEMM (plan kind 3) for large-plane NCHW layers
 struct EpiArgs;
 bool tconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan);

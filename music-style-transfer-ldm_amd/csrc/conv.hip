@@ -1389,6 +1389,30 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     return 0;
 }
 
+namespace ldm {
+int conv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j) {
+    LDM_REQUIRE(p.kind == 1 || p.kind == 2, "pack job: not an MFMA plan");
+    ConvArgs a;
+    int rc = make_args(d, p, a);
+    if (rc) return rc;
+    j.kind = p.kind;
+    j.dt = 0;
+    j.Cin = a.Cin;
+    j.Cout = a.Cout;
+    j.KK = a.KK;
+    j.transposed = a.transposed;
+    j.Mpad = a.Mpad;
+    j.nphase = a.pt.nphase;
+    for (int q = 0; q < kMaxPhase; ++q) {
+        j.ntap[q] = a.pt.ntap[q];
+        j.wofs[q] = a.pt.wofs[q];
+        for (int t = 0; t < kMaxTap; ++t) j.kk[q][t] = a.pt.kk[q][t];
+    }
+    j.total = p.packed_floats;
+    return 0;
+}
+}  // namespace ldm
+
 template <int KIND, int NT, bool NHWC, int DT>
 static int launch_mfma_nt(const ConvArgs& a, const ldm_conv_plan& p, int64_t Nq, hipStream_t st) {
     const int TILE = Mfma<KIND>::TILE;

@@ -317,6 +317,30 @@ bool tconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan) {
     return true;
 }
 
+int tconv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j) {
+    LDM_REQUIRE(p.kind == 3 && (p.tn == LDM_DT_F16 || p.tn == LDM_DT_BF16), "pack job: not a kind-3 plan");
+    PhaseTable pt;
+    int Mpad;
+    int64_t halfs;
+    int rc = tc::layout(d, 64 * p.tm, pt, Mpad, halfs);
+    if (rc) return rc;
+    j.kind = 3;
+    j.dt = p.tn;
+    j.Cin = d.Cin;
+    j.Cout = d.Cout;
+    j.KK = d.kh * d.kw;
+    j.transposed = d.transposed;
+    j.Mpad = Mpad;
+    j.nphase = pt.nphase;
+    for (int q = 0; q < kMaxPhase; ++q) {
+        j.ntap[q] = pt.ntap[q];
+        j.wofs[q] = pt.wofs[q];
+        for (int t = 0; t < kMaxTap; ++t) j.kk[q][t] = pt.kk[q][t];
+    }
+    j.total = halfs;
+    return 0;
+}
+
 int tconv_pack(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* w, float* packed, hipStream_t st) {
     PhaseTable pt;
     int Mpad;

@@ -115,6 +115,10 @@ SIGNATURES = {
                                             c_float, c_vp]),
     "ldm_attention_backward_flash": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32,
                                                c_int32, c_int32, c_int32, c_float, c_vp]),
+    "ldm_pack_job_bytes": (c_int64, []),
+    "ldm_pack_many_prepare": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan), ctypes.POINTER(c_vp),
+                                        ctypes.POINTER(c_vp), c_int32, c_vp, ctypes.POINTER(c_int64)]),
+    "ldm_pack_many": (c_int32, [c_vp, c_int32, c_int64, c_vp]),
     "ldm_im2col": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                              c_fp, c_fp, c_int32, c_int32, c_fp, c_vp]),
     "ldm_col2im": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

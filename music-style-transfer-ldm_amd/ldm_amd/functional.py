@@ -126,7 +126,8 @@ def linear(x, weight, bias, act="none"):
     for s in lead:
         n *= s
     x4 = x.reshape(n, x.shape[-1], 1, 1)
-    y = conv(x4, weight.view(weight.shape[0], weight.shape[1], 1, 1), bias, stride=1, padding=0, act=act)
+    y = conv(x4, weight.view(weight.shape[0], weight.shape[1], 1, 1), bias, stride=1, padding=0, act=act,
+             wkey=(weight, "lin"))     # pack cached against the parameter, not against this step's view
     return y.reshape(*lead, weight.shape[0])
 
 

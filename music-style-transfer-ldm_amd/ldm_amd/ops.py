@@ -142,6 +142,7 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
         per = {}
         _PACK_CACHE[owner] = per
     buf = per.get(key)
+    w = None
     if buf is None:
         # drop stale versions of this weight
         for k in [k for k in per if k[0] != owner._version]:
@@ -150,7 +151,102 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
         buf = torch.empty(int(plan.packed_floats), device=weight.device, dtype=torch.float32)
         L.call("ldm_conv_pack_weight", byref(desc), byref(plan), w.data_ptr(), buf.data_ptr(), stream_handle())
         per[key] = buf
+    if _RECORD is not None and owner.requires_grad and owner.grad_fn is None:
+        _RECORD.add(owner, key[1:], weight.detach() if w is None else w, desc, plan, buf)
     return buf
+
+
+_RECORD = None
+
+
+class _PackRecord:
+    """The packs of trainable weights one step reads (filled by packed_weight while record_packs is open)."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def add(self, owner, tail, w, desc, plan, buf):
+        # only a pack that reads the owner's own storage can be refreshed from it later (not a cast copy)
+        if plan.kind not in (1, 2, 3) or w.dtype != torch.float32 or not w.is_contiguous() or \
+                w.untyped_storage().data_ptr() != owner.untyped_storage().data_ptr():
+            return
+        # no reference to w itself: a slice of a parameter (in_proj rows) keeps its autograd node alive, and
+        # an AccumulateGrad node from an eager step breaks a later graph capture of the step
+        self.entries.setdefault((id(owner), tail), (owner, tail, w.data_ptr() - owner.data_ptr(),
+                                                    L.ConvDesc.from_buffer_copy(desc),
+                                                    L.ConvPlan.from_buffer_copy(plan), buf))
+
+
+class record_packs:
+    """with record_packs() as rec: ... -- rec.entries then lists every trainable-weight pack read inside."""
+
+    def __enter__(self):
+        global _RECORD
+        self._prev, _RECORD = _RECORD, _PackRecord()
+        return _RECORD
+
+    def __exit__(self, *exc):
+        global _RECORD
+        _RECORD = self._prev
+        return False
+
+
+class PackSet:
+    """Every packed trainable conv weight of a train step re-packed by ONE launch (pack.hip ldm_pack_many)
+    after the optimizer step, instead of one ldm_conv_pack_weight launch per weight at its first use in the
+    next step's forward / backward (51 launches per step at B = 32).  The buffers are packed_weight's own
+    cache entries; after a re-pack they are re-keyed to their owners' current _version, so the next step's
+    packed_weight calls hit them.  Built from a record_packs() pass over one step."""
+
+    def __init__(self, record, device):
+        ents = list(record.entries.values())
+        self.owners = [e[0] for e in ents]
+        self.tails = [e[1] for e in ents]
+        self.bufs = [e[5] for e in ents]
+        self.ptrs = tuple(o.data_ptr() for o in self.owners)
+        self.wptrs = [o.data_ptr() + e[2] for o, e in zip(self.owners, ents)]   # the packed weights (or slices)
+        self.descs = [e[3] for e in ents]
+        self.plans = [e[4] for e in ents]
+        self.n = n = len(ents)
+        descs = (L.ConvDesc * n)(*self.descs)
+        plans = (L.ConvPlan * n)(*self.plans)
+        wptr = (ctypes.c_void_p * n)(*self.wptrs)
+        optr = (ctypes.c_void_p * n)(*[e[5].data_ptr() for e in ents])
+        host = ctypes.create_string_buffer(int(L.load().ldm_pack_job_bytes()) * n)
+        launch = ctypes.c_int64()
+        L.call("ldm_pack_many_prepare", descs, plans, wptr, optr, n, ctypes.addressof(host), byref(launch))
+        self.launch = int(launch.value)
+        self.table = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(device)
+        self.versions = None
+
+    def valid(self):
+        """False once a weight moved to other storage (the job table holds raw pointers)."""
+        return all(o.data_ptr() == p for o, p in zip(self.owners, self.ptrs))
+
+    def current(self):
+        return self.versions == tuple(o._version for o in self.owners)
+
+    def repack(self):
+        """Launch the re-pack on the current stream, then re-key the buffers.  Inside a graph capture only the
+        launch is recorded: the buffers hold the new packs once the replay ran (the caller re-keys then)."""
+        if not self.valid():
+            raise RuntimeError("PackSet: a recorded weight moved to new storage; build a new PackSet")
+        L.call("ldm_pack_many", self.table.data_ptr(), self.n, self.launch, stream_handle())
+        if not torch.cuda.is_current_stream_capturing():
+            self.rekey()
+
+    def rekey(self):
+        """Declare the buffers packs of the owners' current versions (the caller knows they are)."""
+        for owner, tail, buf in zip(self.owners, self.tails, self.bufs):
+            v = owner._version
+            per = _PACK_CACHE.get(owner)
+            if per is None:
+                per = {}
+                _PACK_CACHE[owner] = per
+            for k in [k for k in per if k[0] != v]:
+                del per[k]
+            per[(v,) + tail] = buf
+        self.versions = tuple(o._version for o in self.owners)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -36,6 +36,7 @@ except ImportError:   # reference-style flat imports (models/ on sys.path)
     from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
 
 from ldm_amd import dist as hdist
+from ldm_amd import ops
 from ldm_amd import optim as hoptim
 
 
@@ -159,6 +160,12 @@ class LDMTrainer:
         # all-reduces too; over gloo (host-staged collectives) the step stays eager.
         self.graph_step = False
         self.graph_warmup = 2
+        # batched_repack: the packed (MFMA fragment-order) copies of the trainable conv weights are refreshed
+        # by one launch right after the optimizer step (ops.PackSet, recorded on the first eager step) instead
+        # of one launch per weight at its first use in the next step; LDM_AMD_BATCHED_REPACK=0 turns it off
+        self.batched_repack = os.environ.get("LDM_AMD_BATCHED_REPACK", "1") != "0"
+        self._packset = None
+        self._packset_tried = False
         self._graph = None
         self._graph_calls = 0
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", factor=0.5,
@@ -189,6 +196,18 @@ class LDMTrainer:
         if t is None:
             t = self._sample_t(batch_size)
         ac = {} if self.autocast_dtype is None else {"dtype": self.autocast_dtype}
+        record = rec = None
+        if self.batched_repack and not self._packset_tried and self.device.type == "cuda" and \
+                not torch.cuda.is_current_stream_capturing():
+            record = ops.record_packs()
+            rec = record.__enter__()
+        try:
+            return self._step_body(content_spec, style_spec, t, noise, ac, rec)
+        finally:
+            if record is not None:
+                record.__exit__(None, None, None)
+
+    def _step_body(self, content_spec, style_spec, t, noise, ac, rec):
         with torch.autocast(device_type=self.device.type, enabled=self.autocast_enabled, **ac):
             outputs = self.model(content_spec, style_spec, t, noise=noise)
             noise_pred = outputs["noise_pred"]
@@ -207,6 +226,11 @@ class LDMTrainer:
             self.reducer.finish()
         self.scaler.step(self.optimizer)
         self.scaler.update()
+        if rec is not None:
+            self._packset_tried = True
+            self._packset = ops.PackSet(rec, self.device) if rec.entries else None
+        if self._packset is not None:
+            self._packset.repack()
         return compression_loss_, denoisinsg_loss, style_loss_, total_loss
 
     @staticmethod
@@ -245,6 +269,10 @@ class LDMTrainer:
             # is recorded into the graph (a cache hit would bake a pack made outside it into every replay)
             for p in self._trainable:
                 torch.autograd.graph.increment_version(p)
+            if self._packset is not None:
+                # ...except the batched re-pack's buffers: packed here, outside the graph, for the captured
+                # forward to read; the graph re-packs them at its end (after the optimizer) for the next replay
+                self._packset.repack()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -254,12 +282,16 @@ class LDMTrainer:
         for dst, src in zip(self._graph_in, args):
             if dst is not None:
                 dst.copy_(src)
+        if self._packset is not None and not self._packset.current():
+            self._packset.repack()     # the weights changed outside the graph since its last re-pack
         self._graph.replay()
         # the replay rewrote the parameters on the device, but their autograd versions moved only once, at
         # capture: move them again so that version-keyed caches (packed conv weights, the UNet engine's bound
         # weights) never serve pre-replay values to a later eager forward or to a re-capture
         for p in self._trainable:
             torch.autograd.graph.increment_version(p)
+        if self._packset is not None:
+            self._packset.rekey()      # the replay ended by re-packing them from the updated weights
         return self._losses(self._graph_out)
 
     def train_epoch(self, epoch):
