@@ -146,7 +146,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         us = _graph_time_us(run, reps)
         taps = 9 if mode < 2 else 2.25
         fl = 2.0 * B * cout * hout * wout * cin * taps
-        by = 4.0 * (cin * cout * 9 + B * cin * hin * win + B * cout * hout * wout)
+        by = (2.0 if dt else 4.0) * cin * cout * 9 + 4.0 * (B * cin * hin * win + B * cout * hout * wout)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
                      "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else
                                                           ("uconv_kernel (K split)" if layer in KS_LAYERS else "uconv_kernel"))

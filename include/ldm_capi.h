@@ -309,6 +309,10 @@ int ldm_u8_to_unit(const uint8_t* in, float* out, int64_t n, void* stream);
  * dec1 only runs fused with the DDIM update inside ldm_ddim_sample. */
 int64_t ldm_step_packed_floats(int32_t layer);
 int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream);
+/* The pack for an operand precision: LDM_DT_F32 as ldm_step_pack_weight; LDM_DT_F16 / LDM_DT_BF16 write the
+ * same layout in 16-bit elements (ldm_step_packed_floats / 2 floats of storage), which is what every step
+ * conv with that dtype reads (ldm_step_conv_dt, _ws, ldm_step_dec1_ddim, ldm_unet_weights.step_w). */
+int ldm_step_pack_weight_dt(int32_t layer, int32_t dtype, const float* w, float* packed, void* stream);
 int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                   const float* bias, const float* bcast, const float* skip, float* y, void* stream);
 /* The step kernels of the deep layers (enc3, enc4, bottleneck, dec4, dec3) also come in a K-split form: a

@@ -65,6 +65,18 @@ __device__ __forceinline__ floatx4 mma16_lowp(floatx4 a, floatx4 b, floatx4 c) {
     }
 }
 
+// the same with A already rounded to 16 bits (a packed weight fragment, 4 x f16 / bf16 bit patterns)
+template <int DT>
+__device__ __forceinline__ floatx4 mma16_lowp(shortx4 a16, floatx4 b, floatx4 c) {
+    if constexpr (DT == 1) {
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(halfx4, a16), __builtin_convertvector(b, halfx4),
+                                                     c, 0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a16, __builtin_bit_cast(shortx4, __builtin_convertvector(b, bf16x4)),
+                                                         c, 0, 0, 0);
+    }
+}
+
 // Division of a non-negative int < 2^31 by a runtime constant with one mul_hi + shift (Granlund-
 // Montgomery, round-up multiplier): the GPU's integer division is a ~30-instruction VALU sequence.
 // Pin a wave-uniform value to an SGPR (a buffer soffset / resource the compiler leaves in a VGPR is

@@ -21,6 +21,7 @@
 //
 // MFMA operand maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j]
 // and B[k = 8h + j][col r], j = 0..7; D: col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4h.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -50,6 +51,7 @@ struct TArgs {
     float* y;
     int32_t B, Cin, Hin, Win, Cout, Hout, Wout;
     int32_t Mpad, nM, nN, cpt;   // cpt = Cin / KC chunks per tap
+    int32_t xcd_chunk;           // > 0: tiles per XCD of the XCD-contiguous block order (blocks % 8 == 0)
     int64_t N;                   // positions per phase (B * Hq * Wq)
     FastDiv fd_hw, fd_w;
     PhaseTable pt;               // wofs in 16-bit elements
@@ -83,12 +85,16 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     const int wm = wave >> 1, wn = wave & 1;
     const int r = lane & 31, h = lane >> 5;
 
-    // block -> (phase, N tile, M tile), M fastest: the blocks of one N tile gather the same input window
-    const int bid = blockIdx.x;
-    const int mt = bid % a.nM;
-    const int rest = bid / a.nM;
-    const int nt = rest % a.nN;
-    const int ph = rest / a.nN;
+    // block -> (N tile, phase, M tile), M fastest, then the phases: the blocks of one N tile gather the same
+    // input window.  Blocks go round-robin to the 8 XCDs (block b to XCD b % 8), so with xcd_chunk each XCD
+    // walks its own contiguous run of tiles: the windows of neighbouring N tiles and all phases of one N
+    // tile meet in that XCD's L2 instead of being fetched by every XCD from the Infinity Cache.
+    int t = blockIdx.x;
+    if (a.xcd_chunk > 0) t = (t & 7) * a.xcd_chunk + (t >> 3);
+    const int mt = t % a.nM;
+    const int rest = t / a.nM;
+    const int ph = rest % a.pt.nphase;
+    const int nt = rest / a.pt.nphase;
     const int ntap = a.pt.ntap[ph];
     const int nch = ntap * a.cpt;
     const int64_t n0 = (int64_t)nt * BN;
@@ -385,6 +391,11 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     a.fd_w = FastDiv::make(a.pt.Wq);
     a.ep = ep;
     const int64_t blocks = (int64_t)a.pt.nphase * a.nM * a.nN;
+    static const int order = [] {   // LDM_TCONV_XCD=0: plain order (A/B timing)
+        const char* e = std::getenv("LDM_TCONV_XCD");
+        return e ? std::atoi(e) : 1;
+    }();
+    a.xcd_chunk = (order && blocks % 8 == 0) ? (int)(blocks / 8) : 0;
     LDM_REQUIRE(blocks < (1LL << 31), "tconv: grid too large");
     hipStream_t s = st;
     if (p.tm == 2) {

@@ -165,12 +165,16 @@ void uconv_kernel(UArgs a) {
 
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.x), (short)0, uni(a.B * a.Hin * a.Win * CIN * 4), 0x00020000);
-    constexpr int WBYTES = 9 * CIN * COUT * 4;
+    // 16-bit operands read 16-bit packed weights (ldm_step_pack_weight_dt): half the A bytes of the fp32 pack,
+    // which matters because a block's operand stream through its CU's L1 is what bounds these launches
+    constexpr int AE = DT != 0 ? 2 : 4;                        // bytes per packed weight element
+    using AT = std::conditional_t<DT != 0, shortx4, floatx4>;
+    constexpr int WBYTES = 9 * CIN * COUT * AE;
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, WBYTES, 0x00020000);
-    const int va = (m0 + col) * 64 + lg * 16;                 // A: row m0+col, k-local 4*lg .. +3
+    const int va = ((m0 + col) * 16 + lg * 4) * AE;            // A: row m0+col, k-local 4*lg .. +3
     const int kw0 = ks * WK + wk;                              // this wave's slice of K
-    const int sa0 = uni(kw0 * NCH * COUT * 64);                // first chunk of this wave
+    const int sa0 = uni(kw0 * NCH * COUT * 16 * AE);           // first chunk of this wave
     const int sb0 = uni(kw0 * (NCH / CPC) * 64);               // its first channel chunk (16 ch x 4 B)
 
     floatx4 acc[NACC2][NPH][TM][TN];
@@ -183,7 +187,8 @@ void uconv_kernel(UArgs a) {
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) acc[u][p][mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    floatx4 fa[NST > 1 ? 2 : 1][S][TM], fb[NST > 1 ? 2 : 1][S][TN];
+    AT fa[NST > 1 ? 2 : 1][S][TM];
+    floatx4 fb[NST > 1 ? 2 : 1][S][TN];
     auto load_stage = [&](auto stc) {
         constexpr int st = decltype(stc)::value;
         constexpr int bf = NST > 1 ? (st & 1) : 0;
@@ -192,10 +197,15 @@ void uconv_kernel(UArgs a) {
             constexpr int c = st * S + i;                 // chunk within this wave's range
             constexpr int t = c % CPC, cc = c / CPC;
 #pragma unroll
-            for (int mi = 0; mi < TM; ++mi)
-                fa[bf][i][mi] = (UCONV_DIAG & 2) ? floatx4{(float)(va + c), 0.f, 1.f, 2.f}
-                                                 : __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                                   wr, va, sa0 + c * COUT * 64 + mi * 1024, 0));
+            for (int mi = 0; mi < TM; ++mi) {
+                const int so = sa0 + (c * COUT * 16 + mi * 256) * AE;
+                if constexpr ((UCONV_DIAG & 2) != 0)
+                    fa[bf][i][mi] = AT{};
+                else if constexpr (DT != 0)
+                    fa[bf][i][mi] = __builtin_bit_cast(shortx4, __builtin_amdgcn_raw_buffer_load_b64(wr, va, so, 0));
+                else
+                    fa[bf][i][mi] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, va, so, 0));
+            }
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni)
                 fb[bf][i][ni] = (UCONV_DIAG & 2) ? floatx4{(float)vt[t][ni], 1.f, 2.f, 3.f}
@@ -218,22 +228,23 @@ void uconv_kernel(UArgs a) {
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
                         acc[u][p][mi][ni] = mma16_lowp<DT>(fa[bf][i][mi], fb[bf][i][ni], acc[u][p][mi][ni]);
-                return;
-            }
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int mi = 0; mi < TM; ++mi)
+                    for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < TN; ++ni) {
-                        const int u = NACC2 == 2 ? (j & 1) : 0;
-                        if constexpr ((UCONV_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
-                            if (j == 0) acc[u][p][mi][ni][0] = acc[u][p][mi][ni][0] + fa[bf][i][mi][j] * fb[bf][i][ni][j];
-                        } else {
-                            acc[u][p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                                fa[bf][i][mi][j], fb[bf][i][ni][j], acc[u][p][mi][ni], 0, 0, 0);
+                        for (int ni = 0; ni < TN; ++ni) {
+                            const int u = NACC2 == 2 ? (j & 1) : 0;
+                            if constexpr ((UCONV_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
+                                if (j == 0)
+                                    acc[u][p][mi][ni][0] = acc[u][p][mi][ni][0] + fa[bf][i][mi][j] * fb[bf][i][ni][j];
+                            } else {
+                                acc[u][p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    fa[bf][i][mi][j], fb[bf][i][ni][j], acc[u][p][mi][ni], 0, 0, 0);
+                            }
                         }
-                    }
+            }
         });
     };
     // Epilogue operands of the fragments this thread finishes — fragment f = k*WK + wk for k < NMY (all
@@ -416,8 +427,10 @@ void uconv_kernel(UArgs a) {
 }
 
 // packed[c][m][16], c = cc*9 + t, element e = 4*lg + j  ->  input channel cc*16 + e, tap t = ky*3 + kx.
-// conv: w [COUT][CIN][3][3]; transposed conv: w [CIN][COUT][3][3] (torch layouts).
-__global__ __launch_bounds__(256) void uconv_pack_kernel(const float* __restrict__ w, float* __restrict__ out,
+// conv: w [COUT][CIN][3][3]; transposed conv: w [CIN][COUT][3][3] (torch layouts).  DT: element type of the
+// pack (0 fp32; LDM_DT_F16 / LDM_DT_BF16: rounded once here, to nearest even, as the kernels would round it).
+template <int DT>
+__global__ __launch_bounds__(256) void uconv_pack_kernel(const float* __restrict__ w, void* __restrict__ outp,
                                                          int CIN, int COUT, int transposed) {
     const int64_t total = (int64_t)9 * CIN * COUT;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -427,7 +440,13 @@ __global__ __launch_bounds__(256) void uconv_pack_kernel(const float* __restrict
     const int c = (int)(idx / (16 * (int64_t)COUT));
     const int cc = c / 9, t = c % 9;
     const int ci = cc * 16 + e;
-    out[idx] = transposed ? w[((int64_t)ci * COUT + m) * 9 + t] : w[((int64_t)m * CIN + ci) * 9 + t];
+    const float v = transposed ? w[((int64_t)ci * COUT + m) * 9 + t] : w[((int64_t)m * CIN + ci) * 9 + t];
+    if constexpr (DT == 0)
+        reinterpret_cast<float*>(outp)[idx] = v;
+    else if constexpr (DT == LDM_DT_F16)
+        reinterpret_cast<_Float16*>(outp)[idx] = (_Float16)v;
+    else
+        reinterpret_cast<__bf16*>(outp)[idx] = (__bf16)v;
 }
 
 // NCHW <-> NHWC for the sampler state (once before / after the loop)
@@ -676,14 +695,26 @@ extern "C" int ldm_debug_uconv_stamps(unsigned long long* host, int nblocks) {
 }
 #endif
 
-extern "C" int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream) {
+extern "C" int ldm_step_pack_weight_dt(int32_t layer, int32_t dtype, const float* w, float* packed, void* stream) {
     LDM_REQUIRE(layer >= 0 && layer <= 8 && w && packed, "step pack: bad argument");
+    LDM_REQUIRE(dtype >= LDM_DT_F32 && dtype <= LDM_DT_BF16, "step pack: unknown operand precision");
     const uc::LayerGeo& g = uc::kGeo[layer];
     const int64_t total = step_packed_floats(layer);
-    hipLaunchKernelGGL(uc::uconv_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       w, packed, g.cin, g.cout, g.mode == 2 ? 1 : 0);
+    const dim3 grid((unsigned)((total + 255) / 256));
+    const int tr = g.mode == 2 ? 1 : 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == LDM_DT_F32)
+        hipLaunchKernelGGL(uc::uconv_pack_kernel<0>, grid, dim3(256), 0, st, w, packed, g.cin, g.cout, tr);
+    else if (dtype == LDM_DT_F16)
+        hipLaunchKernelGGL(uc::uconv_pack_kernel<LDM_DT_F16>, grid, dim3(256), 0, st, w, packed, g.cin, g.cout, tr);
+    else
+        hipLaunchKernelGGL(uc::uconv_pack_kernel<LDM_DT_BF16>, grid, dim3(256), 0, st, w, packed, g.cin, g.cout, tr);
     LDM_CHECK_LAUNCH("uconv_pack_kernel");
     return 0;
+}
+
+extern "C" int ldm_step_pack_weight(int32_t layer, const float* w, float* packed, void* stream) {
+    return ldm_step_pack_weight_dt(layer, LDM_DT_F32, w, packed, stream);
 }
 
 extern "C" int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,

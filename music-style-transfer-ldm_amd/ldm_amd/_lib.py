@@ -78,6 +78,7 @@ SIGNATURES = {
     "ldm_reduce_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_step_packed_floats": (c_int64, [c_int32]),
     "ldm_step_pack_weight": (c_int32, [c_int32, c_fp, c_fp, c_vp]),
+    "ldm_step_pack_weight_dt": (c_int32, [c_int32, c_int32, c_fp, c_fp, c_vp]),
     "ldm_step_conv": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_step_conv_dt": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
                                    c_vp]),

@@ -165,11 +165,14 @@ class UNetEngine:
             w.use_fold = 1
             if self.step and shape.C == 32 and shape.nf == 64:
                 lib = L.load()
+                sdt = self.step_dtype()
                 for i, n in enumerate(_CONV_NAMES):
                     src = folded[i][0] if i in folded else getattr(u, n).weight.detach()
                     src = ops.f32c(src)
-                    buf = torch.empty(int(lib.ldm_step_packed_floats(i)), device=src.device, dtype=torch.float32)
-                    L.call("ldm_step_pack_weight", i, src.data_ptr(), buf.data_ptr(), ops.stream_handle())
+                    # 16-bit operands read a 16-bit pack (half the floats of storage)
+                    nfl = int(lib.ldm_step_packed_floats(i)) // (2 if sdt else 1)
+                    buf = torch.empty(nfl, device=src.device, dtype=torch.float32)
+                    L.call("ldm_step_pack_weight_dt", i, sdt, src.data_ptr(), buf.data_ptr(), ops.stream_handle())
                     keep += [src, buf]
                     w.step_w[i] = buf.data_ptr()
                 for j, layer in enumerate((3, 4)):
@@ -177,7 +180,7 @@ class UNetEngine:
                     keep.append(pbt)
                     w.step_pb[j] = pbt.data_ptr()
                 w.use_step = self.step
-                w.step_dtype = self.step_dtype()
+                w.step_dtype = sdt
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)

@@ -78,10 +78,12 @@ def test_content_style_100_fp16(ldm, gamp, cuda):
     assert err < TOLS["fp16"], err
 
 
-@pytest.mark.parametrize("name,layer", [(n, l) for n in ("fp16", "bf16") for l in (0, 4, 5)])
-def test_step_layer_lowp(cuda, name, layer):
-    """One step-kernel layer at fp16 / bf16 operands == float64 conv of the operands rounded the same way
-    (accumulation order aside: 1e-5), bias / ReLU / skip in fp32."""
+@pytest.mark.parametrize("name,layer,ksplit", [(n, l, k) for n in ("fp16", "bf16") for l in (0, 4, 5)
+                                               for k in ((False, True) if l in (4, 5) else (False,))])
+def test_step_layer_lowp(cuda, name, layer, ksplit):
+    """One step-kernel layer at fp16 / bf16 operands (weights packed in 16 bits, ldm_step_pack_weight_dt) ==
+    float64 conv of the operands rounded the same way (accumulation order aside: 1e-5), bias / ReLU / skip in
+    fp32; single-block and K-split forms."""
     import torch.nn.functional as F
     from ldm_amd import _lib as L
     LAYERS = [(32, 64, 0, 1), None, None, None, (512, 512, 0, 8), (512, 256, 2, 8)]
@@ -97,15 +99,20 @@ def test_step_layer_lowp(cuda, name, layer):
     sk = torch.randn(B, Cout, Hout, Wout, generator=g) if mode == 2 else None
     lib = L.load()
     st = torch.cuda.current_stream().cuda_stream
-    packed = torch.empty(int(lib.ldm_step_packed_floats(layer)), device=cuda)
-    L.call("ldm_step_pack_weight", layer, w.to(cuda).contiguous().data_ptr(), packed.data_ptr(), st)
+    dt = 1 if name == "fp16" else 2
+    packed = torch.empty(int(lib.ldm_step_packed_floats(layer)) // 2, device=cuda)     # 16-bit pack
+    L.call("ldm_step_pack_weight_dt", layer, dt, w.to(cuda).contiguous().data_ptr(), packed.data_ptr(), st)
     xd = x.permute(0, 2, 3, 1).contiguous().to(cuda)
     bd = bias.contiguous().to(cuda)
     skd = sk.permute(0, 2, 3, 1).contiguous().to(cuda) if sk is not None else None
     y = torch.full((B, Hout, Wout, Cout), float("nan"), device=cuda)
-    dt = 1 if name == "fp16" else 2
-    L.call("ldm_step_conv_dt", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), None,
-           None if skd is None else skd.data_ptr(), y.data_ptr(), dt, st)
+    if ksplit:
+        ws = torch.zeros(int(lib.ldm_step_workspace_floats(B, H, W)), device=cuda)
+        L.call("ldm_step_conv_ws", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), None,
+               None if skd is None else skd.data_ptr(), y.data_ptr(), dt, ws.data_ptr(), st)
+    else:
+        L.call("ldm_step_conv_dt", layer, B, H, W, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), None,
+               None if skd is None else skd.data_ptr(), y.data_ptr(), dt, st)
     torch.cuda.synchronize()
     rnd = (lambda t: t.half().double()) if name == "fp16" else (lambda t: t.bfloat16().double())
     x64, w64 = rnd(x), rnd(w)
