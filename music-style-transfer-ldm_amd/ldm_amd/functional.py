@@ -119,6 +119,48 @@ def _conv_backward(ctx, gy):
     return gx, gw, gb, gbc, (gy if nsk else None)
 
 
+def in_proj(q_nchw, kv_nchw, ipw, ipb):
+    """(Wq q + bq, Wkv kv + bkv) of nn.MultiheadAttention's packed in-projection (in_proj_weight [3E, E],
+    rows q | k | v) as two 1x1 convs under ONE autograd node: its backward writes the two row blocks of
+    dW and db straight into one [3E, E] / [3E] gradient (per-slice nodes would zero-fill, copy and add
+    the full tensor twice per call)."""
+    E = ipw.shape[1]
+
+    def fwd(store, q_, kv_, w_, b_):
+        dt = ops.autocast_dt()
+        wq, wkv = w_[:E].view(E, E, 1, 1), w_[E:].view(2 * E, E, 1, 1)
+        q = ops.conv_forward(q_, wq, b_[:E], stride=1, padding=0, wkey=(ipw, "q"), dtype=dt)
+        kv = ops.conv_forward(kv_, wkv, b_[E:], stride=1, padding=0, wkey=(ipw, "kv"), dtype=dt)
+        store["dtype"] = dt
+        store["owner"] = ipw        # the packed-weight caches are keyed on the parameter itself
+        store["saved"] = (q_, kv_, w_)
+        return q, kv
+
+    return hip_apply("in_proj", fwd, q_nchw, kv_nchw, ipw, ipb)
+
+
+@register_backward("in_proj")
+def _in_proj_backward(ctx, gq, gkv):
+    q_in, kv_in, w = ctx.saved_tensors
+    nq, nkv, nw, nb = ctx.needs_input_grad[3:7]
+    E = w.shape[1]
+    dt, owner = ctx.store["dtype"], ctx.store["owner"]
+    gw = torch.empty_like(w) if nw else None
+    gb = torch.empty((3 * E,), device=w.device, dtype=torch.float32) if nb else None
+    grads = []
+    for x, g, lo, hi, tag, nx in ((q_in, gq, 0, E, "q", nq), (kv_in, gkv, E, 3 * E, "kv", nkv)):
+        g = ops.f32c(g)
+        desc = _conv_desc(x, w[lo:hi].view(hi - lo, E, 1, 1), dict(transposed=False, stride=1, padding=0,
+                                                                  output_padding=0))
+        if nb:
+            ops.act_backward(g, "none", need_dv=False, need_bias=True, db_out=gb[lo:hi])
+        grads.append(ops.conv_backward_data(g, w[lo:hi].view(hi - lo, E, 1, 1), desc, (owner, tag), dtype=dt)
+                     if nx else None)
+        if nw:
+            ops.conv_backward_weight(x, g, desc, dw=gw[lo:hi].view(hi - lo, E, 1, 1), dtype=dt)
+    return grads[0], grads[1], gw, gb
+
+
 def linear(x, weight, bias, act="none"):
     """y = act(x W^T + b) for x [..., in]: a 1x1 conv over N = prod(leading dims) 'pixels'."""
     lead = x.shape[:-1]

@@ -83,8 +83,7 @@ def attention_nchw(mha, q_nchw, kv_nchw):
     Q = 1x1conv(q; W_q), KV = 1x1conv(kv; W_kv), per-head softmax attention, out = 1x1conv(.; W_o)."""
     B, E, h, w = q_nchw.shape
     ipw, ipb = mha.in_proj_weight, mha.in_proj_bias
-    q = F.conv(q_nchw, ipw[:E].view(E, E, 1, 1), ipb[:E], stride=1, padding=0, wkey=(ipw, "q"))
-    kv = F.conv(kv_nchw, ipw[E:].view(2 * E, E, 1, 1), ipb[E:], stride=1, padding=0, wkey=(ipw, "kv"))
+    q, kv = F.in_proj(q_nchw, kv_nchw, ipw, ipb)
     a = F.attention_core(q.view(B, E, h * w), kv.view(B, 2 * E, -1), mha.num_heads)
     ow = mha.out_proj.weight
     out = F.conv(a.view(B, E, h, w), ow.view(E, E, 1, 1), mha.out_proj.bias, stride=1, padding=0, wkey=(ow, "o"))

@@ -389,13 +389,17 @@ def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
     return dw
 
 
-def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=False, need_bcast=False):
-    """(dv, dbias, dbcast) of y = act(v) (+bcast[b,c]) (+skip) for NCHW dy."""
+def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=False, need_bcast=False, db_out=None):
+    """(dv, dbias, dbcast) of y = act(v) (+bcast[b,c]) (+skip) for NCHW dy; db_out (contiguous [C]) receives
+    dbias in place of a new tensor."""
     dy = f32c(dy)
     B, C = dy.shape[0], dy.shape[1]
     HW = dy.numel() // max(1, B * C)
     dv = (dy if act == "none" else torch.empty_like(dy)) if need_dv else None
-    db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_bias else None
+    if db_out is not None:
+        assert db_out.is_contiguous() and db_out.numel() == C and db_out.dtype == torch.float32
+    db = (db_out if db_out is not None else torch.empty(C, device=dy.device, dtype=torch.float32)) \
+        if need_bias else None
     dbc = torch.empty((B, C), device=dy.device, dtype=torch.float32) if need_bcast else None
     if act == "none" and not need_bias and not need_bcast:
         return dv, None, None
