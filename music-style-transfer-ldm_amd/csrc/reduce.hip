@@ -168,11 +168,24 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, fl
                                                             const float* __restrict__ bias, float* __restrict__ rmean,
                                                             float* __restrict__ rvar, float momentum, float eps,
                                                             int act, float* __restrict__ save_mean,
-                                                            float* __restrict__ save_invstd) {
+                                                            float* __restrict__ save_invstd,
+                                                            const double* __restrict__ part, int P) {
     const int k = blockIdx.x, c = blockIdx.y;
     const double count = count_arg > 0.0 ? count_arg : stats[2 * C];   // <= 0: the all-reduced count
-    const double mean = stats[2 * c] / count;
-    double var_sum = stats[2 * c + 1] - mean * stats[2 * c];   // sum (x - mean)^2
+    // part: the slice partials of bn_stats_partial_kernel, summed here in slice order exactly as
+    // slices_finalize_kernel sums them (same bits), so the rank-local path needs no finalize launch
+    double s1 = 0.0, s2 = 0.0;
+    if (part) {
+        for (int q = 0; q < P; ++q) {
+            s1 += part[((size_t)c * P + q) * 2 + 0];
+            s2 += part[((size_t)c * P + q) * 2 + 1];
+        }
+    } else {
+        s1 = stats[2 * c];
+        s2 = stats[2 * c + 1];
+    }
+    const double mean = s1 / count;
+    double var_sum = s2 - mean * s1;   // sum (x - mean)^2
     if (var_sum < 0.0) var_sum = 0.0;
     const float mean_f = (float)mean;
     const float invstd = (float)(1.0 / sqrt(var_sum / count + (double)eps));
@@ -244,11 +257,28 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __r
                                                                 const float* __restrict__ w,
                                                                 const float* __restrict__ bias, int act, int C, int HW,
                                                                 int64_t n, int64_t S, const double* __restrict__ sums,
-                                                                double count_arg, float* __restrict__ dx) {
+                                                                double count_arg, float* __restrict__ dx,
+                                                                const double* __restrict__ part, int P,
+                                                                float* __restrict__ dweight, float* __restrict__ dbias) {
     const int k = blockIdx.x, c = blockIdx.y;
     const double count = count_arg > 0.0 ? count_arg : sums[2 * C];
     const float mu = mean[c], is = invstd[c];
-    const float sgN = (float)(sums[2 * c] / count), sgxN = (float)(sums[2 * c + 1] / count);
+    // part: bn_bwd_partial_kernel's slice partials, summed in slice order as slices_finalize_kernel does
+    double a = 0.0, b = 0.0;
+    if (part) {
+        for (int q = 0; q < P; ++q) {
+            a += part[((size_t)c * P + q) * 2 + 0];
+            b += part[((size_t)c * P + q) * 2 + 1];
+        }
+        if (k == 0 && threadIdx.x == 0) {
+            if (dbias) dbias[c] = (float)a;
+            if (dweight) dweight[c] = (float)b;
+        }
+    } else {
+        a = sums[2 * c];
+        b = sums[2 * c + 1];
+    }
+    const float sgN = (float)(a / count), sgxN = (float)(b / count);
     const float kk = (w ? w[c] : 1.f) * is;
     const float alpha = is * (w ? w[c] : 1.0f);
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
@@ -435,23 +465,34 @@ extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t
     return 0;
 }
 
-extern "C" int ldm_batchnorm_apply_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const double* stats,
-                                       double count, const float* weight, const float* bias, float* running_mean,
-                                       float* running_var, float momentum, float eps, int32_t act, float* save_mean,
-                                       float* save_invstd, void* stream) {
-    LDM_REQUIRE(stats && B >= 0 && C > 0 && HW > 0 && ((x && y) || B == 0), "batchnorm_apply: bad argument");
+// part != NULL: the statistics are summed from bn_stats_partial_kernel's slice partials inside the apply
+static int bn_apply_launch(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const double* stats,
+                           double count, const float* weight, const float* bias, float* running_mean,
+                           float* running_var, float momentum, float eps, int32_t act, float* save_mean,
+                           float* save_invstd, const double* part, void* stream) {
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
     const dim3 grid(P, C);
     if (vec_ok(HW, x, y))
         hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
-                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
+                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd,
+                           part, part ? P : 0);
     else
         hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
-                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd);
+                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd,
+                           part, part ? P : 0);
     LDM_CHECK_LAUNCH("bn_apply_kernel");
     return 0;
+}
+
+extern "C" int ldm_batchnorm_apply_out(const float* x, float* y, int32_t B, int32_t C, int32_t HW, const double* stats,
+                                       double count, const float* weight, const float* bias, float* running_mean,
+                                       float* running_var, float momentum, float eps, int32_t act, float* save_mean,
+                                       float* save_invstd, void* stream) {
+    LDM_REQUIRE(stats && B >= 0 && C > 0 && HW > 0 && ((x && y) || B == 0), "batchnorm_apply: bad argument");
+    return bn_apply_launch(x, y, B, C, HW, stats, count, weight, bias, running_mean, running_var, momentum, eps, act,
+                           save_mean, save_invstd, nullptr, stream);
 }
 
 extern "C" int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
@@ -467,12 +508,21 @@ extern "C" int ldm_batchnorm_train_out(const float* x, float* y, int32_t B, int3
                                        float eps, int32_t act, float* save_mean, float* save_invstd, float* workspace,
                                        void* stream) {
     LDM_REQUIRE(x && y && workspace && B > 0 && C > 0 && HW > 0, "batchnorm: bad argument");
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "batchnorm: workspace must be 8-byte aligned");
     const int64_t n = (int64_t)B * HW;
-    double* stats = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
-    int rc = ldm_batchnorm_stats(x, B, C, HW, stats, workspace, stream);
-    if (rc) return rc;
-    return ldm_batchnorm_apply_out(x, y, B, C, HW, stats, (double)n, weight, bias, running_mean, running_var,
-                                   momentum, eps, act, save_mean, save_invstd, stream);
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    double* part = reinterpret_cast<double*>(workspace);
+    const dim3 grid(P, C);
+    // rank-local: partials, then the apply sums them itself (two launches; the SyncBatchNorm path keeps the
+    // finalize stage, whose sums it all-reduces)
+    if (vec_ok(HW, x))
+        hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
+    else
+        hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
+    LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
+    return bn_apply_launch(x, y, B, C, HW, nullptr, (double)n, weight, bias, running_mean, running_var, momentum, eps,
+                           act, save_mean, save_invstd, part, stream);
 }
 
 extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, const float* weight, const float* bias,
@@ -512,13 +562,11 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
     return 0;
 }
 
-extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
-                                            const float* save_invstd, const float* weight, const float* bias,
-                                            int32_t act, int32_t B, int32_t C, int32_t HW, const double* sums,
-                                            double count, float* dx, void* stream) {
-    LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 &&
-                    ((dy && x && dx && (y || !bn_need_y(act))) || B == 0),
-                "bn_backward_apply: bad argument");
+// part != NULL: the sums come from bn_bwd_partial_kernel's slice partials, and dweight / dbias are written here
+static int bn_bwd_apply_launch(const float* dy, const float* y, const float* x, const float* save_mean,
+                               const float* save_invstd, const float* weight, const float* bias, int32_t act, int32_t B,
+                               int32_t C, int32_t HW, const double* sums, double count, float* dx, const double* part,
+                               float* dweight, float* dbias, void* stream) {
     if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
@@ -526,12 +574,25 @@ extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, con
     const dim3 grid(P, C);
     if (vec_ok(HW, dy, y, x, dx))
         hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx);
+                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part, part ? P : 0, dweight,
+                           dbias);
     else
         hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx);
+                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part, part ? P : 0, dweight,
+                           dbias);
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
     return 0;
+}
+
+extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
+                                            const float* save_invstd, const float* weight, const float* bias,
+                                            int32_t act, int32_t B, int32_t C, int32_t HW, const double* sums,
+                                            double count, float* dx, void* stream) {
+    LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 &&
+                    ((dy && x && dx && (y || !bn_need_y(act))) || B == 0),
+                "bn_backward_apply: bad argument");
+    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums, count, dx, nullptr,
+                               nullptr, nullptr, stream);
 }
 
 extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
@@ -541,11 +602,25 @@ extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const flo
     LDM_REQUIRE(workspace && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
     const int64_t n = (int64_t)B * HW;
     double* sums = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
-    int rc = ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums,
-                                           dweight, dbias, workspace, stream);
-    if (rc || !dx) return rc;
-    return ldm_batchnorm_backward_apply(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums, (double)n,
-                                        dx, stream);
+    if (!dx)   // parameter grads only: partials + finalize
+        return ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums,
+                                             dweight, dbias, workspace, stream);
+    LDM_REQUIRE(dy && x && save_mean && save_invstd && (y || !bn_need_y(act)), "bn_backward: bad argument");
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward: workspace must be 8-byte aligned");
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    double* part = reinterpret_cast<double*>(workspace);
+    const dim3 grid(P, C);
+    if (vec_ok(HW, dy, y, x))
+        hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, weight, bias, act, C, HW, n, S, part);
+    else
+        hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
+                           save_invstd, weight, bias, act, C, HW, n, S, part);
+    LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
+    // the apply sums the partials itself and writes dweight / dbias (no finalize launch)
+    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, nullptr, (double)n, dx,
+                               part, dweight, dbias, stream);
 }
 
 extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
