@@ -132,6 +132,18 @@ static bool ustep_layer(int l) {
     return (m >> l) & 1;
 }
 
+// Layer pairs run as one launch (uconv.hip step_pair): bit l pairs layer l with l + 1 (ldm_step_set_pairs;
+// initial value LDM_UPAIR, else kPairDefault).
+constexpr int kPairDefault = 0;
+static int g_pairs = -1;
+static int step_pair_mask() {
+    if (g_pairs < 0) {
+        const char* e = std::getenv("LDM_UPAIR");
+        g_pairs = e ? (int)std::strtol(e, nullptr, 0) : kPairDefault;
+    }
+    return g_pairs;
+}
+
 static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* w) {
     if (!use_ustep(s, w)) return 0;
     int64_t m = 0;
@@ -302,46 +314,57 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     const int HW = s.H * s.W;
     const bool v3 = use_ustep(s, &w);
     const int L2 = HW / 16, L1 = HW / 64;
-    auto sc = [&](int layer, const float* x, const float* bias, float* y, const float* bcast = nullptr,
-                  const float* skip = nullptr) {
-        StepConv c{};
-        c.x = x;
-        c.w = w.step_w[layer];
-        c.y = y;
-        c.bias = bias;
-        c.bcast = bcast;
-        c.skip = skip;
-        c.dtype = w.step_dtype;
-        c.ws = ws.uks;
-        return v3 && ustep_layer(layer) ? ustep_conv(layer, s.B, c, ws.ustep, st) : step_conv(layer, s.B, s.H, s.W, c, st);
+    // the nine convs' operands: enc1..enc3, enc4 (after CA2), bottleneck (after CA1), dec4..dec2, dec1 + DDIM
+    const float* xin[9] = {ws.xs, ws.z1, ws.z2, ws.a2, ws.a1, ws.zb, ws.d4, ws.d3, ws.d2};
+    float* yout[9] = {ws.z1, ws.z2, ws.z3, ws.z4, ws.zb, ws.d4, ws.d3, ws.d2, nullptr};
+    const float* bias[9] = {w.conv_b[0], w.conv_b[1], w.conv_b[2], w.step_pb[0], w.step_pb[1], w.conv_b[5], w.conv_b[6],
+                            w.conv_b[7], w.conv_b[8]};
+    const float* skip[9] = {nullptr, nullptr, nullptr, nullptr, nullptr, ws.z3, ws.z2, ws.z1, nullptr};
+    StepConv c[9];
+    for (int l = 0; l < 9; ++l) {
+        c[l] = StepConv{};
+        c[l].x = xin[l];
+        c[l].w = w.step_w[l];
+        c[l].y = yout[l];
+        c[l].bias = bias[l];
+        c[l].skip = skip[l];
+        c[l].dtype = w.step_dtype;
+        c[l].ws = ws.uks;
+    }
+    c[1].bcast = temb;
+    c[8].coef = fuse.coef;
+    c[8].eta = fuse.eta;
+    c[8].xs = ws.xs;
+    c[8].x0_log = fuse.x0_log;
+    c[8].eps_log = fuse.eps_log;
+    const int pairs = step_pair_mask();
+    auto run = [&](int l0, int l1) -> int {   // layers [l0, l1], pairs where enabled
+        for (int l = l0; l <= l1; ++l) {
+            if (l < l1 && ((pairs >> l) & 1) && step_pair_supported(l) && ws.uks) {
+                LDM_TRY(step_pair(l, s.B, s.H, s.W, c[l], c[l + 1], st));
+                ++l;
+                continue;
+            }
+            LDM_TRY(v3 && ustep_layer(l) ? ustep_conv(l, s.B, c[l], ws.ustep, st) : step_conv(l, s.B, s.H, s.W, c[l], st));
+        }
+        return 0;
     };
-    LDM_TRY(sc(0, ws.xs, w.conv_b[0], ws.z1));
-    LDM_TRY(sc(1, ws.z1, w.conv_b[1], ws.z2, temb));
-    LDM_TRY(sc(2, ws.z2, w.conv_b[2], ws.z3));
+    LDM_TRY(run(0, 2));
     LDM_TRY(attention_folded(ws.z3, ws.kv2, ws.kf2, ws.bf2, ws.a2, s.B, 256, 4, L2, L2, st));
-    LDM_TRY(sc(3, ws.a2, w.step_pb[0], ws.z4));
+    LDM_TRY(run(3, 3));
     LDM_TRY(attention_folded(ws.z4, ws.kv1, ws.kf1, ws.bf1, ws.a1, s.B, 512, 4, L1, L1, st));
-    LDM_TRY(sc(4, ws.a1, w.step_pb[1], ws.zb));
-    LDM_TRY(sc(5, ws.zb, w.conv_b[5], ws.d4, nullptr, ws.z3));
-    LDM_TRY(sc(6, ws.d4, w.conv_b[6], ws.d3, nullptr, ws.z2));
-    LDM_TRY(sc(7, ws.d3, w.conv_b[7], ws.d2, nullptr, ws.z1));
-    StepConv c{};
-    c.x = ws.d2;
-    c.w = w.step_w[8];
-    c.bias = w.conv_b[8];
-    c.coef = fuse.coef;
-    c.eta = fuse.eta;
-    c.xs = ws.xs;
-    c.x0_log = fuse.x0_log;
-    c.eps_log = fuse.eps_log;
-    c.dtype = w.step_dtype;
-    c.ws = ws.uks;
-    return v3 && ustep_layer(8) ? ustep_conv(8, s.B, c, ws.ustep, st) : step_conv(8, s.B, s.H, s.W, c, st);
+    return run(4, 8);
 }
 
 }  // namespace ldm
 
 using namespace ldm;
+
+extern "C" int32_t ldm_step_set_pairs(int32_t mask) {
+    const int prev = step_pair_mask();
+    if (mask >= 0) g_pairs = mask;
+    return prev;
+}
 
 extern "C" int ldm_unet_layer_desc(const ldm_unet_shape* s, int32_t layer, ldm_conv_desc* d) {
     LDM_REQUIRE(s && d, "unet_layer_desc: null argument");

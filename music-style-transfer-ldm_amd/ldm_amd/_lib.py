@@ -84,6 +84,7 @@ SIGNATURES = {
                                    c_vp]),
     "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
     "ldm_step_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_step_set_pairs": (c_int32, [c_int32]),
     "ldm_step_dec1_ddim": (c_int32, [c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_fp,
                                      c_int32, c_vp]),
     "ldm_step_conv_ws": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,

@@ -6,9 +6,16 @@ copies, the asynchronous RCCL all-reduces and their joins), graph_step captures 
 steps must equal an eager trainer without a reducer BITWISE (a one-rank sum is the identity).  What stays
 unmeasured on hardware: more than one rank (SyncBN's statistic collectives only fire for world > 1) and the
 scaling curve.
+
+The body runs in a child process (a fresh HIP context and RCCL communicator, rendezvous through a FileStore):
+in round 3 the parent test process aborted in 2 of 7 runs from a background thread with no Python frame (the
+TCPStore's libuv loop logs `uv_loop_close failed ... EBUSY` at teardown even in passing runs), which took the
+whole -m gpu session down with it.  The child's exit status and output are the test's.
 """
 import os
-import socket
+import subprocess
+import sys
+import tempfile
 
 import pytest
 import torch
@@ -23,16 +30,18 @@ class _ZeroFeat(torch.nn.Module):
         return torch.zeros((), device=a.device)
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def test_graphed_step_with_rccl_reducer_equals_eager(cuda):
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import conftest, test_gpu_dp_graph as t; "
+            "t._dp_graph_body()" % here)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=here)
+    assert r.returncode == 0, f"child exited {r.returncode}\n{r.stdout[-4000:]}\n{r.stderr[-4000:]}"
+    assert "DP_GRAPH_OK" in r.stdout
+
+
+def _dp_graph_body():
     import torch.distributed as tdist
+    cuda = torch.device("cuda:0")
     import models.model as M
     import models.train as TR
     from ldm_amd import dist as hdist
@@ -40,8 +49,8 @@ def test_graphed_step_with_rccl_reducer_equals_eager(cuda):
     style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 931)).to(cuda)
     t = torch.tensor([33, 144], device=cuda)
     noise = torch.from_numpy(recipe.normal((2, 32, 16, 16), 932)).to(cuda)
-    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
-                             device_id=cuda)
+    store_dir = tempfile.mkdtemp(prefix="ldm_dp_graph_")
+    tdist.init_process_group("nccl", init_method=f"file://{store_dir}/store", rank=0, world_size=1, device_id=cuda)
     try:
         res = []
         for dp in (False, True):
@@ -66,5 +75,7 @@ def test_graphed_step_with_rccl_reducer_equals_eager(cuda):
                 assert a[k] == b[k], (k, a[k], b[k])
         for k in sde:
             assert torch.equal(sde[k], sdg[k]), k
+        torch.cuda.synchronize()
+        print("DP_GRAPH_OK", flush=True)
     finally:
         tdist.destroy_process_group()
