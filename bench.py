@@ -105,10 +105,12 @@ def _graph_time_us(fn, reps):
 STEP_LAYERS = [  # (name, Cin, Cout, mode 0 conv s1 / 1 conv s2 / 2 convT s2, input scale divisor)
     ("enc1", 32, 64, 0, 1), ("enc2", 64, 128, 1, 1), ("enc3", 128, 256, 1, 2), ("enc4", 256, 512, 1, 4),
     ("bottleneck", 512, 512, 0, 8), ("dec4", 512, 256, 2, 8), ("dec3", 256, 128, 2, 4), ("dec2", 128, 64, 2, 2)]
-USTEP_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_USTEP_LAYERS", "0xa1"), 0) >> l) & 1)
-# ^ csrc/unet.hip ustep_layer(): the layers use_step 2 runs on ustep.hip (enc1, dec4, dec2)
-KS_LAYERS = tuple(l for l in range(9) if (int(os.environ.get("LDM_UCONV_KS", "0x18"), 0) >> l) & 1)
-# ^ csrc/uconv.hip ks_on(): the layers that run the K-split step kernel (enc4, bottleneck)
+def _layer_forms():
+    """(USTEP_LAYERS, KS_LAYERS): the layers use_step 2 runs on ustep.hip / on uconv.hip's K-split form, as the
+    library reports them (ldm_step_layer_forms; LDM_USTEP_LAYERS / LDM_UCONV_KS override its defaults)."""
+    from ldm_amd import _lib as L
+    u, k = L.step_layer_forms()
+    return tuple(l for l in range(9) if (u >> l) & 1), tuple(l for l in range(9) if (k >> l) & 1)
 
 
 def time_step_layers(engine, B, H, W, dev, reps=50):
@@ -118,6 +120,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
     events on the launching stream.  dec1 runs fused with the DDIM update and is not timed alone."""
     from ldm_amd import _lib as L
     lib = L.load()
+    USTEP_LAYERS, KS_LAYERS = _layer_forms()
     shape = engine.shape(B, 32, H, W)
     w = engine.weights(shape)
     out = {}

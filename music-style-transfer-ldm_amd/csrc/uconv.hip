@@ -80,6 +80,21 @@ enum : int { ROLE_PLAIN = 0, ROLE_PRODUCER = 1, ROLE_CONSUMER = 2 };
 __host__ __device__ constexpr int tky(int t) { return t / 3; }
 __host__ __device__ constexpr int tkx(int t) { return t % 3; }
 __host__ __device__ constexpr int tphase(int t) { return (tky(t) != 1 ? 2 : 0) + (tkx(t) != 1 ? 1 : 0); }
+// The transposed layers read only four distinct input offsets over their nine taps (tap (ky, kx) reads input
+// (qy + [ky == 0], qx + [kx == 0])): the activation fragment of a tap is loaded once per (channel chunk,
+// offset) within a stage and reused by the other taps with that offset.  B_SRC<MODE, S>(i): the chunk of the
+// stage whose fragment chunk i uses (i itself when it loads).
+__host__ __device__ constexpr int toff(int t) { return (tky(t) == 0 ? 2 : 0) + (tkx(t) == 0 ? 1 : 0); }
+template <int MODE>
+__host__ __device__ constexpr int b_src(int st, int S, int i) {
+    if (MODE != 2) return i;
+    const int c = st * S + i;
+    for (int j = 0; j < i; ++j) {
+        const int cj = st * S + j;
+        if (cj / 9 == c / 9 && toff(cj % 9) == toff(c % 9)) return j;
+    }
+    return i;
+}
 
 // Diagnostic builds only (never shipped; tools/step_diag.sh): UCONV_DIAG bit 0 = no MFMAs, bit 1 = no
 // operand loads, bit 2 = per-block timestamps of wave 0 (entry and exit in 100 MHz wall ticks, the
@@ -232,7 +247,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 else
                     fa[bf][i][mi] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, va, so, 0));
             }
-            if constexpr ((PART & 2) != 0)
+            if constexpr ((PART & 2) != 0 && b_src<MODE>(st, S, i) == i)
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni)
                 fb[bf][i][ni] = (UCONV_DIAG & 2) ? floatx4{(float)vt[t][ni], 1.f, 2.f, 3.f}
@@ -248,13 +263,14 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
             constexpr int i = decltype(ic)::value;
             constexpr int c = st * S + i;
             constexpr int p = MODE == 2 ? tphase(c % CPC) : 0;
+            constexpr int ib = b_src<MODE>(st, S, i);   // the fragment this chunk's taps share
             if constexpr (DT != 0) {   // fp16 / bf16 operands: the whole 16-channel chunk in one MFMA
                 constexpr int u = NACC2 == 2 ? (c & 1) : 0;
 #pragma unroll
                 for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < TN; ++ni)
-                        acc[u][p][mi][ni] = mma16_lowp<DT>(fa[bf][i][mi], fb[bf][i][ni], acc[u][p][mi][ni]);
+                        acc[u][p][mi][ni] = mma16_lowp<DT>(fa[bf][i][mi], fb[bf][ib][ni], acc[u][p][mi][ni]);
             } else {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
@@ -265,10 +281,10 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                             const int u = NACC2 == 2 ? (j & 1) : 0;
                             if constexpr ((UCONV_DIAG & 1) != 0) {   // diagnostic: no MFMAs (operands kept live)
                                 if (j == 0)
-                                    acc[u][p][mi][ni][0] = acc[u][p][mi][ni][0] + fa[bf][i][mi][j] * fb[bf][i][ni][j];
+                                    acc[u][p][mi][ni][0] = acc[u][p][mi][ni][0] + fa[bf][i][mi][j] * fb[bf][ib][ni][j];
                             } else {
                                 acc[u][p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                                    fa[bf][i][mi][j], fb[bf][i][ni][j], acc[u][p][mi][ni], 0, 0, 0);
+                                    fa[bf][i][mi][j], fb[bf][ib][ni][j], acc[u][p][mi][ni], 0, 0, 0);
                             }
                         }
             }
@@ -663,6 +679,8 @@ static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& sl
 
 // Split-K workspace of the step kernels at this shape: arrival counters (one int32 per tile, zero between
 // launches) sized for the layer with the most tiles, then the largest layer's partial slabs.
+int step_ks_mask() { return uc::ks_mask(); }
+
 int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     using namespace uc;
     int64_t mt = 0, ms = 0;

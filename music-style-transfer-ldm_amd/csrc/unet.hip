@@ -121,16 +121,18 @@ static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
            ustep_supported(s.B, s.H, s.W);
 }
 
-// Layers that run on ustep.hip under use_step 2: measured in the reverse loop (rocprofv3, B=8), the
-// LDS-staged form wins for enc1, dec4 and dec2 and loses where it has to split K across blocks or where the
-// register-direct form already streams well (profiles/r02/README.md).
-static bool ustep_layer(int l) {
+// Layers that run on ustep.hip under use_step 2, measured in the reverse loop at B = 8: round 2 chose enc1,
+// dec4 and dec2 (profiles/r02/README.md); since the transposed layers of uconv.hip load each of their four
+// distinct activation offsets once instead of once per tap (round 3), dec4 and dec2 run faster there
+// (loop 92.5 -> 88.9 us per iteration, profiles/r03/dedup): only enc1 stays on the LDS-staged form.
+static int ustep_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_USTEP_LAYERS");   // bit l: layer l on ustep.hip (A/B timing)
-        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0) | (1 << 5) | (1 << 7);
+        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0);
     }();
-    return (m >> l) & 1;
+    return m;
 }
+static bool ustep_layer(int l) { return (ustep_mask() >> l) & 1; }
 
 // Layer pairs run as one launch (uconv.hip step_pair): bit l pairs layer l with l + 1 (ldm_step_set_pairs;
 // initial value LDM_UPAIR, else kPairDefault).
@@ -359,6 +361,13 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
 }  // namespace ldm
 
 using namespace ldm;
+
+extern "C" int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers) {
+    LDM_REQUIRE(ustep_layers && ks_layers, "step_layer_forms: null argument");
+    *ustep_layers = ustep_mask();
+    *ks_layers = step_ks_mask();
+    return 0;
+}
 
 extern "C" int32_t ldm_step_set_pairs(int32_t mask) {
     const int prev = step_pair_mask();

@@ -85,6 +85,7 @@ SIGNATURES = {
     "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
     "ldm_step_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_step_set_pairs": (c_int32, [c_int32]),
+    "ldm_step_layer_forms": (c_int32, [c_vp, c_vp]),
     "ldm_step_dec1_ddim": (c_int32, [c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_fp,
                                      c_int32, c_vp]),
     "ldm_step_conv_ws": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
@@ -212,3 +213,10 @@ def call(name, *args):
     rc = getattr(load(), name)(*args)
     check(rc, name)
     return rc
+
+
+def step_layer_forms():
+    """(ustep_layers, ks_layers) bit masks: which form each reverse-loop layer runs (ldm_step_layer_forms)."""
+    u, k = ctypes.c_int32(0), ctypes.c_int32(0)
+    call("ldm_step_layer_forms", ctypes.byref(u), ctypes.byref(k))
+    return int(u.value), int(k.value)

@@ -9,8 +9,8 @@ pinned to the reference's own outputs by tests/test_oracle_golden.py) run on the
   * timestep list bit-exact (model.py:420);
   * final x, the first pred_x0 log and the last noise_pred log within 1e-4 relative (north_star);
   * every step kernel the bench's loop launches (test_bench_config_step_kernels): each of the nine convs on
-    the instance the loop picks for it (ustep.hip for enc1 / dec4 / dec2, the K-split uconv.hip form for enc4
-    and the bottleneck, uconv.hip for enc2, enc3, dec3; dec1 with its fused DDIM update and both logs), with the
+    the instance the loop picks for it (ldm_step_layer_forms: ustep.hip for enc1, the K-split uconv.hip form for
+    enc4 and the bottleneck, uconv.hip for the others; dec1 with its fused DDIM update and both logs), with the
     engine's packed step weights, the folded out-projections and position biases, on NHWC operands at
     B = 8, 16 x 64, against float64 torch (1e-5 relative);
   * the general-kernel (conv.hip) plans of the same layers, which ldm_unet_forward (single UNet calls) runs
@@ -93,7 +93,6 @@ def _from_layout(y, shape, nhwc):
 
 def test_bench_config_step_kernels(bench_objects, cuda):
     """The loop's nine step-kernel launches at the bench geometry, each on the instance the loop uses."""
-    import os
     from ldm_amd import _lib as L
     eng, ldm = bench_objects["eng"], bench_objects["ldm"]
     B, H, W = 8, 16, 64
@@ -103,7 +102,7 @@ def test_bench_config_step_kernels(bench_objects, cuda):
     u = ldm.unet
     lib = L.load()
     st = torch.cuda.current_stream().cuda_stream
-    ustep_layers = int(os.environ.get("LDM_USTEP_LAYERS", "0xa1"), 0)
+    ustep_layers, _ = L.step_layer_forms()     # the layers the loop runs on ustep.hip
     LAYERS = [(32, 64, 0, 1), (64, 128, 1, 1), (128, 256, 1, 2), (256, 512, 1, 4), (512, 512, 0, 8),
               (512, 256, 2, 8), (256, 128, 2, 4), (128, 64, 2, 2)]
     convs = [u.enc1, u.enc2, u.enc3, u.enc4, u.bottleneck, u.dec4, u.dec3, u.dec2, u.dec1]

@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a USTEP_DIAG/UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--variant", default="hybrid", choices=["uconv", "ustep", "hybrid"],
-                    help="hybrid = what use_step 2 runs: ustep for enc1/dec4/dec2, uconv otherwise")
+                    help="hybrid = what use_step 2 runs (ldm_step_layer_forms)")
     ap.add_argument("--layers", default=None, help="comma list of layer indices (default all)")
     ap.add_argument("--loop-only", default=None, help="comma list of use_step values: only time the loop")
     args = ap.parse_args()
@@ -60,7 +60,7 @@ def main():
     for layer, name in enumerate(NAMES if args.loop_only is None else []):
         if sel is not None and layer not in sel:
             continue
-        v3 = args.variant == "ustep" or (args.variant == "hybrid" and layer in (0, 5, 7))
+        v3 = args.variant == "ustep" or (args.variant == "hybrid" and (L.step_layer_forms()[0] >> layer) & 1)
         Cin, Cout, mode = LAYERS[layer]
         Hin, Win = H // DIV[layer], W // DIV[layer]
         Hout, Wout = (Hin, Win) if mode == 0 else ((Hin // 2, Win // 2) if mode == 1 else (2 * Hin, 2 * Win))
