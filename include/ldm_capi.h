@@ -339,7 +339,7 @@ int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const f
  * previous mask.  A negative mask only reads it.  Default: LDM_UPAIR, else the measured choice. */
 int32_t ldm_step_set_pairs(int32_t mask);
 /* Which form each reverse-loop layer runs under use_step 2 (bit l = layer l): ustep_layers on the LDS-staged
- * ustep.hip kernels (LDM_USTEP_LAYERS, default enc1 only), ks_layers on uconv.hip's K-split form
+ * ustep.hip kernels (LDM_USTEP_LAYERS, default none), ks_layers on uconv.hip's K-split form
  * (LDM_UCONV_KS, default enc4 + bottleneck); every other layer on uconv.hip's single-block form. */
 int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers);
 /* ldm_step_conv with an operand precision LDM_DT_* (ldm_step_conv = LDM_DT_F32). */

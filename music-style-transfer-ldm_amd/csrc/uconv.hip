@@ -41,7 +41,19 @@
 namespace ldm {
 namespace uc {
 
-enum : int { EPI_RELU = 1, EPI_BCAST = 2, EPI_SKIP = 4, EPI_POSB = 8, EPI_DDIM = 16 };
+enum : int { EPI_RELU = 1, EPI_BCAST = 2, EPI_SKIP = 4, EPI_POSB = 8, EPI_DDIM = 16, EPI_PLANE = 32, EPI_WINDOW = 64 };
+// EPI_PLANE (a geometry flag carried with the epilogue bits): the layer's plane is 2 x 8 (the bottleneck at the
+// canonical 16 x 64 latent), so the 16 columns of a lane group are one sample's whole plane and every tap of a
+// stride-1 3x3 conv reads a position some lane of the group already holds.  Each channel chunk's activation
+// fragment is loaded once (the centre tap), parked in the wave's own LDS window, and the other eight taps are
+// read back shifted by 8 dy + dx positions (zero outside the plane): 1 global load per channel chunk instead of
+// 9.  The stride-2 layer onto that plane (enc4, input 4 x 16) parks each sample's whole input plane instead:
+// 4 loads instead of 9.  Needs MODE 0 / 1, a single stage, whole channel chunks per stage.
+// EPI_WINDOW (likewise a geometry flag): a layer whose wave covers 16 TN consecutive columns of ONE row of its
+// column grid (Wq a multiple of the block's columns): the wave loads the input rows and columns those columns'
+// taps read (stride 1: 3 x (16 TN + 2); stride 2: 3 x (32 TN + 1); transposed: 2 x (16 TN + 1); halo and
+// padding included, zeros outside the image) once per channel chunk, parks them in LDS and reads every tap from
+// there: ceil(positions / 16) global loads per channel chunk instead of 9 TN (4 TN transposed).
 
 struct UArgs {
     const float* x;       // NHWC [B, Hin, Win, CIN]
@@ -339,7 +351,200 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
     // waitcnt pass then waits progressively, chunk by chunk, in issue order
     UCONV_STAMP(1);
     using AB = std::integral_constant<int, 3>;
-    if constexpr (ROLE == ROLE_CONSUMER) {
+    constexpr bool PLANE = (EPI & EPI_PLANE) != 0;
+    static_assert(!PLANE || (NST == 1 && S % CPC == 0 && ROLE == ROLE_PLAIN), "EPI_PLANE geometry");
+    if constexpr (PLANE && MODE == 1) {
+        // stride 2 onto a 2 x 8 output plane: each sample's whole 4 x 16 input plane (64 positions, 4 loads per
+        // lane per channel chunk) goes to the wave's LDS window; tap (ky, kx) of output (qy, qx) reads input
+        // (2 qy - 1 + ky, 2 qx - 1 + kx), zero where that is -1 (the top / left padding; the bottom / right
+        // never pass the plane)
+        constexpr int NCC = S / CPC;
+        floatx4 wl[NCC][TN][4];
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+            const int bs = colsel(cb, ni);   // this column set's sample (16 columns = one sample)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = k * 64 + lane, pos = e >> 2, g4 = e & 3;
+                const int off = colsel(cval, ni) ? ((bs * 4 + (pos >> 4)) * 16 + (pos & 15)) * (CIN * 4) + g4 * 16 : kOOB;
+                static_for<0, NCC>([&](auto ccc) {
+                    constexpr int cc = decltype(ccc)::value;
+                    wl[cc][ni][k] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, sb0 + cc * 64, XAUX));
+                });
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        epi_prefetch();
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int kRedFloats = WK > 1 ? WK * WN * NPH * TM * TN * 64 * 4 : 0;
+        float* win = smem + kRedFloats + wave * (NCC * TN * 1024);
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<floatx4*>(win + (cc * TN + ni) * 1024 + (k * 64 + lane) * 4) = wl[cc][ni][k];
+        });
+        const int qy = col >> 3, qx = col & 7;
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+            static_for<0, CPC>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                const int iy = 2 * qy - 1 + tky(t), ix = 2 * qx - 1 + tkx(t);
+                const bool in = iy >= 0 && ix >= 0;
+                const int o = in ? (iy * 16 + ix) * 16 + lg * 4 : 0;
+#pragma unroll
+                for (int ni = 0; ni < TN; ++ni) {
+                    const floatx4 v = *reinterpret_cast<const floatx4*>(win + (cc * TN + ni) * 1024 + o);
+                    fb[0][cc * CPC + t][ni] = in ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+            });
+        });
+    } else if constexpr (PLANE && MODE == 2) {
+        // transposed conv over a 2 x 8 input plane: the four offsets a tap reads, (qy + oy, qx + ox) with oy, ox in
+        // {0, 1}, are all in the sample's own plane (zero past its last row / column): one load per channel chunk
+        constexpr int NCC = S / CPC;
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)   // tap 8 = (2, 2) reads offset (0, 0): the lane's own position
+                fb[0][cc * CPC + 4][ni] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                          xr, vt[8][ni], sb0 + cc * 64, XAUX));
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        epi_prefetch();
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int kRedFloats = WK > 1 ? WK * WN * NPH * TM * TN * 64 * 4 : 0;
+        float* win = smem + kRedFloats + wave * (NCC * TN * 256);
+        const int py = col >> 3, px = col & 7;
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                *reinterpret_cast<floatx4*>(win + ((cc * TN + ni) * 16 + col) * 16 + lg * 4) = fb[0][cc * CPC + 4][ni];
+        });
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+            static_for<0, CPC>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                constexpr int i = cc * CPC + t;
+                if constexpr (b_src<MODE>(0, S, i) == i) {
+                    constexpr int oy = tky(t) == 0 ? 1 : 0, ox = tkx(t) == 0 ? 1 : 0;
+                    const bool in = py + oy < 2 && px + ox < 8;
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const floatx4 v =
+                            *reinterpret_cast<const floatx4*>(win + ((cc * TN + ni) * 16 + col + 8 * oy + ox) * 16 + lg * 4);
+                        fb[0][i][ni] = in ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+            });
+        });
+    } else if constexpr (PLANE) {
+        constexpr int NCC = S / CPC;   // channel chunks of this wave
+        // centre taps first (the window waits on them only), then the weight stream, then the epilogue operands
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                fb[0][cc * CPC + 4][ni] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                          xr, vt[4][ni], sb0 + cc * 64, XAUX));
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        epi_prefetch();
+        __builtin_amdgcn_sched_barrier(0);
+        // the wave's window: [cc][ni][16 positions][16 channels] fp32, after the K-reduction buffer
+        constexpr int kRedFloats = WK > 1 ? WK * WN * NPH * TM * TN * 64 * 4 : 0;
+        float* win = smem + kRedFloats + wave * (NCC * TN * 256);
+        const int py = col >> 3, px = col & 7;
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+                *reinterpret_cast<floatx4*>(win + ((cc * TN + ni) * 16 + col) * 16 + lg * 4) = fb[0][cc * CPC + 4][ni];
+        });
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+            static_for<0, CPC>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                if constexpr (t != 4) {
+                    constexpr int dy = tky(t) - 1, dx = tkx(t) - 1;
+                    const bool in = (unsigned)(py + dy) < 2u && (unsigned)(px + dx) < 8u;
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const floatx4 v =
+                            *reinterpret_cast<const floatx4*>(win + ((cc * TN + ni) * 16 + col + 8 * dy + dx) * 16 + lg * 4);
+                        fb[0][cc * CPC + t][ni] = in ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+            });
+        });
+    } else if constexpr ((EPI & EPI_WINDOW) != 0) {
+        static_assert(NST == 1 && S % CPC == 0 && ROLE == ROLE_PLAIN, "EPI_WINDOW geometry");
+        constexpr int NCC = S / CPC;           // channel chunks of this wave
+        // the input rows and columns the wave's 16 TN output columns (one row of the column grid) read:
+        // stride 1: rows y0-1..y0+1, columns x0-1..x0+16TN; stride 2: rows 2y0-1..2y0+1, columns
+        // 2x0-1..2x0+32TN-1; transposed (input grid): rows y0..y0+1, columns x0..x0+16TN
+        constexpr int WR = MODE == 2 ? 2 : 3;
+        constexpr int WC = MODE == 0 ? 16 * TN + 2 : (MODE == 1 ? 32 * TN + 1 : 16 * TN + 1);
+        constexpr int WPOS = WR * WC;          // window positions
+        constexpr int NLD = (WPOS * 4 + 63) / 64;   // 16-byte loads per lane per channel chunk
+        const int b0 = a.fd_hw.div(nbase);
+        const int rem = nbase - b0 * (a.Hq * a.Wq);
+        const int y0 = a.fd_w.div(rem);
+        const int x0 = rem - y0 * a.Wq;
+        const int iy0 = MODE == 0 ? y0 - 1 : (MODE == 1 ? 2 * y0 - 1 : y0);
+        const int ix0 = MODE == 0 ? x0 - 1 : (MODE == 1 ? 2 * x0 - 1 : x0);
+        floatx4 wl[NCC][NLD];
+        int wpos[NLD];
+        static_for<0, NLD>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int e = k * 64 + lane;       // window slot: (position, 4-channel group)
+            const int pos = e >> 2, g4 = e & 3;
+            const int r = pos / WC, cx = pos - r * WC;
+            const int iy = iy0 + r, ix = ix0 + cx;
+            const bool ok = e < WPOS * 4 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win && nbase < a.Nq;
+            const int off = ok ? ((b0 * a.Hin + iy) * a.Win + ix) * (CIN * 4) + g4 * 16 : kOOB;
+            wpos[k] = e < WPOS * 4 ? pos * 16 + g4 * 4 : -1;
+            static_for<0, NCC>([&](auto ccc) {
+                constexpr int cc = decltype(ccc)::value;
+                wl[cc][k] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, sb0 + cc * 64, XAUX));
+            });
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        epi_prefetch();
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int kRedFloats = WK > 1 ? WK * WN * NPH * TM * TN * 64 * 4 : 0;
+        float* win = smem + kRedFloats + wave * (NCC * WPOS * 16);
+        static_for<0, NLD>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            static_for<0, NCC>([&](auto ccc) {
+                constexpr int cc = decltype(ccc)::value;
+                if (wpos[k] >= 0) *reinterpret_cast<floatx4*>(win + cc * WPOS * 16 + wpos[k]) = wl[cc][k];
+            });
+        });
+        static_for<0, NCC>([&](auto ccc) {
+            constexpr int cc = decltype(ccc)::value;
+            static_for<0, CPC>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                constexpr int i = cc * CPC + t;
+                if constexpr (b_src<MODE>(0, S, i) == i) {   // transposed: one read per distinct offset
+                    constexpr int wr = MODE == 2 ? (tky(t) == 0 ? 1 : 0) : tky(t);
+                    constexpr int wx = MODE == 2 ? (tkx(t) == 0 ? 1 : 0) : tkx(t);
+#pragma unroll
+                    for (int ni = 0; ni < TN; ++ni) {
+                        const int cx = MODE == 1 ? 2 * (16 * ni + col) + wx : 16 * ni + col + wx;
+                        fb[0][i][ni] = *reinterpret_cast<const floatx4*>(win + cc * WPOS * 16 + (wr * WC + cx) * 16 + lg * 4);
+                    }
+                }
+            });
+        });
+    } else if constexpr (ROLE == ROLE_CONSUMER) {
         // the weights and the epilogue operands do not depend on the producer: in flight before the wait
         load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
         epi_prefetch();
@@ -596,7 +801,14 @@ template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, 
 static int launch_dt(const UArgs& a, hipStream_t st) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
     const int blocks = a.nMt * a.nNt * KS;
-    const size_t lds = std::max<size_t>(WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0, KS > 1 ? 16 : 0);
+    size_t lds = std::max<size_t>(WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0, KS > 1 ? 16 : 0);
+    if constexpr ((EPI & EPI_PLANE) != 0)   // + each wave's activation window (see EPI_PLANE; 4 KB per sample at stride 2)
+        lds = (WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0) + (size_t)WN * WK * (S / 9) * TN * (MODE == 1 ? 4096 : 1024);
+    if constexpr ((EPI & EPI_WINDOW) != 0) {   // + each wave's row window (see EPI_WINDOW)
+        constexpr int WR = MODE == 2 ? 2 : 3;
+        constexpr int WC = MODE == 0 ? 16 * TN + 2 : (MODE == 1 ? 32 * TN + 1 : 16 * TN + 1);
+        lds = (WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0) + (size_t)WN * WK * (S / 9) * WR * WC * 64;
+    }
     auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * WN * WK), lds, st, a);
     LDM_CHECK_LAUNCH("uconv_kernel");
@@ -665,6 +877,22 @@ static int ks_mask() {
     return m;
 }
 static bool ks_on(int layer) { return kKs[layer].ks > 1 && ((ks_mask() >> layer) & 1); }
+// EPI_WINDOW instances where the geometry allows (LDM_UCONV_WINDOW=0 turns them off for A/B timing)
+static bool window_taps() {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_WINDOW");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
+// EPI_PLANE instances where the geometry allows (LDM_UCONV_PLANE=0 turns them off for A/B timing)
+static bool plane_taps() {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_PLANE");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
 // spatial size divisor of each layer's input (model.py:178-194)
 constexpr int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
 static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& slab_floats) {
@@ -773,10 +1001,16 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
         switch (layer) {
             case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 2, 1, 4, 9, 9, EPI_RELU, 2>(a, s.dtype, st);
             case 3: LDM_REQUIRE(s.y, "enc4: y");
+                if (a.Hin == 4 && a.Win == 16 && plane_taps())   // the canonical latent: a 2 x 8 output plane
+                    return launch<1, 256, 512, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 4>(a, s.dtype, st);
                 return launch<1, 256, 512, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_POSB, 4>(a, s.dtype, st);
             case 4: LDM_REQUIRE(s.y, "bottleneck: y");
+                if (a.Hin == 2 && a.Win == 8 && plane_taps())   // the canonical latent: one sample per lane group
+                    return launch<0, 512, 512, 2, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 4>(a, s.dtype, st);
                 return launch<0, 512, 512, 2, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB, 4>(a, s.dtype, st);
             case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
+                if (a.Hin == 2 && a.Win == 8 && plane_taps())
+                    return launch<2, 512, 256, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP | EPI_PLANE, 8>(a, s.dtype, st);
                 return launch<2, 512, 256, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, 8>(a, s.dtype, st);
             case 6: LDM_REQUIRE(s.y && s.skip, "dec3: y, skip");
                 return launch<2, 256, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, 4>(a, s.dtype, st);
@@ -784,19 +1018,32 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
         }
     }
     switch (layer) {
-        case 0: LDM_REQUIRE(s.y, "enc1: y"); return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, s.dtype, st);
+        case 0: LDM_REQUIRE(s.y, "enc1: y");
+            if (window_taps() && a.Wq % 64 == 0)   // a block's 64 columns lie in one row
+                return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU | EPI_WINDOW>(a, s.dtype, st);
+            return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 1: LDM_REQUIRE(s.y && s.bcast, "enc2: y, t_emb");
+            if (window_taps() && a.Wq % 32 == 0)
+                return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST | EPI_WINDOW>(a, s.dtype, st);
             return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, s.dtype, st);
-        case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, s.dtype, st);
+        case 2: LDM_REQUIRE(s.y, "enc3: y");
+            if (window_taps() && a.Wq % 16 == 0) return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU | EPI_WINDOW>(a, s.dtype, st);
+            return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 3: LDM_REQUIRE(s.y, "enc4: y"); return launch<1, 256, 512, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_POSB>(a, s.dtype, st);
         case 4: LDM_REQUIRE(s.y, "bottleneck: y"); return launch<0, 512, 512, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_POSB>(a, s.dtype, st);
         case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
             return launch<2, 512, 256, 1, 1, 1, 8, 36, 12, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         case 6: LDM_REQUIRE(s.y && s.skip, "dec3: y, skip");
+            if (window_taps() && a.Wq % 16 == 0)
+                return launch<2, 256, 128, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_SKIP | EPI_WINDOW>(a, s.dtype, st);
             return launch<2, 256, 128, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         case 7: LDM_REQUIRE(s.y && s.skip, "dec2: y, skip");
+            if (window_taps() && a.Wq % 32 == 0)
+                return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP | EPI_WINDOW>(a, s.dtype, st);
             return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         default: LDM_REQUIRE(s.xs && s.coef, "dec1: sampler state, coefficients");
+            if (window_taps() && a.Wq % 32 == 0)   // a block's 32 columns lie in one row
+                return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM | EPI_WINDOW>(a, s.dtype, st);
             return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, s.dtype, st);
     }
 }

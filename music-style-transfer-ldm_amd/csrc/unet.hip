@@ -122,13 +122,15 @@ static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
 }
 
 // Layers that run on ustep.hip under use_step 2, measured in the reverse loop at B = 8: round 2 chose enc1,
-// dec4 and dec2 (profiles/r02/README.md); since the transposed layers of uconv.hip load each of their four
-// distinct activation offsets once instead of once per tap (round 3), dec4 and dec2 run faster there
-// (loop 92.5 -> 88.9 us per iteration, profiles/r03/dedup): only enc1 stays on the LDS-staged form.
+// dec4 and dec2 (profiles/r02/README.md).  Round 3: the transposed layers of uconv.hip load each of their four
+// distinct activation offsets once instead of once per tap (dec4 and dec2 back on uconv.hip: loop 92.5 -> 88.9
+// us per iteration, profiles/r03/dedup), and the stride-1 / small-plane layers form their taps from an LDS
+// window (EPI_WINDOW / EPI_PLANE: 88.9 -> 85.1 with enc1 back on uconv.hip, profiles/r03/taps): none stays on
+// the LDS-DMA form by default.
 static int ustep_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_USTEP_LAYERS");   // bit l: layer l on ustep.hip (A/B timing)
-        return e ? (int)std::strtol(e, nullptr, 0) : (1 << 0);
+        return e ? (int)std::strtol(e, nullptr, 0) : 0;
     }();
     return m;
 }
