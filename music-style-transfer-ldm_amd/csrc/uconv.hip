@@ -387,6 +387,10 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 for (int k = 0; k < 4; ++k)
                     *reinterpret_cast<floatx4*>(win + (cc * TN + ni) * 1024 + (k * 64 + lane) * 4) = wl[cc][ni][k];
         });
+        // the taps read what OTHER lanes of this wave wrote: the compiler, which reasons per lane, may otherwise
+        // hoist a read above a write it cannot alias (and the LDS hand back the previous launch's window).  A
+        // wave's LDS operations execute in order, so the wave only waits for its own writes: no block barrier.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const int qy = col >> 3, qx = col & 7;
         static_for<0, NCC>([&](auto ccc) {
             constexpr int cc = decltype(ccc)::value;
@@ -426,6 +430,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
             for (int ni = 0; ni < TN; ++ni)
                 *reinterpret_cast<floatx4*>(win + ((cc * TN + ni) * 16 + col) * 16 + lg * 4) = fb[0][cc * CPC + 4][ni];
         });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // cross-lane through LDS: see the stride-2 plane branch
         static_for<0, NCC>([&](auto ccc) {
             constexpr int cc = decltype(ccc)::value;
             static_for<0, CPC>([&](auto tc) {
@@ -467,6 +472,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
             for (int ni = 0; ni < TN; ++ni)
                 *reinterpret_cast<floatx4*>(win + ((cc * TN + ni) * 16 + col) * 16 + lg * 4) = fb[0][cc * CPC + 4][ni];
         });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // cross-lane through LDS: see the stride-2 plane branch
         static_for<0, NCC>([&](auto ccc) {
             constexpr int cc = decltype(ccc)::value;
             static_for<0, CPC>([&](auto tc) {
@@ -528,6 +534,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 if (wpos[k] >= 0) *reinterpret_cast<floatx4*>(win + cc * WPOS * 16 + wpos[k]) = wl[cc][k];
             });
         });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // cross-lane through LDS: see the stride-2 plane branch
         static_for<0, NCC>([&](auto ccc) {
             constexpr int cc = decltype(ccc)::value;
             static_for<0, CPC>([&](auto tc) {
@@ -810,6 +817,13 @@ static int launch_dt(const UArgs& a, hipStream_t st) {
         lds = (WK > 1 ? (size_t)WK * WN * NPH * TM * TN * 64 * 16 : 0) + (size_t)WN * WK * (S / 9) * WR * WC * 64;
     }
     auto kfn = uconv_kernel<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS>;
+    if (lds > 64 * 1024) {   // dynamic LDS past 64 KiB needs the per-function opt-in, once
+        static bool opted = false;
+        if (!opted) {
+            LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            opted = true;
+        }
+    }
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * WN * WK), lds, st, a);
     LDM_CHECK_LAUNCH("uconv_kernel");
     return 0;
@@ -844,6 +858,17 @@ constexpr KsGeo kKs[9] = {
     {0, 0, 0, 0},   // dec1
 };
 
+// Variant 2 ("thin"): a 16 x 32 block tile with K split over 2-4 blocks of 8 waves: the same weight bytes per
+// block as variant 1, a partial tile of a quarter / half the size for the last arriver to gather (its hand-off
+// cost grows with KS x the tile).  Selected by bit l of LDM_UCONV_KS2 for a layer also in LDM_UCONV_KS.
+constexpr KsGeo kKs2[9] = {
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+    {1, 2, 8, 2},   // enc4        128 tiles x 2
+    {1, 2, 8, 2},   // bottleneck  128 tiles x 2 (two channel chunks per wave)
+    {1, 2, 8, 4},   // dec4        64 tiles x 4
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+};
+
 constexpr LayerGeo kGeo[9] = {
     {0, 32, 64, 2, 1, 4, 1},     // enc1        conv3x3 s1
     {1, 64, 128, 2, 2, 1, 4},    // enc2        conv3x3 s2 (+ t_emb)
@@ -866,9 +891,11 @@ int64_t step_packed_floats(int layer) {
 
 namespace uc {
 // Layers that run the K-split variant: bit l of LDM_UCONV_KS (read once; default kKsDefault).
-// Measured in the loop's chain timing (bench.py kernels, B = 8): the split form gains 0.4 us on the bottleneck
-// and 0.2 us on enc4, and loses 0.9-1.5 us on enc3, dec4 and dec3 (their single-block forms stay).
-constexpr int kKsDefault = (1 << 3) | (1 << 4);
+// Round 2, in the loop's chain timing (B = 8): the split form gained 0.4 us on the bottleneck and 0.2 us on enc4
+// and lost 0.9-1.5 us on enc3, dec4 and dec3.  Round 3, with the taps formed from LDS windows, the loop with
+// enc4, the bottleneck and dec4 on the thin variant (kKs2) measured best (82.5 us per iteration against 84.0
+// for the round-2 choice, profiles/r03/ks2).
+constexpr int kKsDefault = (1 << 3) | (1 << 4) | (1 << 5);
 static int ks_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS");
@@ -877,6 +904,19 @@ static int ks_mask() {
     return m;
 }
 static bool ks_on(int layer) { return kKs[layer].ks > 1 && ((ks_mask() >> layer) & 1); }
+constexpr int kKs2Default = (1 << 3) | (1 << 4) | (1 << 5);
+static int ks2_mask() {
+    static const int m = [] {
+        const char* e = std::getenv("LDM_UCONV_KS2");
+        return e ? (int)std::strtol(e, nullptr, 0) : kKs2Default;
+    }();
+    return m;
+}
+// K-split form of a layer: 0 none, 1 variant 1 (kKs), 2 variant 2 (kKs2)
+static int ks_form(int layer) {
+    if (layer < 0 || layer > 8 || !ks_on(layer)) return 0;
+    return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
+}
 // EPI_WINDOW instances where the geometry allows (LDM_UCONV_WINDOW=0 turns them off for A/B timing)
 static bool window_taps() {
     static const bool on = [] {
@@ -895,9 +935,9 @@ static bool plane_taps() {
 }
 // spatial size divisor of each layer's input (model.py:178-194)
 constexpr int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
-static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& slab_floats) {
+static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& slab_floats, int form = 1) {
     const LayerGeo& g = kGeo[layer];
-    const KsGeo& k = kKs[layer];
+    const KsGeo& k = form == 2 ? kKs2[layer] : kKs[layer];
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     const int64_t nq = (int64_t)B * (g.mode == 1 ? (Hin / 2) * (Win / 2) : Hin * Win);
     tiles = (int64_t)(g.cout / (16 * k.tm)) * ((nq + 16 * k.tn - 1) / (16 * k.tn));
@@ -913,11 +953,13 @@ int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     using namespace uc;
     int64_t mt = 0, ms = 0;
     for (int l = 0; l < 9; ++l) {
-        if (kKs[l].ks <= 1) continue;   // every K-split geometry: the layer pairs run dec4's whatever the mask
-        int64_t t, sf;
-        ks_tiles(l, B, H, W, t, sf);
-        mt = std::max(mt, t);
-        ms = std::max(ms, sf);
+        for (int form = 1; form <= 2; ++form) {   // every K-split geometry, whatever the masks select
+            if ((form == 1 ? kKs[l].ks : kKs2[l].ks) <= 1) continue;
+            int64_t t, sf;
+            ks_tiles(l, B, H, W, t, sf, form);
+            mt = std::max(mt, t);
+            ms = std::max(ms, sf);
+        }
     }
     const int64_t c = (mt + 63) / 64 * 64;
     if (cnt_floats) *cnt_floats = c;
@@ -934,11 +976,14 @@ static int32_t* pair_counters(float* ws, int B, int H, int W) {
 
 namespace uc {
 // The launch arguments of layer `layer` (ksv: the K-split form).
-static int make_args(int layer, int B, int H, int W, const StepConv& s, bool ksv, UArgs& a) {
+static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv, UArgs& a) {
     LDM_REQUIRE(layer >= 0 && layer <= 8, "step conv: layer index");
     LDM_REQUIRE(B > 0 && H % 8 == 0 && W % 8 == 0, "step conv: latent H, W must be multiples of 8");
     LayerGeo g = kGeo[layer];
-    if (ksv) g.tm = kKs[layer].tm, g.tn = kKs[layer].tn, g.wn = 1, g.wk = kKs[layer].wk;
+    if (ksv) {
+        const KsGeo& k = ksv == 2 ? kKs2[layer] : kKs[layer];
+        g.tm = k.tm, g.tn = k.tn, g.wn = 1, g.wk = k.wk;
+    }
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     a = UArgs{};
     a.x = s.x;
@@ -979,7 +1024,7 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, bool ksv
         int64_t cnt = 0;
         const int64_t wsf = step_ws_floats(B, H, W, &cnt);
         int64_t tiles, sf;
-        ks_tiles(layer, B, H, W, tiles, sf);
+        ks_tiles(layer, B, H, W, tiles, sf, ksv);
         LDM_REQUIRE(tiles == (int64_t)a.nMt * a.nNt && wsf >= cnt + sf && (cnt + sf) * 4 < 0x7fffffffLL,
                     "step conv: split-K workspace geometry");
         a.cnt = reinterpret_cast<int32_t*>(s.ws);
@@ -994,9 +1039,27 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, bool ksv
 
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st) {
     using namespace uc;
-    const bool ksv = layer >= 0 && layer <= 8 && ks_on(layer) && s.ws;   // without a workspace: single-block form
+    const int ksv = s.ws ? ks_form(layer) : 0;   // without a workspace: the single-block form
     UArgs a;
     UC_TRY(make_args(layer, B, H, W, s, ksv, a));
+    if (ksv == 2) {
+        const bool pl = plane_taps();
+        switch (layer) {
+            case 3: LDM_REQUIRE(s.y, "enc4: y");
+                if (a.Hin == 4 && a.Win == 16 && pl)
+                    return launch<1, 256, 512, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 2>(a, s.dtype, st);
+                return launch<1, 256, 512, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB, 2>(a, s.dtype, st);
+            case 4: LDM_REQUIRE(s.y, "bottleneck: y");
+                if (a.Hin == 2 && a.Win == 8 && pl)
+                    return launch<0, 512, 512, 1, 2, 1, 8, 18, 18, EPI_RELU | EPI_POSB | EPI_PLANE, 2>(a, s.dtype, st);
+                return launch<0, 512, 512, 1, 2, 1, 8, 18, 18, EPI_RELU | EPI_POSB, 2>(a, s.dtype, st);
+            case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
+                if (a.Hin == 2 && a.Win == 8 && pl)
+                    return launch<2, 512, 256, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_SKIP | EPI_PLANE, 4>(a, s.dtype, st);
+                return launch<2, 512, 256, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_SKIP, 4>(a, s.dtype, st);
+            default: return fail(2, "step conv: no K-split variant 2 for this layer");
+        }
+    }
     if (ksv) {
         switch (layer) {
             case 2: LDM_REQUIRE(s.y, "enc3: y"); return launch<1, 128, 256, 2, 2, 1, 4, 9, 9, EPI_RELU, 2>(a, s.dtype, st);
@@ -1086,8 +1149,8 @@ int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& s
     using namespace uc;
     LDM_REQUIRE(step_pair_supported(la) && sa.ws && sa.dtype == sb.dtype, "step pair: unsupported layer pair");
     UArgs a, b;
-    UC_TRY(make_args(la, B, H, W, sa, la == 6, a));
-    UC_TRY(make_args(la + 1, B, H, W, sb, false, b));
+    UC_TRY(make_args(la, B, H, W, sa, la == 6 ? 1 : 0, a));
+    UC_TRY(make_args(la + 1, B, H, W, sb, 0, b));
     int32_t* cnt = pair_counters(sa.ws, B, H, W);
     switch (sa.dtype) {
         case LDM_DT_F32: return pair_dt<0>(la, a, b, cnt, st);

@@ -367,7 +367,7 @@ using namespace ldm;
 extern "C" int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers) {
     LDM_REQUIRE(ustep_layers && ks_layers, "step_layer_forms: null argument");
     *ustep_layers = ustep_mask();
-    *ks_layers = step_ks_mask();
+    *ks_layers = step_ks_mask();   // (their K-split geometry: LDM_UCONV_KS2, uconv.hip kKs2)
     return 0;
 }
 
