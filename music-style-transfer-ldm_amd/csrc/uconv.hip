@@ -917,6 +917,16 @@ static int ks_form(int layer) {
     if (layer < 0 || layer > 8 || !ks_on(layer)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
 }
+// enc3 on 16-row tiles (half the weight bytes per block of the 32-row form), each wave one 16-column row of the
+// 4 x 16 output plane so that its taps come from a row window.  Measured in the loop: 80.9 against 80.5 us per
+// iteration for the 32-row form (profiles/r03/enc3_thin), so off unless LDM_UCONV_ENC3_THIN=1.
+static bool enc3_thin(int W) {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_ENC3_THIN");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    return on && (W / 4) % 16 == 0;   // enc3's output row (W / 4 columns) holds whole 16-column groups
+}
 // EPI_WINDOW instances where the geometry allows (LDM_UCONV_WINDOW=0 turns them off for A/B timing)
 static bool window_taps() {
     static const bool on = [] {
@@ -983,6 +993,8 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     if (ksv) {
         const KsGeo& k = ksv == 2 ? kKs2[layer] : kKs[layer];
         g.tm = k.tm, g.tn = k.tn, g.wn = 1, g.wk = k.wk;
+    } else if (layer == 2 && enc3_thin(W)) {
+        g = LayerGeo{1, 128, 256, 1, 1, 2, 2};   // 16 rows x 2 column groups of one row each, K over 2 waves
     }
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     a = UArgs{};
@@ -1090,6 +1102,10 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST | EPI_WINDOW>(a, s.dtype, st);
             return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, s.dtype, st);
         case 2: LDM_REQUIRE(s.y, "enc3: y");
+            if (enc3_thin(W)) {
+                if (window_taps()) return launch<1, 128, 256, 1, 1, 2, 2, 36, 36, EPI_RELU | EPI_WINDOW>(a, s.dtype, st);
+                return launch<1, 128, 256, 1, 1, 2, 2, 36, 36, EPI_RELU>(a, s.dtype, st);
+            }
             if (window_taps() && a.Wq % 16 == 0) return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU | EPI_WINDOW>(a, s.dtype, st);
             return launch<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 3: LDM_REQUIRE(s.y, "enc4: y"); return launch<1, 256, 512, 1, 1, 1, 4, 36, 36, EPI_RELU | EPI_POSB>(a, s.dtype, st);
@@ -1123,7 +1139,6 @@ static int launch_pair(const UArgs& a, const UArgs& b, int ksA, int ksB, int32_t
 // the instances of step_conv's table, as types
 template <int DT> using UEnc1 = UBody<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU, DT>;
 template <int DT> using UEnc2 = UBody<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST, DT>;
-template <int DT> using UEnc3 = UBody<1, 128, 256, 2, 1, 1, 4, 18, 18, EPI_RELU, DT>;
 template <int DT> using UDec3K = UBody<2, 256, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, DT, 4>;
 template <int DT> using UDec2 = UBody<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP, DT>;
 template <int DT> using UDec1 = UBody<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM, DT>;
@@ -1132,7 +1147,6 @@ template <int DT>
 static int pair_dt(int la, const UArgs& a, const UArgs& b, int32_t* cnt, hipStream_t st) {
     switch (la) {
         case 0: return launch_pair<UEnc1<DT>, UEnc2<DT>>(a, b, 1, 1, cnt, st);
-        case 1: return launch_pair<UEnc2<DT>, UEnc3<DT>>(a, b, 1, 1, cnt, st);
         case 6: return launch_pair<UDec3K<DT>, UDec2<DT>>(a, b, 4, 1, cnt, st);
         case 7: return launch_pair<UDec2<DT>, UDec1<DT>>(a, b, 1, 1, cnt, st);
         default: return fail(2, "step pair: no pair starts at this layer");
@@ -1140,7 +1154,7 @@ static int pair_dt(int la, const UArgs& a, const UArgs& b, int32_t* cnt, hipStre
 }
 }  // namespace uc
 
-bool step_pair_supported(int la) { return la == 0 || la == 1 || la == 6 || la == 7; }
+bool step_pair_supported(int la) { return la == 0 || la == 6 || la == 7; }
 
 // Layers la and la + 1 in one launch (uc::upair_kernel): la's blocks hand their output to la + 1's blocks
 // inside the launch.  sa.ws: the step workspace (its tail holds the pair counters).  A dec3 producer runs its
