@@ -630,10 +630,9 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
     if constexpr (KS > 1) {
         // ---- K split over blocks: write-through (sc1) partial tile, arrival counter, the last block of the
         //      tile sums the KS partials in split order (deterministic) and runs the epilogue ---------------
-        static_assert(WN == 1, "one wave column per block under a K split");
         const int tile = mt + nt * a.nMt;
         const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.slab), (short)0, 0x7fffffff, 0x00020000);
-        auto slab_off = [&](int kk, int f) { return (((tile * KS + kk) * NFR + f) * 64 + lane) * 16; };
+        auto slab_off = [&](int kk, int f) { return ((((tile * KS + kk) * WN + wn) * NFR + f) * 64 + lane) * 16; };
         static_for<0, NMY>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int f = frag(k);
@@ -844,7 +843,7 @@ static int launch(const UArgs& a, int dtype, hipStream_t st) {
 // 16 x 16, so a block pulls half the operand bytes per MFMA, with K split over KS blocks to keep 256 blocks
 // (write-through partial tiles, last arriver sums in split order).  {tm, tn, wk, ks}; ks 0 = no variant.
 struct KsGeo {
-    int tm, tn, wk, ks;
+    int tm, tn, wk, ks, wn = 1;
 };
 constexpr KsGeo kKs[9] = {
     {0, 0, 0, 0},   // enc1
@@ -864,7 +863,7 @@ constexpr KsGeo kKs[9] = {
 constexpr KsGeo kKs2[9] = {
     {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
     {1, 2, 8, 2},   // enc4        128 tiles x 2
-    {1, 2, 8, 2},   // bottleneck  128 tiles x 2 (two channel chunks per wave)
+    {1, 2, 4, 4, 2},   // bottleneck  64 tiles (16 x 64: 2 wave columns) x 4, two channel chunks per wave
     {1, 2, 8, 4},   // dec4        64 tiles x 4
     {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
 };
@@ -893,8 +892,8 @@ namespace uc {
 // Layers that run the K-split variant: bit l of LDM_UCONV_KS (read once; default kKsDefault).
 // Round 2, in the loop's chain timing (B = 8): the split form gained 0.4 us on the bottleneck and 0.2 us on enc4
 // and lost 0.9-1.5 us on enc3, dec4 and dec3.  Round 3, with the taps formed from LDS windows, the loop with
-// enc4, the bottleneck and dec4 on the thin variant (kKs2) measured best (82.5 us per iteration against 84.0
-// for the round-2 choice, profiles/r03/ks2).
+// enc4, the bottleneck and dec4 split (enc4 and dec4 on the thin variant kKs2) measured best (79.7-79.9 us per
+// iteration against 84.0 for the round-2 choice, profiles/r03/ks2, profiles/r03/geo).
 constexpr int kKsDefault = (1 << 3) | (1 << 4) | (1 << 5);
 static int ks_mask() {
     static const int m = [] {
@@ -904,7 +903,9 @@ static int ks_mask() {
     return m;
 }
 static bool ks_on(int layer) { return kKs[layer].ks > 1 && ((ks_mask() >> layer) & 1); }
-constexpr int kKs2Default = (1 << 3) | (1 << 4) | (1 << 5);
+// (the bottleneck's variants measured alike: 16 x 32 KS 2 79.7, 16 x 64 KS 4 80.1, 32 x 32 KS 4 79.9 us per
+// iteration, profiles/r03/geo; it keeps variant 1)
+constexpr int kKs2Default = (1 << 3) | (1 << 5);
 static int ks2_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS2");
@@ -916,6 +917,16 @@ static int ks2_mask() {
 static int ks_form(int layer) {
     if (layer < 0 || layer > 8 || !ks_on(layer)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
+}
+// enc2 on 16-row x 64-position tiles (four wave columns sharing each weight fragment through L1): half the weight
+// bytes per block of the 32 x 32 form, measured slower in the loop (81.6 vs 80.1 us per iteration,
+// profiles/r03/geo); LDM_UCONV_ENC2_WIDE=1 (A/B timing)
+static bool enc2_wide(int W) {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_ENC2_WIDE");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    return on && (W / 2) % 16 == 0;
 }
 // enc3 on 16-row tiles (half the weight bytes per block of the 32-row form), each wave one 16-column row of the
 // 4 x 16 output plane so that its taps come from a row window.  Measured in the loop: 80.9 against 80.5 us per
@@ -950,8 +961,8 @@ static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& sl
     const KsGeo& k = form == 2 ? kKs2[layer] : kKs[layer];
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     const int64_t nq = (int64_t)B * (g.mode == 1 ? (Hin / 2) * (Win / 2) : Hin * Win);
-    tiles = (int64_t)(g.cout / (16 * k.tm)) * ((nq + 16 * k.tn - 1) / (16 * k.tn));
-    slab_floats = tiles * k.ks * (g.mode == 2 ? 4 : 1) * k.tm * k.tn * 256;
+    tiles = (int64_t)(g.cout / (16 * k.tm)) * ((nq + 16 * k.tn * k.wn - 1) / (16 * k.tn * k.wn));
+    slab_floats = tiles * k.ks * (g.mode == 2 ? 4 : 1) * k.tm * k.tn * k.wn * 256;
 }
 }  // namespace uc
 
@@ -992,7 +1003,9 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     LayerGeo g = kGeo[layer];
     if (ksv) {
         const KsGeo& k = ksv == 2 ? kKs2[layer] : kKs[layer];
-        g.tm = k.tm, g.tn = k.tn, g.wn = 1, g.wk = k.wk;
+        g.tm = k.tm, g.tn = k.tn, g.wn = k.wn, g.wk = k.wk;
+    } else if (layer == 1 && enc2_wide(W)) {
+        g = LayerGeo{1, 64, 128, 1, 1, 4, 1};   // 16 rows x 4 wave columns of 16 (64 positions), whole K per wave
     } else if (layer == 2 && enc3_thin(W)) {
         g = LayerGeo{1, 128, 256, 1, 1, 2, 2};   // 16 rows x 2 column groups of one row each, K over 2 waves
     }
@@ -1063,8 +1076,8 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 return launch<1, 256, 512, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_POSB, 2>(a, s.dtype, st);
             case 4: LDM_REQUIRE(s.y, "bottleneck: y");
                 if (a.Hin == 2 && a.Win == 8 && pl)
-                    return launch<0, 512, 512, 1, 2, 1, 8, 18, 18, EPI_RELU | EPI_POSB | EPI_PLANE, 2>(a, s.dtype, st);
-                return launch<0, 512, 512, 1, 2, 1, 8, 18, 18, EPI_RELU | EPI_POSB, 2>(a, s.dtype, st);
+                    return launch<0, 512, 512, 1, 2, 2, 4, 18, 18, EPI_RELU | EPI_POSB | EPI_PLANE, 4>(a, s.dtype, st);
+                return launch<0, 512, 512, 1, 2, 2, 4, 18, 18, EPI_RELU | EPI_POSB, 4>(a, s.dtype, st);
             case 5: LDM_REQUIRE(s.y && s.skip, "dec4: y, skip");
                 if (a.Hin == 2 && a.Win == 8 && pl)
                     return launch<2, 512, 256, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_SKIP | EPI_PLANE, 4>(a, s.dtype, st);
@@ -1098,6 +1111,10 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU | EPI_WINDOW>(a, s.dtype, st);
             return launch<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU>(a, s.dtype, st);
         case 1: LDM_REQUIRE(s.y && s.bcast, "enc2: y, t_emb");
+            if (enc2_wide(W)) {
+                if (window_taps()) return launch<1, 64, 128, 1, 1, 4, 1, 36, 36, EPI_RELU | EPI_BCAST | EPI_WINDOW>(a, s.dtype, st);
+                return launch<1, 64, 128, 1, 1, 4, 1, 36, 36, EPI_RELU | EPI_BCAST>(a, s.dtype, st);
+            }
             if (window_taps() && a.Wq % 32 == 0)
                 return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST | EPI_WINDOW>(a, s.dtype, st);
             return launch<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST>(a, s.dtype, st);
