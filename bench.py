@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic_step.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic_step.json"),
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
     a = ap.parse_args()
     if a.batch is None:
@@ -502,7 +502,7 @@ def main():
                 traffic = None
         peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
         if args.dtype != "fp32":
-            traffic = None     # profiles/r02/pmc_traffic_step.json holds the fp32 kernels' counters
+            traffic = None     # profiles/r03/pmc_traffic_step.json holds the fp32 kernels' counters
         result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
                               "achieved": dk["tflops"], "peak": peak, "unit": "TFLOP/s",
                               "frac": round(dk["tflops"] / peak, 4), "traffic": traffic,

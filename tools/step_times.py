@@ -73,7 +73,8 @@ def main():
         sk = torch.randn(B, Hout, Wout, Cout, device=dev)
         y = torch.empty(B, Hout, Wout, Cout, device=dev)
 
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else 0
+        # the split-K forms run with a workspace, as the loop runs them (ldm_step_layer_forms)
+        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else int(lib.ldm_step_workspace_floats(B, H, W))
         ws = torch.zeros(max(nws, 1), device=dev)
 
         def run():
@@ -84,8 +85,8 @@ def main():
                 rc = lib.ldm_ustep_conv(layer, B, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
                                         y.data_ptr(), ws.data_ptr() if nws else None, stp)
             else:
-                rc = lib.ldm_step_conv(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
-                                       y.data_ptr(), stp)
+                rc = lib.ldm_step_conv_ws(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
+                                          y.data_ptr(), 0, ws.data_ptr(), stp)
             assert rc == 0
 
         us = graph_us(run, args.reps)
