@@ -349,6 +349,67 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
     }
 }
 
+// The same for planes of 64..1024 elements (the UNet's latent-scale maps at the train batch): the sliced
+// kernel gives such a plane a whole 256-thread block, with a two-level block reduction for as little as 64
+// elements (8192 blocks, 10-12 us per launch).  Here TP = HW / 4 threads own one plane (one float4 each) and
+// a block holds 256 / TP planes; the plane's sums reduce over its TP lanes (shuffles within the segment, then
+// the plane's waves in order through LDS when TP > 64).  One partial per plane (Q = 1) for the finalize.
+template <int TP>
+__global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const float* __restrict__ dy,
+                                                                  const float* __restrict__ aval, int act, int nplanes,
+                                                                  float* dv, float* __restrict__ part) {
+    constexpr int PPB = kThreads / TP;
+    __shared__ float red[2][kThreads / 64];
+    const int pl = blockIdx.x * PPB + (int)threadIdx.x / TP;
+    const int t = (int)threadIdx.x % TP;
+    float sd = 0.f, sg = 0.f;
+    if (pl < nplanes) {
+        const size_t o = (size_t)pl * (TP * 4) + (size_t)t * 4;
+        float g[4], d[4];
+        ld<4>(dy + o, g);
+        if (aval) {
+            float a[4];
+            ld<4>(aval + o, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = g[j] * act_grad(act, a[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = g[j];
+        }
+        if (dv) st<4>(dv + o, d);
+        sd = ((d[0] + d[1]) + d[2]) + d[3];
+        sg = ((g[0] + g[1]) + g[2]) + g[3];
+    }
+    constexpr int SEG = TP < 64 ? TP : 64;
+#pragma unroll
+    for (int o = SEG / 2; o > 0; o >>= 1) {
+        sd += __shfl_xor(sd, o);
+        sg += __shfl_xor(sg, o);
+    }
+    if constexpr (TP > 64) {   // the plane spans TP / 64 waves: add their sums in wave order
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (lane == 0) {
+            red[0][wave] = sd;
+            red[1][wave] = sg;
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int w0 = wave;   // the plane's first wave
+            sd = red[0][w0];
+            sg = red[1][w0];
+#pragma unroll
+            for (int w = 1; w < TP / 64; ++w) {
+                sd += red[0][w0 + w];
+                sg += red[1][w0 + w];
+            }
+        }
+    }
+    if (part && t == 0 && pl < nplanes) {
+        part[(size_t)pl * 2 + 0] = sd;
+        part[(size_t)pl * 2 + 1] = sg;
+    }
+}
+
 // dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy.  One block per channel: wave w takes
 // the planes b = w, w + 4, ...; its lanes sum a plane's Q slice partials (lane stride, then a shuffle
 // tree), lane 0 keeps the wave's running dbias sum; the four wave sums are added in wave order.  A fixed
@@ -638,6 +699,28 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         return 0;
     }
     LDM_REQUIRE(!sums || workspace, "act_backward: bias / bcast sums need the workspace");
+    if (HW >= 64 && HW <= 1024 && (HW & (HW - 1)) == 0 && act != LDM_ACT_GELU &&
+        vec_ok(HW, dy, aval0, nullptr, act == LDM_ACT_NONE ? nullptr : dv)) {
+        const int nplanes = B * C;
+        float* part = sums ? workspace : nullptr;
+        float* dvp = act == LDM_ACT_NONE ? nullptr : dv;
+        const int tp = HW / 4;
+        const unsigned blocks = (unsigned)((nplanes + kThreads / tp - 1) / (kThreads / tp));
+        hipStream_t st = (hipStream_t)stream;
+        switch (tp) {
+            case 16: hipLaunchKernelGGL(act_bwd_planes_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
+            case 32: hipLaunchKernelGGL(act_bwd_planes_kernel<32>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
+            case 64: hipLaunchKernelGGL(act_bwd_planes_kernel<64>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
+            case 128: hipLaunchKernelGGL(act_bwd_planes_kernel<128>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
+            default: hipLaunchKernelGGL(act_bwd_planes_kernel<256>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
+        }
+        LDM_CHECK_LAUNCH("act_bwd_planes_kernel");
+        if (sums) {
+            hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, dbias, dbcast);
+            LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
+        }
+        return 0;
+    }
     const int Q = act_slices(B, C, HW);
     const int64_t S = ((HW + Q - 1) / Q + 3) & ~3;
     const dim3 grid(Q, B * C);

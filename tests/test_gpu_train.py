@@ -591,11 +591,13 @@ def test_wgrad_tap_shared(cuda, case):
     assert rel_err(npy(acc), wt.grad.numpy() + 1.0) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(32, 128, 1, 1), (32, 512, 2, 8), (3, 8, 36, 36), (2, 64, 5, 5)])
+@pytest.mark.parametrize("shape", [(32, 128, 1, 1), (32, 512, 2, 8), (3, 8, 36, 36), (2, 64, 5, 5),
+                                   (4, 96, 8, 8), (5, 24, 8, 16), (3, 40, 16, 16), (2, 8, 16, 32), (2, 16, 16, 64)])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu"])
 def test_act_backward_sums(cuda, shape, act):
-    """ldm_act_backward (dv, dbias, dbcast) against fp64 on the small-plane kernel (HW <= 16) and the
-    sliced one (scalar and float4 paths)."""
+    """ldm_act_backward (dv, dbias, dbcast) against fp64 on the small-plane kernel (HW <= 16), the multi-plane
+    kernel (HW = 64..1024, powers of two: 16-256 threads per plane) and the sliced one (scalar and float4
+    paths)."""
     from ldm_amd import ops
     B, C = shape[0], shape[1]
     v = torch.from_numpy(_rand(shape, 31, -2, 2)).double()
