@@ -918,6 +918,16 @@ static int ks_form(int layer) {
     if (layer < 0 || layer > 8 || !ks_on(layer)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
 }
+// dec1 on 16-row x 64-position tiles: half of the 32 output channels per block, so a block streams half of the
+// layer's weights (every block streams all of them in the 32-row form): loop 81.2 -> 80.7 us per iteration
+// (profiles/r03/dec1_thin); LDM_UCONV_DEC1_THIN=0 keeps the 32-row form
+static bool dec1_thin(int W) {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_DEC1_THIN");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on && W % 32 == 0;
+}
 // enc2 on 16-row x 64-position tiles (four wave columns sharing each weight fragment through L1): half the weight
 // bytes per block of the 32 x 32 form, measured slower in the loop (81.6 vs 80.1 us per iteration,
 // profiles/r03/geo); LDM_UCONV_ENC2_WIDE=1 (A/B timing)
@@ -1004,6 +1014,8 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     if (ksv) {
         const KsGeo& k = ksv == 2 ? kKs2[layer] : kKs[layer];
         g.tm = k.tm, g.tn = k.tn, g.wn = k.wn, g.wk = k.wk;
+    } else if (layer == 8 && dec1_thin(W)) {
+        g = LayerGeo{0, 64, 32, 1, 2, 2, 2};   // 16 of the 32 rows x 64 positions (2 wave columns), K over 2 waves
     } else if (layer == 1 && enc2_wide(W)) {
         g = LayerGeo{1, 64, 128, 1, 1, 4, 1};   // 16 rows x 4 wave columns of 16 (64 positions), whole K per wave
     } else if (layer == 2 && enc3_thin(W)) {
@@ -1138,6 +1150,10 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP | EPI_WINDOW>(a, s.dtype, st);
             return launch<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP>(a, s.dtype, st);
         default: LDM_REQUIRE(s.xs && s.coef, "dec1: sampler state, coefficients");
+            if (dec1_thin(W)) {
+                if (window_taps()) return launch<0, 64, 32, 1, 2, 2, 2, 18, 18, EPI_DDIM | EPI_WINDOW>(a, s.dtype, st);
+                return launch<0, 64, 32, 1, 2, 2, 2, 18, 18, EPI_DDIM>(a, s.dtype, st);
+            }
             if (window_taps() && a.Wq % 32 == 0)   // a block's 32 columns lie in one row
                 return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM | EPI_WINDOW>(a, s.dtype, st);
             return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, s.dtype, st);
