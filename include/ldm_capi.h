@@ -334,7 +334,8 @@ int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const f
 /* Layer pairs of the reverse loop (ldm_ddim_sample with use_step): bit l of `mask` runs layers l and l + 1
  * as ONE launch whose first blocks compute layer l and hand their output tiles to layer l + 1's blocks
  * inside the launch (write-through stores, a sharded arrival count; the consumer blocks stream their
- * weights before they wait).  Pairs start at l = 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1);
+ * weights before they wait).  Pairs start at l = 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1, with
+ * LDM_UCONV_DEC1_THIN=0 only);
  * other bits are ignored.  Takes effect for loops issued (or graphs captured) afterwards; returns the
  * previous mask.  A negative mask only reads it.  Default: LDM_UPAIR, else the measured choice. */
 int32_t ldm_step_set_pairs(int32_t mask);

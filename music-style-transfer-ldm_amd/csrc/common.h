@@ -221,7 +221,7 @@ int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats = nullptr);
 int step_ks_mask();   // layers running the K-split step form (LDM_UCONV_KS)
 // Two consecutive step layers in one launch with an in-launch hand-off (uconv.hip upair_kernel); pairs start
 // at layer 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1).
-bool step_pair_supported(int la);
+bool step_pair_supported(int la, int W);
 int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& sb, hipStream_t st);
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
 // ustep.hip: the LDS-staged step kernels at the canonical latent (16 x 64, batch a multiple of 4)

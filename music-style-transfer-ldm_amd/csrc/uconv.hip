@@ -1187,14 +1187,15 @@ static int pair_dt(int la, const UArgs& a, const UArgs& b, int32_t* cnt, hipStre
 }
 }  // namespace uc
 
-bool step_pair_supported(int la) { return la == 0 || la == 6 || la == 7; }
+// (dec1's pair instance is its 32-row form: not while dec1 runs on 16-row tiles)
+bool step_pair_supported(int la, int W) { return la == 0 || la == 6 || (la == 7 && !uc::dec1_thin(W)); }
 
 // Layers la and la + 1 in one launch (uc::upair_kernel): la's blocks hand their output to la + 1's blocks
 // inside the launch.  sa.ws: the step workspace (its tail holds the pair counters).  A dec3 producer runs its
 // K-split form (the single-block form needs more than the 256 registers a shared CU leaves it).
 int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& sb, hipStream_t st) {
     using namespace uc;
-    LDM_REQUIRE(step_pair_supported(la) && sa.ws && sa.dtype == sb.dtype, "step pair: unsupported layer pair");
+    LDM_REQUIRE(step_pair_supported(la, W) && sa.ws && sa.dtype == sb.dtype, "step pair: unsupported layer pair");
     UArgs a, b;
     UC_TRY(make_args(la, B, H, W, sa, la == 6 ? 1 : 0, a));
     UC_TRY(make_args(la + 1, B, H, W, sb, 0, b));

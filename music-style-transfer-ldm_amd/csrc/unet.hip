@@ -344,7 +344,7 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     const int pairs = step_pair_mask();
     auto run = [&](int l0, int l1) -> int {   // layers [l0, l1], pairs where enabled
         for (int l = l0; l <= l1; ++l) {
-            if (l < l1 && ((pairs >> l) & 1) && step_pair_supported(l) && ws.uks) {
+            if (l < l1 && ((pairs >> l) & 1) && step_pair_supported(l, s.W) && ws.uks) {
                 LDM_TRY(step_pair(l, s.B, s.H, s.W, c[l], c[l + 1], st));
                 ++l;
                 continue;

@@ -488,6 +488,19 @@ def test_autoencoder_step_matches_reference(goldens2, cuda):
             continue
         assert adam_step_err(npy(named[k]), goldens2["ae_adamw1_" + k], goldens2["ae_grad_" + k], 5e-4,
                              rel=2e-3, grad=adam_grads[k]) < 1e-5, k
+    # ... and, element by element including the below-noise ones, the update is exactly AdamW's first step
+    # on OUR gradient (float64 restatement of torch.optim.AdamW: decoupled decay, bias-corrected moments):
+    # a sign or bias-correction error anywhere fails here whatever the gradient noise
+    grp = opt.param_groups[0]
+    lr, (b1, b2), eps, wd = grp["lr"], grp["betas"], grp["eps"], grp["weight_decay"]
+    for k in AE_KEYS:
+        g = adam_grads[k].astype(np.float64)
+        p0 = w0[k].astype(np.float64)
+        m_hat = ((1 - b1) * g) / (1 - b1)
+        v_hat = ((1 - b2) * g * g) / (1 - b2)
+        want = p0 * (1 - lr * wd) - lr * m_hat / (np.sqrt(v_hat) + eps)
+        err = np.abs(npy(named[k]) - want).max()
+        assert err <= 1e-6 * (np.abs(p0).max() + lr), (k, err)
     assert rel_err(npy(enc.encoder[4].running_mean), goldens2["ae_enc_rm4"]) < TOL
     assert rel_err(npy(dec.decoder[1].running_var), goldens2["ae_dec_rv1"]) < TOL
 
