@@ -380,10 +380,10 @@ __global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __
 __global__ __launch_bounds__(256) void attention_fold_keys_kernel(const float* __restrict__ kv, const float* __restrict__ wq,
                                                                   const float* __restrict__ bq, int B, int E, int heads,
                                                                   int S, float scale, float* __restrict__ kf,
-                                                                  float* __restrict__ bf) {
+                                                                  float* __restrict__ bf, int64_t first) {
     const int d = E / heads;
     const int64_t nk = (int64_t)B * heads * E * S;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t idx = first + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // first = nk: bf only
     if (idx < nk) {   // kf [B,heads,S,E]: e fastest (the attention reads 16-byte runs along E)
         const int e = (int)(idx % E);
         int64_t r = idx / E;
@@ -418,6 +418,66 @@ __global__ __launch_bounds__(256) void attention_fold_keys_kernel(const float* _
         for (int c = 0; c < d; ++c) acc += (double)bq[h * d + c] * (double)kr[(int64_t)c * S];
         bf[j] = (float)(acc * (double)scale);
     }
+}
+
+// The same folded keys, four key positions per thread (S % 4 == 0): each Wq element loaded once feeds four
+// fp64 sums (the one-output-per-thread form re-reads Wq once per key position: 268 MB of L1/L2 traffic for
+// CA2 at B = 8), the four K values of a channel are one 16-byte broadcast load, and 16 channels' loads are
+// in flight per step.  Each sum runs serially in c as in attention_fold_keys_kernel: the same roundings.
+__global__ __launch_bounds__(256) void attention_fold_keys4_kernel(const float* __restrict__ kv, const float* __restrict__ wq,
+                                                                   const float* __restrict__ bq, int B, int E, int heads,
+                                                                   int S, float scale, float* __restrict__ kf,
+                                                                   float* __restrict__ bf) {
+    // column e == E of the (b, h, key group) row is the bias fold bf (w = bq instead of a Wq column)
+    const int d = E / heads;
+    const int SG = S / 4;
+    const int64_t n = (int64_t)B * heads * SG * (E + 1);
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const int e = (int)(idx % (E + 1));
+    int64_t r = idx / (E + 1);
+    const int sg = (int)(r % SG);
+    r /= SG;
+    const int h = (int)(r % heads), b = (int)(r / heads);
+    const float* kr = kv + ((int64_t)b * 2 * E + (int64_t)h * d) * S + sg * 4;
+    const bool isb = e == E;
+    const float* wr = isb ? bq + h * d : wq + (int64_t)h * d * E + e;
+    const int64_t ws = isb ? 1 : E;
+    double acc[4] = {0., 0., 0., 0.};
+    int c = 0;
+    for (; c + 16 <= d; c += 16) {
+        float wv[16];
+        float4 kq[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            wv[u] = wr[(int64_t)(c + u) * ws];
+            kq[u] = *reinterpret_cast<const float4*>(kr + (int64_t)(c + u) * S);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const double w = (double)wv[u];
+            acc[0] += w * (double)kq[u].x;
+            acc[1] += w * (double)kq[u].y;
+            acc[2] += w * (double)kq[u].z;
+            acc[3] += w * (double)kq[u].w;
+        }
+    }
+    for (; c < d; ++c) {
+        const double w = (double)wr[(int64_t)c * ws];
+        const float4 k = *reinterpret_cast<const float4*>(kr + (int64_t)c * S);
+        acc[0] += w * (double)k.x;
+        acc[1] += w * (double)k.y;
+        acc[2] += w * (double)k.z;
+        acc[3] += w * (double)k.w;
+    }
+    if (isb) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[((int64_t)b * heads + h) * S + sg * 4 + j] = (float)(acc[j] * (double)scale);
+        return;
+    }
+    float* out = kf + (((int64_t)b * heads + h) * S + sg * 4) * E + e;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[(int64_t)j * E] = (float)(acc[j] * (double)scale);
 }
 
 // W'[co, ci, t] = sum_j Wc[co, j, t] Wp[j, ci]  (conv after a Linear/1x1 projection, composed), and the
@@ -680,9 +740,22 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
 int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
                         int32_t S, float scale, float* kf, float* bf, hipStream_t st) {
     LDM_REQUIRE(kv && wq && bq && kf && bf && B > 0 && heads > 0 && E % heads == 0 && S > 0, "fold keys: bad argument");
-    const int64_t n = (int64_t)B * heads * E * S + (int64_t)B * heads * S;
+    const int64_t nk = (int64_t)B * heads * E * S, nb = (int64_t)B * heads * S;
+    static const bool k4_on = [] {   // LDM_FOLD_KEYS4=0: the one-output-per-thread kernel only (A/B timing)
+        const char* e = std::getenv("LDM_FOLD_KEYS4");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    const bool k4 = k4_on && S % 4 == 0 && ((uintptr_t)kv & 15) == 0;
+    if (k4) {   // keys and bias in one launch
+        const int64_t n4 = (int64_t)B * heads * (S / 4) * (E + 1);
+        hipLaunchKernelGGL(attention_fold_keys4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, kv, wq, bq,
+                           B, E, heads, S, scale, kf, bf);
+        LDM_CHECK_LAUNCH("attention_fold_keys4_kernel");
+        return 0;
+    }
+    const int64_t first = 0, n = nk + nb - first;
     hipLaunchKernelGGL(attention_fold_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, kv, wq, bq, B,
-                       E, heads, S, scale, kf, bf);
+                       E, heads, S, scale, kf, bf, first);
     LDM_CHECK_LAUNCH("attention_fold_keys_kernel");
     return 0;
 }

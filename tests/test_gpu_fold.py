@@ -1,7 +1,8 @@
 """The reverse loop's folded cross-attention, kernel by kernel (csrc/misc.hip).
 
 ldm_attention_fold_keys: kf [B,heads,S,E] = scale * Wq_h^T K_h and bf [B,heads,S] = scale * bq_h^T K_h (fp64
-sums, one rounding), at the reverse loop's key counts and two others; ldm_attention_folded: z [B,L,E] -> softmax((Wq z + bq) * scale)^T K) V, token-major, against float64
+sums, one rounding), at the reverse loop's key counts and others (S % 4 == 0: four keys per thread with the
+bias as an extra column; S = 10: the one-output-per-thread kernel); ldm_attention_folded: z [B,L,E] -> softmax((Wq z + bq) * scale)^T K) V, token-major, against float64
 torch of the unfolded attention (model.py:140-153, nn.MultiheadAttention's Q in-projection + score product).
 """
 import numpy as np
@@ -17,7 +18,7 @@ def npy(t):
     return t.detach().double().cpu().numpy()
 
 
-@pytest.mark.parametrize("B,E,S", [(8, 256, 64), (8, 512, 16), (2, 256, 12), (3, 512, 40)])
+@pytest.mark.parametrize("B,E,S", [(8, 256, 64), (8, 512, 16), (2, 256, 12), (3, 512, 40), (2, 256, 10)])
 def test_fold_keys_vs_float64(cuda, B, E, S):
     from ldm_amd import _lib as L
     heads, d = 4, E // 4

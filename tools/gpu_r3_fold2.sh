@@ -9,3 +9,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/tools/pair_times.py 0 > $GRAFT_REPO_ROOT/$O/prof.log 2>&1 || { echo "rocprof failed"; tail $GRAFT_REPO_ROOT/$O/prof.log; exit 1; }
 grep -h "fold_keys" $GRAFT_REPO_ROOT/$O/prof/*kernel_stats.csv | cut -c1-200
 cd $GRAFT_REPO_ROOT && timeout -k 10 120 python -u tools/pair_times.py 0 > $O/loop.txt 2>&1 && echo "loop: $(grep pairs $O/loop.txt)"
+for k in 1 0 1 0; do LDM_FOLD_KEYS4=$k timeout -k 10 120 python -u tools/pair_times.py 0 > $O/loop_k4_$k.txt 2>&1 || exit 1; echo "keys4 $k: $(grep pairs $O/loop_k4_$k.txt)"; done
