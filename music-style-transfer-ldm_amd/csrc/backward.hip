@@ -109,8 +109,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     const int per = (S + G - 1) / G;
     float v = 0.f;
     if (i < MN) {
+        // eight splits' loads in flight per step, summed in split order (same roundings as one at a time)
         const int s1 = min(S, (g + 1) * per);
-        for (int s = g * per; s < s1; ++s) v = v + partial[(size_t)s * MN + i];
+        int s = g * per;
+        for (; s + 8 <= s1; s += 8) {
+            float p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = partial[(size_t)(s + u) * MN + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v = v + p[u];
+        }
+        for (; s < s1; ++s) v = v + partial[(size_t)s * MN + i];
     }
     if (G > 1) {
         red[threadIdx.x] = v;

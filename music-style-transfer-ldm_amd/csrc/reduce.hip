@@ -410,32 +410,40 @@ __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const float* _
     }
 }
 
-// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy.  One block per channel: wave w takes
-// the planes b = w, w + 4, ...; its lanes sum a plane's Q slice partials (lane stride, then a shuffle
-// tree), lane 0 keeps the wave's running dbias sum; the four wave sums are added in wave order.  A fixed
-// partition and order, so bitwise reproducible (a single thread walking B*Q partials serially took
-// 150 us for the decoder's one-channel output layer at B = 32).
+// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy.  One block per channel: a plane's Q slice
+// partials go to QP lanes (QP = Q rounded up to a power of two, at most 64; lane stride past 64), so a wave
+// takes 64 / QP planes per step (wave w the planes from w * 64 / QP on, stepping by 256 / QP) and sums each
+// plane by a segmented shuffle tree; the plane sums meet in a full-wave tree, the four wave sums in wave
+// order.  A fixed partition and order, so bitwise reproducible (a single thread walking B*Q partials
+// serially took 150 us for the decoder's one-channel output layer at B = 32; one plane per wave step left
+// the Q = 1 finalize of the plane kernels at 8 serial load round trips per wave).
 __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float* __restrict__ part, int B, int C,
-                                                                    int Q, float* __restrict__ dbias,
+                                                                    int Q, int QP, float* __restrict__ dbias,
                                                                     float* __restrict__ dbcast) {
     __shared__ float wsum[kThreads / 64];
     const int c = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ppw = 64 / QP, sub = lane / QP, k0 = lane % QP;
     float sb = 0.f;
-    for (int b = wave; b < B; b += kThreads / 64) {
+    for (int b0 = wave * ppw; b0 < B; b0 += (kThreads / 64) * ppw) {
+        const int b = b0 + sub;
         const size_t pl = (size_t)b * C + c;
         float sd = 0.f, sg = 0.f;
-        for (int k = lane; k < Q; k += 64) {
-            sd += part[(pl * Q + k) * 2 + 0];
-            sg += part[(pl * Q + k) * 2 + 1];
-        }
-        for (int o = 32; o > 0; o >>= 1) {
+        if (b < B)
+            for (int k = k0; k < Q; k += QP) {
+                sd += part[(pl * Q + k) * 2 + 0];
+                sg += part[(pl * Q + k) * 2 + 1];
+            }
+        for (int o = QP / 2; o > 0; o >>= 1) {
             sd += __shfl_xor(sd, o);
             sg += __shfl_xor(sg, o);
         }
-        sb += sd;
-        if (dbcast && lane == 0) dbcast[pl] = sg;
+        if (k0 == 0 && b < B) {
+            sb += sd;
+            if (dbcast) dbcast[pl] = sg;
+        }
     }
+    for (int o = 32; o > 0; o >>= 1) sb += __shfl_xor(sb, o);
     if (lane == 0) wsum[wave] = sb;
     __syncthreads();
     if (threadIdx.x == 0 && dbias) {
@@ -443,6 +451,11 @@ __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float*
         for (int w = 0; w < kThreads / 64; ++w) s += wsum[w];
         dbias[c] = s;
     }
+}
+static int finalize_lanes(int Q) {
+    int qp = 1;
+    while (qp < Q && qp < 64) qp *= 2;
+    return qp;
 }
 
 // Small planes (HW <= 16: the Linear layers, HW = 1, and the 2x8 projections): one block per channel
@@ -716,7 +729,7 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         }
         LDM_CHECK_LAUNCH("act_bwd_planes_kernel");
         if (sums) {
-            hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, dbias, dbcast);
+            hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, 1, dbias, dbcast);
             LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
         }
         return 0;
@@ -735,7 +748,7 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
     LDM_CHECK_LAUNCH("act_bwd_kernel");
     if (sums) {
         hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, (hipStream_t)stream, part, B, C, Q,
-                           dbias, dbcast);
+                           finalize_lanes(Q), dbias, dbcast);
         LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
     }
     return 0;

@@ -605,7 +605,8 @@ def test_wgrad_tap_shared(cuda, case):
 
 
 @pytest.mark.parametrize("shape", [(32, 128, 1, 1), (32, 512, 2, 8), (3, 8, 36, 36), (2, 64, 5, 5),
-                                   (4, 96, 8, 8), (5, 24, 8, 16), (3, 40, 16, 16), (2, 8, 16, 32), (2, 16, 16, 64)])
+                                   (4, 96, 8, 8), (5, 24, 8, 16), (3, 40, 16, 16), (2, 8, 16, 32), (2, 16, 16, 64),
+                                   (70, 4, 8, 8), (300, 2, 4, 16), (40, 3, 40, 40)])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu"])
 def test_act_backward_sums(cuda, shape, act):
     """ldm_act_backward (dv, dbias, dbcast) against fp64 on the small-plane kernel (HW <= 16), the multi-plane
