@@ -1158,6 +1158,103 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
         }
 }
 
+// The same tiles with the input channels split over the block's four waves (Cin % 8 == 0): wave g sums the
+// quarter g * Cin / 4 .. of the channels for the 64 tiles of its block, then the quarters meet in LDS in wave
+// order.  At B = 32 the two-rows-per-lane kernel has 65,536 lanes, one 4-wave block per CU walking all 64
+// channels in a chain of dependent loads (119 us per launch); here 4x the waves walk a quarter each.
+__global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
+    __shared__ float part[3][32][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int W4 = a.Win >> 2, H2 = a.Hin >> 1;
+    const int idx = (int)(blockIdx.x * 64 + lane);
+    const bool valid = idx < a.B * H2 * W4;
+    const int id = valid ? idx : 0;
+    const int r = a.fd_dwo.div(id);   // fd_dwo = W4
+    const int qx0 = (id - r * W4) * 4;
+    const int b = a.fd_dho.div(r);     // fd_dho = Hin / 2
+    const int qy0 = (r - b * H2) * 2;
+    const int HW = a.Hin * a.Win;
+    const int cq = a.Cin >> 2, c0 = g * cq;
+    float acc[2][2][8];   // [input row][ry][2 jj + rx]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[u][i][j] = 0.f;
+    bool rok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rok[i] = valid && (unsigned)(qy0 - 1 + i) < (unsigned)a.Hin;
+    const bool lok = qx0 > 0, hok = qx0 + 4 < a.Win;
+    const float* xp = a.x + ((size_t)b * a.Cin + c0) * HW + (qy0 - 1) * a.Win + qx0;
+    auto load = [&](const float* p, float (&xr)[4][6]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float* row = p + i * a.Win;
+            const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
+            xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
+            xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+        }
+    };
+    auto mac = [&](const float (&xr)[4][6], const float* wq) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+                for (int rx = 0; rx < 2; ++rx)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int ia = t >> 1, ib = t & 1;
+                        const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
+                        const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
+                    }
+    };
+    float xa[4][6], xb[4][6];
+    for (int ci = c0; ci < c0 + cq; ci += 2, xp += 2 * HW) {   // cq even; channel order kept within the quarter
+        load(xp, xa);
+        load(xp + HW, xb);
+        mac(xa, a.w + ci * 16);
+        mac(xb, a.w + (ci + 1) * 16);
+    }
+    if (g > 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) part[g - 1][u * 16 + i * 8 + j][lane] = acc[u][i][j];
+    }
+    __syncthreads();
+    if (g > 0 || !valid) return;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[u][i][j] = acc[u][i][j] + part[q][u * 16 + i * 8 + j][lane];
+    const ChanEpi ce = chan_epi(a, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry) {
+            const size_t o = ((size_t)b * a.Hout + 2 * (qy0 + u) + ry) * a.Wout + 2 * qx0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[u][ry][4 * h + j]);
+                store4(a, o + 4 * h, v);
+            }
+        }
+}
+
 // ------------------------------------------------------------------------------------------------
 // weight packing into fragment order: packed[phase][chunk][Mpad][NLG][4], k = chunk*CK + NLG*j + lg
 // ------------------------------------------------------------------------------------------------
@@ -1505,6 +1602,17 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             d.out_pad == 0 && d.Win % 4 == 0 && a.pt.nphase == 4 && ((uintptr_t)y & 15) == 0 &&
             (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Win / 4);
+            static const bool split = [] {   // LDM_CT4_SPLIT=0: the unsplit channel walk (A/B timing)
+                const char* e = std::getenv("LDM_CT4_SPLIT");
+                return !e || std::atoi(e) != 0;
+            }();
+            if (d.Hin % 2 == 0 && d.Cin % 8 == 0 && split) {
+                a.fd_dho = FastDiv::make(d.Hin / 2);
+                const int64_t tiles = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
+                hipLaunchKernelGGL(convT4_cout1_r2s_kernel, dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0, st, a);
+                LDM_CHECK_LAUNCH("convT4_cout1_r2s_kernel");
+                return 0;
+            }
             if (d.Hin % 2 == 0) {
                 a.fd_dho = FastDiv::make(d.Hin / 2);
                 const int64_t lanes = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);

@@ -88,3 +88,25 @@ def test_tiled_plan_classes(cuda):
     assert ops.tiled_plan(ops.make_desc(8, 256, 4, 16, 512, 3, 3, 2, 1), 2) is None        # UNet-sized: general
     assert ops.tiled_plan(ops.make_desc(32, 1, 128, 512, 64, 3, 3, 2, 1), 2) is None      # Cin = 1: x4 kernel
     assert ops.tiled_plan(ops.make_desc(32, 48, 64, 64, 64, 3, 3, 1, 1), 2) is None       # Cin % 32 != 0
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 256), (3, 64, 8, 16), (5, 8, 6, 12), (2, 12, 6, 8), (2, 16, 5, 8)])
+@pytest.mark.parametrize("act", ["none", "tanh"])
+def test_convT_cout1(cuda, shape, act):
+    """The decoder's 64 -> 1 output convT (k4 s2 p1; model.py:44) on its own kernels (conv.hip): channel
+    quarters over a block's four waves (Cin % 8 == 0, Hin even), two input rows per lane (other even Hin),
+    one row (odd Hin).  fp32 against float64 torch, 1e-5 of max |y|, run-to-run bitwise."""
+    from ldm_amd import ops
+    B, Cin, H, W = shape
+    seed = B * 1000 + Cin * 10 + H
+    x = _rand((B, Cin, H, W), seed)
+    w = _rand((Cin, 1, 4, 4), seed + 1, -0.2, 0.2)
+    b = _rand((1,), seed + 2, -0.1, 0.1)
+    v = tF.conv_transpose2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    ref = torch.tanh(v) if act == "tanh" else v
+    y = ops.conv_forward(x.to(cuda), w.to(cuda), b.to(cuda), stride=2, padding=1, transposed=True, act=act)
+    y2 = ops.conv_forward(x.to(cuda), w.to(cuda), b.to(cuda), stride=2, padding=1, transposed=True, act=act)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape
+    assert rel_err(y.double().cpu().numpy(), ref.numpy()) < 1e-5
+    assert torch.equal(y, y2)
