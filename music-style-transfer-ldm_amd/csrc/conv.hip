@@ -1214,12 +1214,22 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
                     }
     };
-    float xa[4][6], xb[4][6];
-    for (int ci = c0; ci < c0 + cq; ci += 2, xp += 2 * HW) {   // cq even; channel order kept within the quarter
-        load(xp, xa);
-        load(xp + HW, xb);
+    // cq even; channel order kept within the quarter; the next channel pair's loads are issued before the
+    // current pair's FMAs (the last pass re-loads the final pair: a harmless L2 hit)
+    float xa[4][6], xb[4][6], na[4][6], nb[4][6];
+    load(xp, xa);
+    load(xp + HW, xb);
+    for (int ci = c0; ci < c0 + cq; ci += 2) {
+        const float* np = ci + 2 < c0 + cq ? xp + 2 * HW : xp;
+        load(np, na);
+        load(np + HW, nb);
         mac(xa, a.w + ci * 16);
         mac(xb, a.w + (ci + 1) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) xa[i][c] = na[i][c], xb[i][c] = nb[i][c];
+        xp = np;
     }
     if (g > 0) {
 #pragma unroll
