@@ -88,7 +88,8 @@ def _graph_time_us(fn, reps):
         fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    from ldm_amd.graphs import capture
+    with capture(g):
         for _ in range(reps):
             fn()
     g.replay()
@@ -305,7 +306,8 @@ TRAIN_GFLOP_PER_SAMPLE = 10.7   # frozen VAE enc fwd 0.698 + 3
 def run_train(args, world, rank, dev, M):
     """Configs 3/4: LDMTrainer.train_step (reference train.py:163-208) = VAE encode -> style encode ->
     q_sample -> UNet -> predict_start -> VAE decode -> losses -> backward -> (RCCL bucketed grad
-    all-reduce when N>1) -> GradScaler + Adam.  Eager (the step ends in the reference's .item() syncs).
+    all-reduce when N>1) -> GradScaler + Adam, replayed from one hipGraph (LDMTrainer.graph_step; the RCCL
+    all-reduces and SyncBN's statistic all-reduces are graph nodes when N > 1; --train-eager for the eager step).
     value = samples/s over all ranks; weak scaling (batch per GPU fixed)."""
     import torch.distributed as dist
     from models.train import LDMTrainer
@@ -316,8 +318,8 @@ def run_train(args, world, rank, dev, M):
         hdist.broadcast_parameters(ldm)
     trainer = LDMTrainer(ldm, None, dev, lr=1e-4)                 # LDMTrainer default (train.py:142)
     trainer.autocast_dtype = {"fp32": None, "fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
-    # one rank: the whole step replayed from a hipGraph (LDMTrainer.graph_step; warm-up covers the 2 eager
-    # steps and the capture); with N > 1 the bucketed RCCL all-reduce keeps the step eager
+    # the whole step replayed from a hipGraph (LDMTrainer.graph_step; warm-up covers the 2 eager steps and the
+    # capture); with N > 1 the capture holds the bucketed RCCL gradient all-reduces and SyncBN's collectives
     trainer.graph_step = not args.train_eager
     if args.dtype == "fp32":
         os.environ["LDM_AMD_DTYPE"] = "fp32"                      # autocast region present, fp32 operands

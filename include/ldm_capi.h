@@ -322,6 +322,9 @@ int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x
  * floats, zero-filled once (its counters return to zero after every launch); launches on one stream may
  * share it.  ldm_step_conv / ldm_step_conv_dt run the single-block form. */
 int64_t ldm_step_workspace_floats(int32_t B, int32_t H, int32_t W);
+/* The leading part of that workspace that holds the split-K tile counters (one int32 per tile of the layer with
+ * the most tiles, rounded up to 64): zero between launches, like the 64 layer-pair counters at its end. */
+int64_t ldm_step_workspace_counter_floats(int32_t B, int32_t H, int32_t W);
 int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                      const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype,
                      float* workspace, void* stream);
@@ -331,6 +334,11 @@ int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float
 int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const float* packed, const float* bias,
                        const float* coef, float eta, float* xs, float* x0_log, float* eps_log, int32_t dtype,
                        void* stream);
+/* 1 when this library is the diagnostic build (make DIAG=1: lib/libldm_amd_diag.so), which adds the reverse-loop
+ * forms measured and not kept: the layer pairs below and the LDS-staged ustep.hip kernels.  In the shipped
+ * build (0) ldm_step_set_pairs only records the mask (no pair runs) and the ldm_ustep_* entry points report
+ * that they are absent (-1 / an error code). */
+int32_t ldm_step_diag_build(void);
 /* Layer pairs of the reverse loop (ldm_ddim_sample with use_step): bit l of `mask` runs layers l and l + 1
  * as ONE launch whose first blocks compute layer l and hand their output tiles to layer l + 1's blocks
  * inside the launch (write-through stores, a sharded arrival count; the consumer blocks stream their

@@ -219,6 +219,12 @@ struct StepConv {
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
 int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats = nullptr);
 int step_ks_mask();   // layers running the K-split step form (LDM_UCONV_KS)
+// LDM_STEP_DIAG (make DIAG=1, lib/libldm_amd_diag.so): the reverse-loop forms measured and not kept — the
+// LDS-staged step kernels (ustep.hip) and the in-launch layer pairs (uconv.hip upair_kernel).  The shipped
+// library reports them unsupported.
+#ifndef LDM_STEP_DIAG
+#define LDM_STEP_DIAG 0
+#endif
 // Two consecutive step layers in one launch with an in-launch hand-off (uconv.hip upair_kernel); pairs start
 // at layer 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1).
 bool step_pair_supported(int la, int W);

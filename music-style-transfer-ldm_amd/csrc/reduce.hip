@@ -712,11 +712,11 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         return 0;
     }
     LDM_REQUIRE(!sums || workspace, "act_backward: bias / bcast sums need the workspace");
-    if (HW >= 64 && HW <= 1024 && (HW & (HW - 1)) == 0 && act != LDM_ACT_GELU &&
-        vec_ok(HW, dy, aval0, nullptr, act == LDM_ACT_NONE ? nullptr : dv)) {
+    // act none: dv = dy, so the write is dropped only when dv IS dy (a separate dv buffer is still written)
+    float* dvp = act == LDM_ACT_NONE && dv == dy ? nullptr : dv;
+    if (HW >= 64 && HW <= 1024 && (HW & (HW - 1)) == 0 && act != LDM_ACT_GELU && vec_ok(HW, dy, aval0, nullptr, dvp)) {
         const int nplanes = B * C;
         float* part = sums ? workspace : nullptr;
-        float* dvp = act == LDM_ACT_NONE ? nullptr : dv;
         const int tp = HW / 4;
         const unsigned blocks = (unsigned)((nplanes + kThreads / tp - 1) / (kThreads / tp));
         hipStream_t st = (hipStream_t)stream;

@@ -237,6 +237,9 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 for (int ni = 0; ni < TN; ++ni) acc[u][p][mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     constexpr int XAUX = ROLE == ROLE_CONSUMER ? 16 : UCONV_XAUX;   // 16: sc1 (the producer's stores are sc1)
+    // a consumer whose wait passed its bound writes NaN, so that a pair launch can never return plausible but
+    // wrong activations (the sticky word cnt[9] records it as well)
+    [[maybe_unused]] int poison = 0;
     AT fa[NST > 1 ? 2 : 1][S][TM];
     floatx4 fb[NST > 1 ? 2 : 1][S][TN];
     // PART bit 0: weight (A) fragments, bit 1: activation (B) fragments
@@ -557,14 +560,15 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
         epi_prefetch();
         __builtin_amdgcn_sched_barrier(0);
         if (threadIdx.x == 0) {
-            int spins = 0;
+            int spins = 0, timed_out = 0;
             for (;;) {
                 int s = 0;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) s += __hip_atomic_load(ps.cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (s >= ps.target) break;
-                if (++spins > (1 << 18)) {   // bounded: report instead of hanging
+                if (++spins > (1 << 18)) {   // bounded: report instead of hanging, and poison this block's output
                     __hip_atomic_store(ps.cnt + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    timed_out = 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -573,8 +577,11 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
 #pragma unroll
                 for (int i = 0; i < 9; ++i) __hip_atomic_store(ps.cnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            reinterpret_cast<int*>(smem)[0] = timed_out;   // (a consumer holds no LDS window: smem is free here)
         }
         __syncthreads();
+        poison = reinterpret_cast<const int*>(smem)[0];
+        __syncthreads();   // read before the K reduction or the split-K flag reuse smem
         load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
     } else {
         load_stage(std::integral_constant<int, 0>{}, AB{});
@@ -640,6 +647,12 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vv[k]),
                                                        sr, slab_off(ks, f), 0, 16);
         });
+        // Ordering of the hand-off: the partial tile is stored write-through (sc1) and drained (vmcnt(0)) before
+        // the block's barrier, and thread 0 counts the block only after that barrier; the last arriver reads the
+        // other partials with sc1 loads after its own barrier, whose workgroup-scope acquire keeps the compiler
+        // from hoisting them above the counter.  An agent-scope acq_rel RMW would order the same traffic through
+        // the memory model, but on gfx950 it lowers to an L2 write-back + invalidate per block (the plain-store +
+        // release form the guide's handoff-flag / publish-large rows price at 2-2.7x the sc1 form).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int* flag = reinterpret_cast<int*>(smem);
@@ -686,6 +699,9 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
         if constexpr ((EPI & EPI_SKIP) != 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = o[r] + pre_s[k][r];
+        }
+        if constexpr (ROLE == ROLE_CONSUMER) {
+            if (poison) o = floatx4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
         }
         if constexpr ((EPI & EPI_DDIM) != 0) {
             // noise_pred = o; the reverse update of model.py:442-458 (ddim_update, one rounding per op)
@@ -735,6 +751,7 @@ struct UBody {
     }
 };
 
+#if LDM_STEP_DIAG
 // Two consecutive layers in one launch: blocks [0, nA) run layer A, blocks [nA, nA + nB) run layer B, which
 // waits in-launch for A's output (PairSync) after issuing its own weight stream.  Deadlock-free under in-order
 // workgroup dispatch (every producer block is dispatched before any consumer block) and bounded otherwise.
@@ -748,6 +765,7 @@ void upair_kernel(UArgs a, UArgs b, PairSync ps) {
     else
         BB::template run<ROLE_CONSUMER>(b, (int)blockIdx.x - ps.nA, ps);
 }
+#endif  // LDM_STEP_DIAG
 
 // packed[c][m][16], c = cc*9 + t, element e = 4*lg + j  ->  input channel cc*16 + e, tap t = ky*3 + kx.
 // conv: w [COUT][CIN][3][3]; transposed conv: w [CIN][COUT][3][3] (torch layouts).  DT: element type of the
@@ -997,6 +1015,7 @@ int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     return c + ms + 64;   // + the layer-pair counters (uc::PairSync, zero between launches)
 }
 
+#if LDM_STEP_DIAG
 namespace uc {
 static int32_t* pair_counters(float* ws, int B, int H, int W) {
     int64_t c = 0;
@@ -1004,6 +1023,7 @@ static int32_t* pair_counters(float* ws, int B, int H, int W) {
     return reinterpret_cast<int32_t*>(ws + total - 64);
 }
 }  // namespace uc
+#endif
 
 namespace uc {
 // The launch arguments of layer `layer` (ksv: the K-split form).
@@ -1160,6 +1180,7 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
     }
 }
 
+#if LDM_STEP_DIAG
 namespace uc {
 template <class BA, class BB>
 static int launch_pair(const UArgs& a, const UArgs& b, int ksA, int ksB, int32_t* cnt, hipStream_t st) {
@@ -1207,6 +1228,12 @@ int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& s
         default: return fail(2, "step pair: unknown operand precision");
     }
 }
+#else   // the shipped library: layer pairs (measured 10-21 us per iteration slower) are diagnostic only
+bool step_pair_supported(int, int) { return false; }
+int step_pair(int, int, int, int, const StepConv&, const StepConv&, hipStream_t) {
+    return fail(2, "step pair: in-launch layer pairs are in the diagnostic build only (make DIAG=1)");
+}
+#endif  // LDM_STEP_DIAG
 
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st) {
     const int64_t n = (int64_t)B * C * HW;
@@ -1262,6 +1289,13 @@ extern "C" int ldm_step_conv(int32_t layer, int32_t B, int32_t H, int32_t W, con
 extern "C" int64_t ldm_step_workspace_floats(int32_t B, int32_t H, int32_t W) {
     if (B <= 0 || H % 8 || W % 8) return -1;
     return step_ws_floats(B, H, W, nullptr);
+}
+
+extern "C" int64_t ldm_step_workspace_counter_floats(int32_t B, int32_t H, int32_t W) {
+    if (B <= 0 || H % 8 || W % 8) return -1;
+    int64_t c = 0;
+    step_ws_floats(B, H, W, &c);
+    return c;
 }
 
 extern "C" int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,

@@ -371,6 +371,8 @@ extern "C" int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers) {
     return 0;
 }
 
+extern "C" int32_t ldm_step_diag_build(void) { return LDM_STEP_DIAG; }
+
 extern "C" int32_t ldm_step_set_pairs(int32_t mask) {
     const int prev = step_pair_mask();
     if (mask >= 0) g_pairs = mask;

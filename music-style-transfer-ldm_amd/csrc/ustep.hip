@@ -28,6 +28,10 @@
 
 #pragma clang fp contract(off)
 
+// Diagnostic build only (make DIAG=1 -> lib/libldm_amd_diag.so): no layer runs these kernels by default
+// (unet.hip ustep_mask), so the shipped library carries the entry points as stubs that report it.
+#if LDM_STEP_DIAG
+
 namespace ldm {
 namespace us {
 
@@ -679,3 +683,25 @@ extern "C" int ldm_ustep_conv(int32_t layer, int32_t B, const float* x, const fl
     s.skip = skip;
     return ustep_conv(layer, B, s, workspace, (hipStream_t)stream);
 }
+
+#else   // !LDM_STEP_DIAG
+
+namespace ldm {
+bool ustep_supported(int, int, int) { return false; }
+int64_t ustep_workspace_floats(int, int, int64_t* cnt_floats) {
+    if (cnt_floats) *cnt_floats = 0;
+    return 0;
+}
+int ustep_conv(int, int, const StepConv&, float*, hipStream_t) {
+    return fail(2, "ustep: the LDS-staged step kernels are in the diagnostic build only (make DIAG=1)");
+}
+}  // namespace ldm
+
+extern "C" int64_t ldm_ustep_workspace_floats(int32_t, int32_t) { return -1; }
+
+extern "C" int ldm_ustep_conv(int32_t, int32_t, const float*, const float*, const float*, const float*, const float*,
+                              float*, float*, void*) {
+    return ldm::fail(2, "ldm_ustep_conv: the LDS-staged step kernels are in the diagnostic build only (make DIAG=1)");
+}
+
+#endif  // LDM_STEP_DIAG

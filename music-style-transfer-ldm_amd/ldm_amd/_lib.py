@@ -85,6 +85,8 @@ SIGNATURES = {
     "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
     "ldm_step_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_step_set_pairs": (c_int32, [c_int32]),
+    "ldm_step_diag_build": (c_int32, []),
+    "ldm_step_workspace_counter_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_step_layer_forms": (c_int32, [c_vp, c_vp]),
     "ldm_step_dec1_ddim": (c_int32, [c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_fp,
                                      c_int32, c_vp]),

@@ -13,6 +13,7 @@ import torch
 
 from . import _lib as L
 from . import ops
+from .graphs import capture
 
 TUNED_PATH = os.path.join(L.PKG_ROOT, "tuned_plans.json")
 
@@ -64,7 +65,7 @@ def time_plan(desc, cand, x, w, y, reps=30):
     # the kernel boundary, without the host launch cost that dominates eager timing of short kernels
     cap = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=cap):
+    with capture(g, stream=cap):
         a2 = args[:-1] + (cap.cuda_stream,)
         for _ in range(reps):
             lib.ldm_conv_forward_ws(*a2)

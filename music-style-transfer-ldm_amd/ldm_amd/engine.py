@@ -11,6 +11,7 @@ import torch
 
 from . import _lib as L
 from . import ops
+from .graphs import capture
 
 byref = ctypes.byref
 
@@ -318,7 +319,7 @@ class GraphedDDIM:
         if not self.plan:
             self.graphs = [torch.cuda.CUDAGraph()]
             self.streams = None
-            with torch.cuda.graph(self.graphs[0]):
+            with capture(self.graphs[0]):
                 self.x.copy_(self.x_init)
                 self.engine.ddim_loop(self.x, self.s5, self.s6, self.t_table, self.coef, self.eta, self.x0_logs,
                                       self.eps_logs)
@@ -331,7 +332,7 @@ class GraphedDDIM:
         per_step = self.x[0].numel() * self.x.shape[0]
         for k, (lo, hi, t_sub) in enumerate(self.plan):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.streams[k]):
+            with capture(g, stream=self.streams[k]):
                 self.x[lo:hi].copy_(self.x_init[lo:hi])
                 engine._ddim_call(self.x[lo:hi], self.s5[lo:hi], self.s6[lo:hi], t_sub, self.coef, self.eta,
                                   None if self.x0_logs is None else self.x0_logs[0, lo:hi],

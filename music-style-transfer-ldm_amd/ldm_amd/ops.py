@@ -423,8 +423,12 @@ class _Sync:
 
 def _sync_group(group):
     """The group a SyncBatchNorm-marked module reduces over as a _Sync, or None when the statistics stay
-    local (sync off, no process group, or a group of one rank).  group=True means the default group."""
+    local (sync off, no process group, or a group of one rank).  group=True means the default group.  An
+    object with an `ldm_allreduce_sum(t)` method stands in for a process group (it sums t in place over its
+    ranks): the captured-step tests simulate a world-2 SyncBatchNorm with one on a single GPU."""
     import torch.distributed as dist
+    if hasattr(group, "ldm_allreduce_sum"):
+        return _Sync(group)
     if group is False or group is None or not dist.is_available() or not dist.is_initialized():
         return None
     g = None if group is True else group
@@ -432,6 +436,9 @@ def _sync_group(group):
 
 
 def _allreduce_sum(t, group):
+    if hasattr(group, "ldm_allreduce_sum"):
+        group.ldm_allreduce_sum(t)
+        return
     import torch.distributed as dist
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 

@@ -36,6 +36,7 @@ except ImportError:   # reference-style flat imports (models/ on sys.path)
     from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
 
 from ldm_amd import dist as hdist
+from ldm_amd import graphs as hgraphs
 from ldm_amd import ops
 from ldm_amd import optim as hoptim
 
@@ -275,7 +276,7 @@ class LDMTrainer:
                 self._packset.repack()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with hgraphs.capture(g):
                 outs = self._step(*static)
             self._graph, self._graph_in, self._graph_out, self._graph_sig = g, static, outs, sig
             self._graph_tables = tables

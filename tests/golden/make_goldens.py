@@ -3,6 +3,7 @@
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py          # ref_goldens.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r2     # ref_goldens_r2.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp    # ref_goldens_amp.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp8   # ref_goldens_amp8.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --vggish # ref_goldens_vggish.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r3     # ref_goldens_r3.npz
 
@@ -337,6 +338,39 @@ def amp():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
 
 
+def amp8():
+    """Config 5 at its bench shard -> tests/golden/ref_goldens_amp8.npz: content_style_ddim_sample (T'=100,
+    eta=1) at batch 8 on the canonical [8,32,16,64] latent under torch.autocast("cpu", float16), as
+    bench.py --workload transfer runs it per GPU.  The reference loop logs t.item(), which raises for batch >
+    1 (model.py:555), so it runs eight times at batch 1 (sample b: z_T[b], style[b]; the loop and the UNet are
+    per-sample) and the results are stacked; fp32 likewise, for the reference's own autocast-vs-fp32 gap.
+    Style embeddings in fp32 outside the autocast region, as in amp()."""
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+    B = 8
+    with torch.no_grad():
+        ldm = M.LDM(32, pretrained_path="")
+        recipe.fill_module(ldm, seed=700)
+        ldm.eval()
+        style = torch.from_numpy(recipe.uniform01((B, 1, 128, 512), 751))
+        zT = torch.from_numpy(recipe.normal((B, 32, 16, 64), 752))
+        for name, dt in (("fp32", None), ("fp16", torch.float16)):
+            xs = []
+            for b in range(B):
+                emb = ldm.style_encoder(style[b:b + 1])
+                if dt is None:
+                    x, _ = ldm.content_style_ddim_sample(zT[b:b + 1], emb, timesteps=100, eta=1.0)
+                else:
+                    with torch.autocast("cpu", dtype=dt):
+                        x, _ = ldm.content_style_ddim_sample(zT[b:b + 1], emb, timesteps=100, eta=1.0)
+                xs.append(x.float())
+            G[f"cs100b8_{name}_x"] = np32(torch.cat(xs, 0))
+    path = os.path.join(HERE, "ref_goldens_amp8.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
 def vggish_stack():
     """A VGGish-shaped `features` stack (3x3 convs 64-M-128-M-256-256-M-512-512-M, ReLU after each conv,
     MaxPool2d(2, 2)): the architecture torchvggish's VGG.features is built from; the weights are the
@@ -498,6 +532,8 @@ if __name__ == "__main__":
         round2()
     elif "--r3" in sys.argv:
         round3()
+    elif "--amp8" in sys.argv:
+        amp8()
     elif "--amp" in sys.argv:
         amp()
     elif "--vggish" in sys.argv:

@@ -78,6 +78,50 @@ def test_content_style_100_fp16(ldm, gamp, cuda):
     assert err < TOLS["fp16"], err
 
 
+@pytest.fixture(scope="module")
+def gamp8():
+    return np.load(f"{ROOT}/tests/golden/ref_goldens_amp8.npz")
+
+
+@pytest.mark.parametrize("path", ["sampler", "bench_object"])
+def test_content_style_100_fp16_b8(ldm, gamp8, cuda, path):
+    """Config 5 at its bench shard: batch 8, [8,32,16,64], T'=100, eta=1, fp16 step-kernel operands, fp32
+    scheduler accumulators, against the reference's autocast-fp16 loop (make_goldens.py --amp8: eight batch-1
+    runs stacked, since the reference loop raises for batch > 1 at model.py:555).  "sampler" runs
+    LDM.content_style_ddim_sample under torch.autocast("cuda", float16); "bench_object" the object bench.py
+    --workload transfer times (a GraphedDDIM replay with the engine's dtype set to fp16).  Tolerance 1e-3
+    (max-norm relative, as the batch-1 test); the reference's own fp16-vs-fp32 gap is printed."""
+    import models.model as M
+    from ldm_amd.engine import GraphedDDIM
+    B = 8
+    style = torch.from_numpy(recipe.uniform01((B, 1, 128, 512), 751)).to(cuda)
+    zT = torch.from_numpy(recipe.normal((B, 32, 16, 64), 752)).to(cuda)
+    with torch.no_grad():
+        emb = ldm.style_encoder(style)
+        if path == "sampler":
+            with torch.autocast("cuda", dtype=torch.float16):
+                x, _ = ldm.content_style_ddim_sample(zT, emb, timesteps=100, eta=1.0)
+        else:
+            times = torch.linspace(99, 0, 100).long()
+            coefs = ldm.noise_scheduler.reverse_coefs(times).to(cuda)
+            t_table = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(cuda)
+            eng = M.engine_for(ldm.unet)
+            prev = eng.dtype
+            eng.dtype = "fp16"
+            try:
+                gd = GraphedDDIM(eng, zT, emb["s5"], emb["s6"], t_table, coefs, 1.0, logs=True)
+                gd.replay()
+                x = gd.replay().clone()       # a second replay restarts from z_T: same result
+            finally:
+                eng.dtype = prev
+    ref16, ref32 = gamp8["cs100b8_fp16_x"], gamp8["cs100b8_fp32_x"]
+    err = rel_err(npy(x), ref16)
+    print(f"ours vs reference fp16 {err:.2e}; reference fp16 vs fp32 {rel_err(ref16, ref32):.2e}")
+    assert err < TOLS["fp16"], err
+    for b in range(B):   # and per sample, so that no sample hides behind the batch's max norm
+        assert rel_err(npy(x[b]), ref16[b]) < TOLS["fp16"], b
+
+
 @pytest.mark.parametrize("name,layer,ksplit", [(n, l, k) for n in ("fp16", "bf16") for l in (0, 4, 5)
                                                for k in ((False, True) if l in (4, 5) else (False,))])
 def test_step_layer_lowp(cuda, name, layer, ksplit):

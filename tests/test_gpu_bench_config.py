@@ -9,8 +9,9 @@ pinned to the reference's own outputs by tests/test_oracle_golden.py) run on the
   * timestep list bit-exact (model.py:420);
   * final x, the first pred_x0 log and the last noise_pred log within 1e-4 relative (north_star);
   * every step kernel the bench's loop launches (test_bench_config_step_kernels): each of the nine convs on
-    the instance the loop picks for it (ldm_step_layer_forms: ustep.hip for enc1, the K-split uconv.hip form for
-    enc4 and the bottleneck, uconv.hip for the others; dec1 with its fused DDIM update and both logs), with the
+    the instance the loop picks for it (ldm_step_layer_forms: the K-split uconv.hip form for enc4, the bottleneck
+    and dec4, uconv.hip's single-block form for the others, ustep.hip for none by default; dec1 with its fused
+    DDIM update and both logs), with the
     engine's packed step weights, the folded out-projections and position biases, on NHWC operands at
     B = 8, 16 x 64, against float64 torch (1e-5 relative);
   * the general-kernel (conv.hip) plans of the same layers, which ldm_unet_forward (single UNet calls) runs

@@ -18,6 +18,13 @@ import torch
 from conftest import rel_err
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _diag_build_only(cuda):
+    from ldm_amd import _lib as L
+    if not L.load().ldm_step_diag_build():
+        pytest.skip("layer pairs are in the diagnostic build only (make DIAG=1, LDM_AMD_LIB=lib/libldm_amd_diag.so)")
 TOL = 1e-4
 PAIRS = [0x1, 0x40, 0x80, 0x1 | 0x40, 0x1 | 0x80]
 

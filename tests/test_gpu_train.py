@@ -633,6 +633,27 @@ def test_act_backward_sums(cuda, shape, act):
     assert rel_err(npy(dbc).reshape(B, C), dy.sum(dim=(2, 3)).numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(2, 8, 4, 4), (3, 16, 8, 8), (2, 16, 16, 64), (3, 40, 16, 16)])
+def test_act_backward_none_separate_dv(cuda, shape):
+    """ldm_act_backward through the C ABI with act = none and a dv buffer separate from dy (ldm_capi.h: dv =
+    dy * act'(v), 'may alias' dy): dv must be written on every kernel form (small planes, the multi-plane
+    kernel at HW = 64..1024, the sliced one), with and without the bias sums."""
+    from ldm_amd import _lib as L, ops
+    B, C = shape[0], shape[1]
+    HW = shape[2] * shape[3]
+    dy = torch.from_numpy(_rand(shape, 41)).to(cuda)
+    for sums in (False, True):
+        dv = torch.full_like(dy, float("nan"))
+        db = torch.empty(C, device=cuda) if sums else None
+        ws = ops.reduce_workspace(B, C, HW, cuda)
+        L.call("ldm_act_backward", dy.data_ptr(), None, None, L.ACT["none"], B, C, HW, dv.data_ptr(),
+               None if db is None else db.data_ptr(), None, ws.data_ptr(), ops.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(dv, dy), (shape, sums)
+        if sums:
+            assert rel_err(npy(db), dy.double().sum(dim=(0, 2, 3)).cpu().numpy()) < 1e-5
+
+
 # ---- train_ldm: the reference's LDM entry point (train.py:296-316) ------------------------------------------
 def test_train_ldm_entry_point(cuda, tmp_path, monkeypatch):
     """models.train.train_ldm end to end on a tiny on-disk pair dataset, as the reference runs it from its
