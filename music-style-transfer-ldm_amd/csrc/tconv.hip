@@ -21,6 +21,7 @@
 //
 // MFMA operand maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j]
 // and B[k = 8h + j][col r], j = 0..7; D: col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4h.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -254,6 +255,214 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Window form (tconvw_kernel): the same tiles, plan and packed weights, but the activation operand is staged
+// once per 16-channel window instead of once per (tap, 32-channel chunk).  tconv_kernel's time went into its
+// per-chunk instruction stream (16 four-byte gathers per lane per chunk of K = 32, one barrier per chunk):
+// here a block loads, for 16 input channels, the whole input window its 128 positions' taps read (rows x
+// columns incl. halo and zero padding) with 16-byte loads along the NCHW rows, converts it to 16 bits and
+// parks it position-major in LDS ([window position][16 channels + 8 pad], 48-B rows: the 32-position B-fragment
+// reads are conflict-free).  Every tap then reads its B fragment (8 channels of one position, one ds_read_b128)
+// at a tap-constant offset from that image: K = 16 x taps per barrier (144 for a 3x3 conv) instead of 32.
+//   * stride-2 windows are stored with even and odd columns apart, so that the 32 consecutive positions of a
+//     fragment read consecutive image positions for every tap;
+//   * the next window's loads are issued before this window's MFMAs and written to the other LDS buffer after
+//     them; the A fragments (weights) of every tap of the next window are issued as soon as this window's tap
+//     has consumed its set, so the in-order vector-memory returns never make a tap wait for the window loads;
+//   * one phase per block and the same tap count for every block of a launch (template NT): transposed convs
+//     whose phases differ in taps run one launch per tap count.
+// Geometry (tconvw_geometry): a tile of 128 positions is R = 128 / Cq rows x Cq columns of the phase grid (Cq =
+// 128 or Wq | 128, inside one sample); Win % 4 == 0 (a 16-byte quad is wholly inside or outside a row).
+constexpr int WCH = 16;   // input channels per window
+constexpr int WP = 24;    // 16-bit elements per image position (48-B rows)
+
+struct WArgs {
+    const float* x;
+    const unsigned short* w;   // packed [phase][chunk][Mpad][32] 16-bit (as tconv_kernel)
+    float* y;
+    int32_t B, Cin, Hin, Win, Cout, Hout, Wout;
+    int32_t Mpad, nM, nN, cpt;
+    int32_t xcd_chunk;
+    int32_t nph;                      // phases in this launch
+    int32_t phs[kMaxPhase];           // their indices
+    int64_t N;                        // positions per phase
+    FastDiv fd_hw, fd_w;
+    int32_t cq_log2;                  // tile columns Cq = 1 << cq_log2
+    int32_t NQ, rowp, half, nsu;      // window: quads per row, image positions per row, odd-column plane, super-units
+    int32_t imgsz;                    // 16-bit elements per image buffer
+    int32_t ybase[kMaxPhase], xbase[kMaxPhase];   // window origin = (qy0 * sy + ybase, qx0 * sy + xbase)
+    int32_t toff[kMaxPhase][kMaxTap];             // image-position offset of each tap
+    PhaseTable pt;
+    EpiArgs ep;
+};
+
+template <int BM, int NT, int SY, int DT, int NS>
+__global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
+    constexpr int MT = BM / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned short img[];   // [2][image]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int r = lane & 31, h = lane >> 5;
+
+    int t = blockIdx.x;
+    if (a.xcd_chunk > 0) t = (t & 7) * a.xcd_chunk + (t >> 3);
+    const int mt = t % a.nM;
+    const int rest = t / a.nM;
+    const int ph = a.phs[rest % a.nph];
+    const int nt = rest / a.nph;
+    const int n0 = nt * BN;
+    const int HWq = a.pt.Hq * a.pt.Wq;
+    const int b = a.fd_hw.div(n0);
+    const int rem = n0 - b * HWq;
+    const int qy0 = a.fd_w.div(rem);
+    const int qx0 = rem - qy0 * a.pt.Wq;
+    const int iyb = qy0 * SY + a.ybase[ph], ixb = qx0 * SY + a.xbase[ph];
+    const int HWin = a.Hin * a.Win;
+    const int imgsz = a.imgsz;   // 16-bit elements per image buffer (+ a 48-B dummy row after it)
+
+    // ---- window super-units of this thread: 4 channels x one 16-byte column quad of one window row
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
+    int svo[NS], slp[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int su = s * 256 + tid;
+        const bool valid = su < a.nsu;
+        const int q4 = a.NQ * 4;
+        const int wr = su / q4;
+        const int rr = su - wr * q4;
+        const int q = rr >> 2, cg = rr & 3;
+        const int iy = iyb + wr, ix = ixb + 4 * q;
+        const bool ok = valid && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+        svo[s] = ok ? ((b * a.Cin + 4 * cg) * HWin + iy * a.Win + ix) * 4 : kOOB;
+        // (a slot past the window writes to the dummy row after the image: the store stays branch-free)
+        slp[s] = valid ? (wr * a.rowp + (SY == 2 ? 2 * q : 4 * q)) * WP + 4 * cg : imgsz;
+    }
+    floatx4 wv[NS][4];
+    auto load_win = [&](int w) {   // channels 16 w + 4 cg + i of every super-unit
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                wv[s][i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           xr, svo[s], uni((w * WCH + i) * HWin * 4), 0));
+    };
+    auto store_win = [&](int buf) {
+        unsigned short* base = img + buf * (imgsz + WP);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                floatx4 v{wv[s][0][k], wv[s][1][k], wv[s][2][k], wv[s][3][k]};
+                const int col = slp[s] == imgsz ? 0 : (SY == 2 ? ((k & 1) * a.half + (k >> 1)) : k);
+                uint2 pk;
+                if constexpr (DT == 1)
+                    pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, halfx4));
+                else
+                    pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+                *reinterpret_cast<uint2*>(base + slp[s] + col * WP) = pk;
+            }
+        }
+    };
+
+    // ---- B fragments: this lane's two 32-column tiles, image position of tap 0's origin
+    int lb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int nl = wn * 64 + 32 * j + r;
+        const int rrow = nl >> a.cq_log2, cx = nl & ((1 << a.cq_log2) - 1);
+        lb[j] = (rrow * SY * a.rowp + cx) * WP + 8 * h;
+    }
+
+    // ---- A fragments: rows mbase + 32 i + r, k = 16 (w & 1) + 8 h of chunk (w / 2) * NT + tap
+    const int mbase = mt * BM + wm * (BM / 2);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, 0x7ffffff0, 0x00020000);
+    const int wph = (int)a.pt.wofs[ph];
+    u16x8 af[NT][MT];
+    auto loadA = [&](int w, int tap, u16x8 (&dst)[MT]) {
+        const int c = (w >> 1) * NT + tap;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int e = wph + (c * a.Mpad + mbase + 32 * i + r) * KC + 16 * (w & 1) + 8 * h;
+            dst[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, e * 2, 0, 0));
+        }
+    };
+
+    floatx16 acc[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+    const int NW = a.Cin / WCH;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) loadA(0, tp, af[tp]);
+    load_win(0);
+    store_win(0);
+    __syncthreads();
+    // Every iteration issues the same instruction stream (past the end: re-loads of the last window and its
+    // weights, stored into the idle buffer, which nothing reads), so that the loads are never sunk into a
+    // conditional store and the waitcnt pass counts them exactly; the scheduling fences keep the window
+    // loads ahead of the MFMAs and each tap's weight loads right after the tap that frees their registers.
+    for (int w = 0; w < NW; ++w) {
+        const int buf = w & 1;
+        const int wn1 = w + 1 < NW ? w + 1 : w;
+        load_win(wn1);
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned short* bimg = img + buf * (imgsz + WP);
+#pragma unroll
+        for (int tp = 0; tp < NT; ++tp) {
+            const int to = a.toff[ph][tp] * WP;
+            u16x8 bf[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const u16x8*>(bimg + lb[j] + to);
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = mma<DT>(af[tp][i], bf[j], acc[i][j]);
+            loadA(wn1, tp, af[tp]);   // this tap's set is free: the next window's weights for it
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        store_win(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store (as tconv_kernel)
+    const EpiArgs& e = a.ep;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int nn = n0 + wn * 64 + 32 * j + r;
+        const int bb = a.fd_hw.div(nn);
+        const int rr = nn - bb * HWq;
+        const int qy = a.fd_w.div(rr);
+        const int qx = rr - qy * a.pt.Wq;
+        const int oy = qy * a.pt.osy + a.pt.ry[ph], ox = qx * a.pt.osy + a.pt.rx[ph];
+        const size_t obase = (size_t)bb * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int co = mbase + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (co >= a.Cout) continue;
+                float v = acc[i][j][q];
+                if (e.bias) v = v + e.bias[co];
+                if (e.bn_w) {
+                    const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
+                    const float alpha = invstd * e.bn_w[co];
+                    const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
+                    v = v * alpha + beta;
+                }
+                v = apply_act(v, e.act);
+                const size_t o = obase + (size_t)co * a.Hout * a.Wout;
+                if (e.act_out) e.act_out[o] = v;
+                a.y[o] = v;
+            }
+    }
+}
+
 // packed[p][c][m][e] = w(co = m, tap t = c % ntap, ci = (c / ntap) * 32 + e) in 16 bits, zero past Cout
 template <int DT>
 __global__ __launch_bounds__(256) void tconv_pack_kernel(const float* __restrict__ w, unsigned short* __restrict__ out,
@@ -292,6 +501,119 @@ static int layout(const ldm_conv_desc& d, int bm, PhaseTable& pt, int& Mpad, int
         pt.wofs[p] = halfs;
         pt.kchunks[p] = pt.ntap[p] * (d.Cin / KC);
         halfs += (int64_t)pt.kchunks[p] * Mpad * KC;
+    }
+    return 0;
+}
+
+// ---- the window form's geometry and launch ------------------------------------------------------------
+// Tap count and stride of one launch of the window form (template NT, SY); its image sizes (NS super-unit
+// slots per thread, LDS bytes) are checked here against the instance.
+template <int BM, int NT, int SY, int DT, int NS>
+static int launch_w(WArgs& a, hipStream_t st) {
+    LDM_REQUIRE(a.nsu <= NS * 256, "tconvw: window larger than the instance's register slots");
+    const size_t lds = (size_t)2 * (a.imgsz + WP) * 2;
+    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS>;
+    if (lds > 64 * 1024) {
+        static bool opted = false;
+        if (!opted) {
+            LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            opted = true;
+        }
+    }
+    const int64_t blocks = (int64_t)a.nph * a.nM * a.nN;
+    a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(256), lds, st, a);
+    LDM_CHECK_LAUNCH("tconvw_kernel");
+    return 0;
+}
+
+// Window geometry of the phases `phs` (same tap count) of a kind-3 conv; false when the tile / window shape
+// does not fit the window form (tconv_kernel then runs).
+static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* phs, int nph, WArgs& a) {
+    if (d.Win % 4 || d.Cin % WCH) return false;
+    const int HWq = pt.Hq * pt.Wq;
+    if (HWq % BN) return false;
+    int cq;
+    if (pt.Wq % BN == 0) cq = BN;
+    else if (BN % pt.Wq == 0) cq = pt.Wq;
+    else return false;
+    int l2 = 0;
+    while ((1 << l2) < cq) ++l2;
+    if ((1 << l2) != cq) return false;
+    const int R = BN / cq, sy = pt.sy;
+    if (sy != 1 && sy != 2) return false;
+    int NR = 0, NQ = 0;
+    a.nph = nph;
+    for (int i = 0; i < nph; ++i) {
+        const int p = phs[i];
+        a.phs[i] = p;
+        int dy0 = 1 << 20, dy1 = -(1 << 20), dx0 = 1 << 20, dx1 = -(1 << 20);
+        for (int t = 0; t < pt.ntap[p]; ++t) {
+            dy0 = std::min(dy0, (int)pt.dy[p][t]), dy1 = std::max(dy1, (int)pt.dy[p][t]);
+            dx0 = std::min(dx0, (int)pt.dx[p][t]), dx1 = std::max(dx1, (int)pt.dx[p][t]);
+        }
+        const int xb = dx0 >= 0 ? (dx0 / 4) * 4 : -((-dx0 + 3) / 4) * 4;   // 4 * floor(dx0 / 4)
+        a.ybase[p] = dy0;
+        a.xbase[p] = xb;
+        NR = std::max(NR, (R - 1) * sy + (dy1 - dy0) + 1);
+        NQ = std::max(NQ, ((cq - 1) * sy + dx1 - xb) / 4 + 1);
+    }
+    a.NQ = NQ;
+    a.rowp = 4 * NQ;
+    a.half = 2 * NQ;
+    a.nsu = 4 * NR * NQ;
+    a.imgsz = NR * a.rowp * WP;
+    if ((size_t)2 * a.imgsz * 2 > 150 * 1024) return false;
+    for (int i = 0; i < nph; ++i) {
+        const int p = phs[i];
+        for (int t = 0; t < pt.ntap[p]; ++t) {
+            const int c0 = pt.dx[p][t] - a.xbase[p];
+            a.toff[p][t] = (pt.dy[p][t] - a.ybase[p]) * a.rowp + (sy == 2 ? ((c0 & 1) * a.half + (c0 >> 1)) : c0);
+        }
+    }
+    a.cq_log2 = l2;
+    return true;
+}
+
+// The window form of one kind-3 conv: one launch per group of phases with equal tap counts.  Returns 1 (and
+// launches nothing) when some group's geometry does not fit an instance.
+static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st) {
+    const PhaseTable& pt = t.pt;
+    int groups[kMaxPhase][kMaxPhase], gn[kMaxPhase], gt[kMaxPhase], ng = 0;
+    for (int p = 0; p < pt.nphase; ++p) {
+        int g = 0;
+        while (g < ng && gt[g] != pt.ntap[p]) ++g;
+        if (g == ng) gt[ng] = pt.ntap[p], gn[ng] = 0, ++ng;
+        groups[g][gn[g]++] = p;
+    }
+    WArgs w[kMaxPhase];
+    for (int g = 0; g < ng; ++g) {
+        w[g] = WArgs{};
+        if (!w_geometry(d, pt, groups[g], gn[g], w[g])) return 1;
+        const int nt = gt[g], sy = pt.sy;
+        const int ns = (w[g].nsu + 255) / 256;
+        const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && bm == 64 && ns <= 5) ||
+                        ((nt == 1 || nt == 2 || nt == 4) && sy == 1 && ns <= 2);
+        if (!ok) return 1;
+    }
+    for (int g = 0; g < ng; ++g) {
+        WArgs& a = w[g];
+        a.x = t.x, a.w = t.w, a.y = t.y;
+        a.B = t.B, a.Cin = t.Cin, a.Hin = t.Hin, a.Win = t.Win, a.Cout = t.Cout, a.Hout = t.Hout, a.Wout = t.Wout;
+        a.Mpad = t.Mpad, a.nM = t.nM, a.nN = t.nN, a.cpt = t.cpt;
+        a.N = t.N, a.fd_hw = t.fd_hw, a.fd_w = t.fd_w, a.pt = t.pt, a.ep = t.ep;
+        const int nt = gt[g], sy = pt.sy;
+        int rc;
+#define TCW(BM_, NT_, SY_, NS_)                                                                          \
+    (dt == LDM_DT_F16 ? launch_w<BM_, NT_, SY_, 1, NS_>(a, st) : launch_w<BM_, NT_, SY_, 2, NS_>(a, st))
+        if (nt == 16) rc = TCW(64, 16, 2, 5);
+        else if (nt == 9 && sy == 2) rc = bm == 128 ? TCW(128, 9, 2, 4) : TCW(64, 9, 2, 4);
+        else if (nt == 9) rc = bm == 128 ? TCW(128, 9, 1, 2) : TCW(64, 9, 1, 2);
+        else if (nt == 4) rc = bm == 128 ? TCW(128, 4, 1, 2) : TCW(64, 4, 1, 2);
+        else if (nt == 2) rc = bm == 128 ? TCW(128, 2, 1, 2) : TCW(64, 2, 1, 2);
+        else rc = bm == 128 ? TCW(128, 1, 1, 2) : TCW(64, 1, 1, 2);
+#undef TCW
+        if (rc) return rc;
     }
     return 0;
 }
@@ -398,6 +720,21 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     a.xcd_chunk = (order && blocks % 8 == 0) ? (int)(blocks / 8) : 0;
     LDM_REQUIRE(blocks < (1LL << 31), "tconv: grid too large");
     hipStream_t s = st;
+    // the window form where the geometry allows (LDM_TCONV_WIN=0: the per-chunk gather form, A/B timing).
+    // 16-tap (4x4 stride-2) convs run it on 64-row tiles: their image needs five register slots per thread.
+    static const bool win = [] {
+        const char* e = std::getenv("LDM_TCONV_WIN");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (win) {
+        const bool k16 = a.pt.nphase == 1 && a.pt.ntap[0] == 16;
+        if (!k16 || p.tm == 1 || a.Mpad % 64 == 0) {
+            tc::TArgs t = a;
+            if (k16 && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
+            const int rc = tc::forward_window(d, t, k16 ? 64 : 64 * p.tm, p.tn, s);
+            if (rc != 1) return rc;
+        }
+    }
     if (p.tm == 2) {
         if (p.tn == LDM_DT_F16)
             hipLaunchKernelGGL((tc::tconv_kernel<128, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);

@@ -23,6 +23,15 @@ CASES = {
     "convT_k4_128to64": (2, 128, 32, 64, 64, 4, 2, 1, 0, True),       # decoder.3 class: 4 phases x 4 taps
     "convT_k3op1_64to32": (2, 64, 32, 64, 32, 3, 2, 1, 1, True),      # style-encoder dgrad class: 1/2/2/4 taps
     "ragged_32to40": (3, 32, 17, 97, 40, 3, 1, 1, 0, False),          # N % 128 != 0, Cout % 32 != 0
+    # window-form geometries (tconvw_kernel): 128-position tiles of one output row (Wq = 128) or of R rows
+    "w_k3s2_row128": (2, 64, 64, 256, 128, 3, 2, 1, 0, False),        # VAE / style enc2 class, Wq = 128
+    "w_k3s2_cout32": (4, 128, 32, 128, 32, 3, 2, 1, 0, False),        # VAE enc3 class: 64-row tiles, Wq = 64
+    "w_k3s2_wq16": (32, 64, 16, 32, 128, 3, 2, 1, 0, False),           # 8 rows of 16 per tile
+    "w_k4s2_row128": (2, 128, 64, 256, 64, 4, 2, 1, 0, False),        # 16 taps, five register slots
+    "w_k4s2_cout128": (2, 64, 64, 256, 128, 4, 2, 1, 0, False),       # 16 taps on the 128-row pack as 64-row tiles
+    "w_convT_k4_row128": (2, 128, 32, 128, 64, 4, 2, 1, 0, True),     # decoder.3 class, phase grid Wq = 128
+    "w_convT_k3op1_row128": (2, 64, 32, 128, 32, 3, 2, 1, 1, True),   # 1/2/2/4-tap phases, three launches
+    "w_k3s1_cout256": (4, 32, 16, 64, 256, 3, 1, 1, 0, False),        # stride 1, two M tiles
 }
 EPIS = {"plain": {}, "bias_relu_actout": {"bias": True, "act": "relu", "act_out": True},
         "bn_relu": {"bias": True, "bn": True, "act": "relu"}, "tanh": {"act": "tanh"}}
@@ -110,3 +119,36 @@ def test_convT_cout1(cuda, shape, act):
     assert y.shape == ref.shape
     assert rel_err(y.double().cpu().numpy(), ref.numpy()) < 1e-5
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("case", sorted(c for c in CASES if c.startswith("w_")) + ["k3s1_64to128", "k4s2_128to64"])
+def test_tiled_conv_window_vs_gather(cuda, case, monkeypatch):
+    """The window form (tconvw_kernel) and the per-chunk gather form (tconv_kernel, LDM_TCONV_WIN=0) of the
+    same kind-3 plan: both within 1e-5 of float64 of the bf16-rounded operands, and of each other (they sum K
+    in different orders).  The env switch is read once per process, so the gather form runs in a child."""
+    import os
+    import subprocess
+    import sys
+    from ldm_amd import ops
+    B, Cin, H, W, Cout, k, s, p, op, tr = CASES[case]
+    x = _rand((B, Cin, H, W), 5)
+    w = _rand((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), 6, -0.1, 0.1)
+    y = ops.conv_forward(x.to(cuda), w.to(cuda), None, stride=s, padding=p, transposed=tr, output_padding=op, dtype=2)
+    xr, wr = x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()
+    ref = tF.conv_transpose2d(xr, wr, stride=s, padding=p, output_padding=op) if tr else tF.conv2d(xr, wr, stride=s, padding=p)
+    assert rel_err(y.double().cpu().numpy(), ref.numpy()) < 1e-5
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys, torch, numpy as np; sys.path.insert(0, %r); import conftest, test_gpu_tiled as t; "
+            "from ldm_amd import ops; c = t.CASES[%r]; B, Cin, H, W, Cout, k, s, p, op, tr = c; "
+            "x = t._rand((B, Cin, H, W), 5); w = t._rand((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), 6, -0.1, 0.1); "
+            "y = ops.conv_forward(x.cuda(), w.cuda(), None, stride=s, padding=p, transposed=tr, output_padding=op, "
+            "dtype=2); np.save(sys.argv[1], y.double().cpu().numpy())" % (here, case))
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"tcw_{case}_{os.getpid()}.npy")
+    env = dict(os.environ, LDM_TCONV_WIN="0")
+    r = subprocess.run([sys.executable, "-c", code, out], env=env, cwd=here, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    y_gather = np.load(out)
+    os.remove(out)
+    assert rel_err(y_gather, ref.numpy()) < 1e-5
+    assert rel_err(y.double().cpu().numpy(), y_gather) < 1e-5
+
