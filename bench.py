@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic_step.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic_step.json"),
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
     a = ap.parse_args()
     if a.batch is None:
@@ -353,6 +353,21 @@ def run_train(args, world, rank, dev, M):
     flops = TRAIN_GFLOP_PER_SAMPLE * 1e9 * B
     achieved = flops / (ms_step * 1e-3) / 1e12
     peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
+    # HBM bytes per step from the newest committed PMC passes of this line (tools/pmc_train.sh: FETCH_SIZE x2 +
+    # WRITE_SIZE summed over the step's dispatches), bf16 only (the passes profile the default line)
+    traffic = None
+    if args.dtype == "bf16" and world == 1:
+        for rnd in ("r04", "r03"):
+            pth = os.path.join(ROOT, "profiles", rnd, "train_pmc.json")
+            if os.path.exists(pth):
+                try:
+                    with open(pth) as f:
+                        traffic = json.load(f).get("step_hbm_bytes")
+                    traffic = {"bytes_per_step": traffic, "source": f"profiles/{rnd}/train_pmc.json",
+                               "achieved_gbs": round(traffic / (ms_step * 1e-3) / 1e9, 1)}
+                except (OSError, ValueError, TypeError):
+                    traffic = None
+                break
     return {
         "metric": "LDM train samples/sec (encode -> UNet train step -> decode), 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -369,7 +384,7 @@ def run_train(args, world, rank, dev, M):
                    "global_batch": B * world, "parallelism": f"dp{world}"},
         "roofline": {"kernel": "whole train step (composite)", "bound": "mfma", "achieved": round(achieved, 2),
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     "traffic": None, "flops_per_step": flops},
+                     "traffic": traffic, "flops_per_step": flops},
         "last_losses": {k: round(v, 6) for k, v in losses.items()},
     }
 
@@ -504,7 +519,7 @@ def main():
                 traffic = None
         peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
         if args.dtype != "fp32":
-            traffic = None     # profiles/r03/pmc_traffic_step.json holds the fp32 kernels' counters
+            traffic = None     # profiles/r04/pmc_traffic_step.json holds the fp32 kernels' counters
         result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
                               "achieved": dk["tflops"], "peak": peak, "unit": "TFLOP/s",
                               "frac": round(dk["tflops"] / peak, 4), "traffic": traffic,

@@ -273,6 +273,15 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 //     whose phases differ in taps run one launch per tap count.
 // Geometry (tconvw_geometry): a tile of 128 positions is R = 128 / Cq rows x Cq columns of the phase grid (Cq =
 // 128 or Wq | 128, inside one sample); Win % 4 == 0 (a 16-byte quad is wholly inside or outside a row).
+// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 constexpr int WCH = 16;   // input channels per window
 constexpr int WP = 24;    // 16-bit elements per image position (48-B rows)
 
@@ -296,9 +305,19 @@ struct WArgs {
     EpiArgs ep;
 };
 
-template <int BM, int NT, int SY, int DT, int NS>
+// PK = 1: the four output-parity phases of a k3 s2 p1 op1 transposed conv (the data gradient of a 3x3 stride-2
+// conv) in ONE block over one shared window — phases (0,0), (0,1), (1,0), (1,1) have 1, 2, 2, 4 taps, all reading
+// input offsets {0, 1} x {0, 1}, so the block runs nine (phase, tap) pairs per window into four accumulator sets,
+// the compute density of a 3x3 conv (a launch per phase reloads the window for one to four taps).
+__host__ __device__ constexpr int pk1_phase(int i) { return i < 1 ? 0 : (i < 3 ? 1 : (i < 5 ? 2 : 3)); }
+__host__ __device__ constexpr int pk1_tap(int i) { return i < 1 ? i : (i < 3 ? i - 1 : (i < 5 ? i - 3 : i - 5)); }
+__host__ __device__ constexpr int pk1_ntap(int p) { return p == 0 ? 1 : (p == 3 ? 4 : 2); }
+
+template <int BM, int NT, int SY, int DT, int NS, int PK = 0>
 __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     constexpr int MT = BM / 64;
+    constexpr int NACC = PK ? 4 : 1;
+    static_assert(!PK || (NT == 9 && SY == 1), "PK 1: the nine (phase, tap) pairs of a k3 op1 transposed conv");
     extern __shared__ __attribute__((aligned(16))) unsigned short img[];   // [2][image]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -309,8 +328,8 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     if (a.xcd_chunk > 0) t = (t & 7) * a.xcd_chunk + (t >> 3);
     const int mt = t % a.nM;
     const int rest = t / a.nM;
-    const int ph = a.phs[rest % a.nph];
-    const int nt = rest / a.nph;
+    const int ph = PK ? 0 : a.phs[rest % a.nph];   // (PK 1: every phase; the window origin is phase 0's)
+    const int nt = PK ? rest : rest / a.nph;
     const int n0 = nt * BN;
     const int HWq = a.pt.Hq * a.pt.Wq;
     const int b = a.fd_hw.div(n0);
@@ -378,10 +397,13 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     // ---- A fragments: rows mbase + 32 i + r, k = 16 (w & 1) + 8 h of chunk (w / 2) * NT + tap
     const int mbase = mt * BM + wm * (BM / 2);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, 0x7ffffff0, 0x00020000);
-    const int wph = (int)a.pt.wofs[ph];
     u16x8 af[NT][MT];
-    auto loadA = [&](int w, int tap, u16x8 (&dst)[MT]) {
-        const int c = (w >> 1) * NT + tap;
+    // pair tp: phase PK ? pk1_phase(tp) : ph, tap in that phase PK ? pk1_tap(tp) : tp
+    auto loadA = [&](int w, auto tpc, u16x8 (&dst)[MT]) {
+        constexpr int tp = decltype(tpc)::value;
+        const int pp = PK ? pk1_phase(tp) : ph;
+        const int c = (w >> 1) * (PK ? pk1_ntap(pk1_phase(tp)) : NT) + (PK ? pk1_tap(tp) : tp);
+        const int wph = (int)a.pt.wofs[pp];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int e = wph + (c * a.Mpad + mbase + 32 * i + r) * KC + 16 * (w & 1) + 8 * h;
@@ -389,17 +411,18 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         }
     };
 
-    floatx16 acc[MT][2];
+    floatx16 acc[NACC][MT][2];
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int u = 0; u < NACC; ++u)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[u][i][j][q] = 0.f;
 
     const int NW = a.Cin / WCH;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) loadA(0, tp, af[tp]);
+    static_for<0, NT>([&](auto tpc) { loadA(0, tpc, af[decltype(tpc)::value]); });
     load_win(0);
     store_win(0);
     __syncthreads();
@@ -413,53 +436,112 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         load_win(wn1);
         __builtin_amdgcn_sched_barrier(0);
         const unsigned short* bimg = img + buf * (imgsz + WP);
-#pragma unroll
-        for (int tp = 0; tp < NT; ++tp) {
-            const int to = a.toff[ph][tp] * WP;
+        static_for<0, NT>([&](auto tpc) {
+            constexpr int tp = decltype(tpc)::value;
+            constexpr int u = PK ? pk1_phase(tp) : 0;
+            const int to = (PK ? a.toff[u][pk1_tap(tp)] : a.toff[ph][tp]) * WP;
             u16x8 bf[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const u16x8*>(bimg + lb[j] + to);
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = mma<DT>(af[tp][i], bf[j], acc[i][j]);
-            loadA(wn1, tp, af[tp]);   // this tap's set is free: the next window's weights for it
+                for (int j = 0; j < 2; ++j) acc[u][i][j] = mma<DT>(af[tp][i], bf[j], acc[u][i][j]);
+            loadA(wn1, tpc, af[tp]);   // this tap's set is free: the next window's weights for it
             __builtin_amdgcn_sched_barrier(0);
-        }
+        });
         store_win(buf ^ 1);
         __syncthreads();
     }
 
-    // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store (as tconv_kernel)
+    // ---- epilogue: bias -> eval-BN -> act (-> act_out)
     const EpiArgs& e = a.ep;
+    auto epi = [&](float v, int co) {
+        if (e.bias) v = v + e.bias[co];
+        if (e.bn_w) {   // as epi_finish (conv.hip)
+            const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
+            const float alpha = invstd * e.bn_w[co];
+            const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
+            v = v * alpha + beta;
+        }
+        return apply_act(v, e.act);
+    };
+    if constexpr (NT == 4) {
+        // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int nn = n0 + wn * 64 + 32 * j + r;
-        const int bb = a.fd_hw.div(nn);
-        const int rr = nn - bb * HWq;
-        const int qy = a.fd_w.div(rr);
-        const int qx = rr - qy * a.pt.Wq;
-        const int oy = qy * a.pt.osy + a.pt.ry[ph], ox = qx * a.pt.osy + a.pt.rx[ph];
-        const size_t obase = (size_t)bb * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+        for (int j = 0; j < 2; ++j) {
+            const int nn = n0 + wn * 64 + 32 * j + r;
+            const int bb = a.fd_hw.div(nn);
+            const int rr = nn - bb * HWq;
+            const int qy = a.fd_w.div(rr);
+            const int qx = rr - qy * a.pt.Wq;
+            const int oy = qy * a.pt.osy + a.pt.ry[ph], ox = qx * a.pt.osy + a.pt.rx[ph];
+            const size_t obase = (size_t)bb * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+            for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int co = mbase + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
-                if (co >= a.Cout) continue;
-                float v = acc[i][j][q];
-                if (e.bias) v = v + e.bias[co];
-                if (e.bn_w) {
-                    const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
-                    const float alpha = invstd * e.bn_w[co];
-                    const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-                    v = v * alpha + beta;
+                for (int q = 0; q < 16; ++q) {
+                    const int co = mbase + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                    if (co >= a.Cout) continue;
+                    const float v = epi(acc[0][i][j][q], co);
+                    const size_t o = obase + (size_t)co * a.Hout * a.Wout;
+                    if (e.act_out) e.act_out[o] = v;
+                    a.y[o] = v;
                 }
-                v = apply_act(v, e.act);
-                const size_t o = obase + (size_t)co * a.Hout * a.Wout;
-                if (e.act_out) e.act_out[o] = v;
-                a.y[o] = v;
+        }
+    } else {
+        // Staged through LDS (the image buffers are free now) as [channel][output row segment], then written
+        // with 16-byte stores along the NCHW rows: a lane's accumulator holds one position of 16 channels, so
+        // direct stores are 4-byte scalars (64-128 per lane), and the store issue, not the bytes, bounded the
+        // large-plane layers.  One pass for a single phase (the tile's R rows x Cq columns); PK 1: one pass per
+        // output row parity ry, holding phases (ry, 0) and (ry, 1) interleaved into whole output rows.
+        constexpr int NPASS = PK ? 2 : 1;
+        const int cq = 1 << a.cq_log2, R = BN >> a.cq_log2;
+        const int rowlen = PK ? 2 * cq : cq;            // floats per staged output row
+        const int seg = R * rowlen;                     // floats per channel in one pass
+        const int pitch = seg + 4;                      // (+16 B: consecutive channels start on different banks)
+        float* stg = reinterpret_cast<float*>(img);
+        const int HWo = a.Hout * a.Wout;
+        static_for<0, NPASS>([&](auto passc) {
+            constexpr int pass = decltype(passc)::value;
+            __syncthreads();   // every wave is done with the image (pass 0) / the previous pass's reads
+            static_for<0, NACC>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                if constexpr (PK && (u >> 1) != pass) return;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int nl = wn * 64 + 32 * j + r;
+                    const int rr = nl >> a.cq_log2, cx = nl & (cq - 1);
+                    const int col = rr * rowlen + (PK ? 2 * cx + (u & 1) : cx);
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) {
+                            const int cl = wm * (BM / 2) + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                            const int co = mt * BM + cl;
+                            stg[cl * pitch + col] = epi(acc[u][i][j][q], co < a.Cout ? co : 0);
+                        }
+                }
+            });
+            __syncthreads();
+            const int nv = BM * seg / 4;               // 16-byte pieces of the staged tile
+            const int b = a.fd_hw.div(n0);
+            const int rem0 = n0 - b * HWq;
+            const int qy0 = a.fd_w.div(rem0), qx0 = rem0 - qy0 * a.pt.Wq;
+            for (int k = tid; k < nv; k += 256) {
+                const int cl = k / (seg / 4);
+                const int rest4 = (k - cl * (seg / 4)) * 4;
+                const int co = mt * BM + cl;
+                if (co >= a.Cout) continue;
+                const int rr = rest4 / rowlen, c0 = rest4 - rr * rowlen;
+                const int oy = PK ? 2 * (qy0 + rr) + pass : qy0 + rr;
+                const int ox = PK ? 2 * qx0 + c0 : qx0 + c0;
+                const floatx4 v = *reinterpret_cast<const floatx4*>(stg + cl * pitch + rest4);
+                const size_t o = ((size_t)b * a.Cout + co) * HWo + (size_t)oy * a.Wout + ox;
+                if (e.act_out) *reinterpret_cast<floatx4*>(e.act_out + o) = v;
+                *reinterpret_cast<floatx4*>(a.y + o) = v;
             }
+        });
     }
 }
 
@@ -508,11 +590,15 @@ static int layout(const ldm_conv_desc& d, int bm, PhaseTable& pt, int& Mpad, int
 // ---- the window form's geometry and launch ------------------------------------------------------------
 // Tap count and stride of one launch of the window form (template NT, SY); its image sizes (NS super-unit
 // slots per thread, LDS bytes) are checked here against the instance.
-template <int BM, int NT, int SY, int DT, int NS>
+template <int BM, int NT, int SY, int DT, int NS, int PK = 0>
 static int launch_w(WArgs& a, hipStream_t st) {
     LDM_REQUIRE(a.nsu <= NS * 256, "tconvw: window larger than the instance's register slots");
-    const size_t lds = (size_t)2 * (a.imgsz + WP) * 2;
-    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS>;
+    // the image double buffer, or the epilogue's staged output tile if larger (BM channels x the pass's floats)
+    const int cq = 1 << a.cq_log2;
+    const size_t stage = NT == 4 ? 0 : (size_t)BM * ((PK ? 2 * BN : BN) + 4) * 4;
+    const size_t lds = std::max((size_t)2 * (a.imgsz + WP) * 2, stage);
+    (void)cq;
+    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK>;
     if (lds > 64 * 1024) {
         static bool opted = false;
         if (!opted) {
@@ -529,8 +615,9 @@ static int launch_w(WArgs& a, hipStream_t st) {
 
 // Window geometry of the phases `phs` (same tap count) of a kind-3 conv; false when the tile / window shape
 // does not fit the window form (tconv_kernel then runs).
-static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* phs, int nph, WArgs& a) {
-    if (d.Win % 4 || d.Cin % WCH) return false;
+static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* phs, int nph, WArgs& a,
+                       bool shared = false) {
+    if (d.Win % 4 || d.Wout % 4 || d.Cin % WCH) return false;   // 16-byte window quads and output stores
     const int HWq = pt.Hq * pt.Wq;
     if (HWq % BN) return false;
     int cq;
@@ -558,6 +645,18 @@ static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* 
         NR = std::max(NR, (R - 1) * sy + (dy1 - dy0) + 1);
         NQ = std::max(NQ, ((cq - 1) * sy + dx1 - xb) / 4 + 1);
     }
+    if (shared) {   // one window for every phase of the block: the common origin and extent
+        int y0 = 1 << 20, x0 = 1 << 20, y1 = -(1 << 20), x1 = -(1 << 20);
+        for (int i = 0; i < nph; ++i)
+            for (int t = 0; t < pt.ntap[phs[i]]; ++t) {
+                y0 = std::min(y0, (int)pt.dy[phs[i]][t]), y1 = std::max(y1, (int)pt.dy[phs[i]][t]);
+                x0 = std::min(x0, (int)pt.dx[phs[i]][t]), x1 = std::max(x1, (int)pt.dx[phs[i]][t]);
+            }
+        const int xb = x0 >= 0 ? (x0 / 4) * 4 : -((-x0 + 3) / 4) * 4;
+        for (int i = 0; i < nph; ++i) a.ybase[phs[i]] = y0, a.xbase[phs[i]] = xb;
+        NR = (R - 1) * sy + (y1 - y0) + 1;
+        NQ = ((cq - 1) * sy + x1 - xb) / 4 + 1;
+    }
     a.NQ = NQ;
     a.rowp = 4 * NQ;
     a.half = 2 * NQ;
@@ -579,6 +678,22 @@ static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* 
 // launches nothing) when some group's geometry does not fit an instance.
 static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st) {
     const PhaseTable& pt = t.pt;
+    auto fill = [&](WArgs& a) {
+        a.x = t.x, a.w = t.w, a.y = t.y;
+        a.B = t.B, a.Cin = t.Cin, a.Hin = t.Hin, a.Win = t.Win, a.Cout = t.Cout, a.Hout = t.Hout, a.Wout = t.Wout;
+        a.Mpad = t.Mpad, a.nM = t.nM, a.nN = t.nN, a.cpt = t.cpt;
+        a.N = t.N, a.fd_hw = t.fd_hw, a.fd_w = t.fd_w, a.pt = t.pt, a.ep = t.ep;
+    };
+    // the data gradient of a 3x3 stride-2 conv (k3 s2 p1 op1 transposed: phases of 1, 2, 2, 4 taps): all four
+    // phases in one block over a shared window, on 64-row tiles (four accumulator sets)
+    if (pt.nphase == 4 && pt.sy == 1 && pt.ntap[0] == 1 && pt.ntap[1] == 2 && pt.ntap[2] == 2 && pt.ntap[3] == 4) {
+        WArgs a{};
+        const int all[4] = {0, 1, 2, 3};
+        if (bm != 64 || !w_geometry(d, pt, all, 4, a, true) || a.nsu > 2 * 256) return 1;
+        fill(a);
+        a.nph = 1;
+        return dt == LDM_DT_F16 ? launch_w<64, 9, 1, 1, 2, 1>(a, st) : launch_w<64, 9, 1, 2, 2, 1>(a, st);
+    }
     int groups[kMaxPhase][kMaxPhase], gn[kMaxPhase], gt[kMaxPhase], ng = 0;
     for (int p = 0; p < pt.nphase; ++p) {
         int g = 0;
@@ -592,16 +707,17 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         if (!w_geometry(d, pt, groups[g], gn[g], w[g])) return 1;
         const int nt = gt[g], sy = pt.sy;
         const int ns = (w[g].nsu + 255) / 256;
-        const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && bm == 64 && ns <= 5) ||
-                        ((nt == 1 || nt == 2 || nt == 4) && sy == 1 && ns <= 2);
+        // measured (profiles/r04/tconv_window): the window form wins for 3x3 convs (5-25 %) and where a window
+        // feeds >= 16 MFMAs per wave with one M tile (the decoder's 32 -> 128 convT and its data gradient); with
+        // fewer taps x rows per window, or a window re-loaded by two M tiles, the per-chunk form is faster
+        const bool dense = nt * (bm / 64) >= 8 && t.nM == 1;
+        const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && bm == 64 && ns <= 5 && dense) ||
+                        (nt == 4 && sy == 1 && ns <= 2 && dense);
         if (!ok) return 1;
     }
     for (int g = 0; g < ng; ++g) {
         WArgs& a = w[g];
-        a.x = t.x, a.w = t.w, a.y = t.y;
-        a.B = t.B, a.Cin = t.Cin, a.Hin = t.Hin, a.Win = t.Win, a.Cout = t.Cout, a.Hout = t.Hout, a.Wout = t.Wout;
-        a.Mpad = t.Mpad, a.nM = t.nM, a.nN = t.nN, a.cpt = t.cpt;
-        a.N = t.N, a.fd_hw = t.fd_hw, a.fd_w = t.fd_w, a.pt = t.pt, a.ep = t.ep;
+        fill(a);
         const int nt = gt[g], sy = pt.sy;
         int rc;
 #define TCW(BM_, NT_, SY_, NS_)                                                                          \
@@ -609,9 +725,7 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         if (nt == 16) rc = TCW(64, 16, 2, 5);
         else if (nt == 9 && sy == 2) rc = bm == 128 ? TCW(128, 9, 2, 4) : TCW(64, 9, 2, 4);
         else if (nt == 9) rc = bm == 128 ? TCW(128, 9, 1, 2) : TCW(64, 9, 1, 2);
-        else if (nt == 4) rc = bm == 128 ? TCW(128, 4, 1, 2) : TCW(64, 4, 1, 2);
-        else if (nt == 2) rc = bm == 128 ? TCW(128, 2, 1, 2) : TCW(64, 2, 1, 2);
-        else rc = bm == 128 ? TCW(128, 1, 1, 2) : TCW(64, 1, 1, 2);
+        else rc = bm == 128 ? TCW(128, 4, 1, 2) : TCW(64, 4, 1, 2);
 #undef TCW
         if (rc) return rc;
     }
@@ -722,16 +836,21 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     hipStream_t s = st;
     // the window form where the geometry allows (LDM_TCONV_WIN=0: the per-chunk gather form, A/B timing).
     // 16-tap (4x4 stride-2) convs run it on 64-row tiles: their image needs five register slots per thread.
-    static const bool win = [] {
+    // LDM_TCONV_WIN: bit 0 the single-phase window forms, bit 1 the four-phase form of the k3 s2 op1 transposed
+    // convs (0 = the per-chunk gather form everywhere).  Default bit 0 only: in the train step (B = 32, bf16)
+    // 4.899 ms per step on the gather form, 4.823 with bit 0, 4.874 with both — the four-phase form won only on
+    // style_enc3's data gradient (85 -> 71 us) and lost 5-16 us on the other four (profiles/r04/tconv_window)
+    static const int win = [] {
         const char* e = std::getenv("LDM_TCONV_WIN");
-        return e ? std::atoi(e) != 0 : true;
+        return e ? (int)std::strtol(e, nullptr, 0) : 1;
     }();
     if (win) {
         const bool k16 = a.pt.nphase == 1 && a.pt.ntap[0] == 16;
-        if (!k16 || p.tm == 1 || a.Mpad % 64 == 0) {
+        const bool k3t = a.pt.nphase == 4 && a.pt.ntap[0] == 1 && a.pt.ntap[3] == 4;   // k3 s2 op1 transposed
+        if ((k3t && (win & 2)) || (!k3t && (win & 1))) {
             tc::TArgs t = a;
-            if (k16 && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
-            const int rc = tc::forward_window(d, t, k16 ? 64 : 64 * p.tm, p.tn, s);
+            if ((k16 || k3t) && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
+            const int rc = tc::forward_window(d, t, (k16 || k3t) ? 64 : 64 * p.tm, p.tn, s);
             if (rc != 1) return rc;
         }
     }

@@ -70,6 +70,7 @@ struct UArgs {
     int32_t B, Hin, Win, Hout, Wout;
     int32_t Hq, Wq, Nq;   // column grid: output pixels (conv) or input pixels (transposed)
     int32_t nMt, nNt, order;
+    int32_t xpm, xpn;     // order 2: the 8 XCDs as an xpm x xpn grid over (M tiles, N tiles), contiguous slices
     FastDiv fd_hw, fd_w, fd_mt, fd_nt, fd_tiles;
     float* slab;          // KS > 1: partial tiles [tile][KS][NFR][64] float4 (write-through)
     int32_t* cnt;         // KS > 1: arrival counter per tile (zero between launches)
@@ -172,9 +173,21 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
             ks = a.fd_tiles.div(bid);
             bid -= ks * (a.nMt * a.nNt);
         }
-        const int q1 = a.fd_mt.div(bid), q2 = a.fd_nt.div(bid);
-        mt = a.order == 0 ? bid - q1 * a.nMt : q2;
-        nt = a.order == 0 ? q1 : bid - q2 * a.nNt;
+        if (a.order == 2) {
+            // XCD-aware: tile T goes to XCD T % 8 (round-robin placement); XCD x = (xm, xn) owns the contiguous
+            // M-tile slice xm and N-tile slice xn, so it fetches 1/xpm of the weights and 1/xpn of the input
+            // (and the input rows a slice shares with its neighbour once)
+            const int x = bid & 7, l = bid >> 3;
+            const int xm = x / a.xpn, xn = x - xm * a.xpn;
+            const int mloc = a.nMt / a.xpm, nloc = a.nNt / a.xpn;
+            const int ln = l / mloc;
+            mt = xm * mloc + (l - ln * mloc);
+            nt = xn * nloc + ln;
+        } else {
+            const int q1 = a.fd_mt.div(bid), q2 = a.fd_nt.div(bid);
+            mt = a.order == 0 ? bid - q1 * a.nMt : q2;
+            nt = a.order == 0 ? q1 : bid - q2 * a.nNt;
+        }
     }
     const int m0 = mt * (16 * TM);
     const int nbase = nt * (16 * TN * WN) + wn * (16 * TN);
@@ -974,6 +987,14 @@ static bool window_taps() {
     }();
     return on;
 }
+// XCD-grid block order (order 2 in make_args); LDM_UCONV_XCD=0 turns it off for A/B timing
+static bool xcd_grid() {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_UCONV_XCD");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
 // EPI_PLANE instances where the geometry allows (LDM_UCONV_PLANE=0 turns them off for A/B timing)
 static bool plane_taps() {
     static const bool on = [] {
@@ -1072,6 +1093,19 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     // over every XCD's L2); activation-heavy ones walk M fastest
     const int64_t wbytes = (int64_t)9 * g.cin * g.cout * 4, xbytes = (int64_t)B * Hin * Win * g.cin * 4;
     a.order = wbytes > xbytes ? 0 : 1;
+    // XCD grid (order 2, LDM_UCONV_XCD=0 keeps orders 0 / 1): the split of the 8 XCDs over (M, N) tiles with
+    // the fewest bytes fetched into the eight L2s, xpn x weights + xpm x input (each XCD its weight and input
+    // slices; contiguous N slices share their halo rows); only where both tile counts divide
+    if (xcd_grid() && ((int64_t)a.nMt * a.nNt) % 8 == 0) {
+        int64_t best = -1;
+        for (int pm = 1; pm <= 8; pm *= 2) {
+            const int pn = 8 / pm;
+            if (a.nMt % pm || ((a.Nq + bn - 1) / bn) % pn) continue;
+            const int64_t est = pn * wbytes + pm * xbytes;
+            if (best < 0 || est < best) best = est, a.xpm = pm, a.xpn = pn;
+        }
+        if (best >= 0) a.order = 2;
+    }
     a.fd_hw = FastDiv::make(a.Hq * a.Wq);
     a.fd_w = FastDiv::make(a.Wq);
     a.fd_mt = FastDiv::make(a.nMt);
