@@ -57,6 +57,13 @@ enum {
  * with fp32 accumulation, fp32 epilogue and fp32 outputs / sampler state (the torch.autocast fp16 / bf16
  * regions of the train step and of a sampling loop; BASELINE configs 3 and 5). */
 enum { LDM_DT_F32 = 0, LDM_DT_F16 = 1, LDM_DT_BF16 = 2 };
+/* Or'ed into ldm_epilogue.dtype (with LDM_DT_F16 / LDM_DT_BF16): ATen's autocast OUTPUT semantics as well —
+ * the conv output, the eval-BN output, the activation and each add are rounded to that type (stored in the
+ * fp32 tensor), as the reference's conv / linear outputs are 16-bit tensors inside torch.autocast
+ * (train.py:174).  Or'ed into the act code of ldm_batchnorm_train_out / ldm_batchnorm_apply_out as
+ * LDM_ACT_ROUND_F16 / LDM_ACT_ROUND_BF16: the BatchNorm output likewise (a 16-bit input's BN output). */
+enum { LDM_DT_ROUND_OUT = 0x100 };
+enum { LDM_ACT_ROUND_F16 = LDM_DT_F16 << 8, LDM_ACT_ROUND_BF16 = LDM_DT_BF16 << 8 };
 
 typedef struct ldm_epilogue {
     const float* bias;      /* [Cout] or NULL                                                */
@@ -70,8 +77,8 @@ typedef struct ldm_epilogue {
     const float* skip_add;  /* [B,Cout,Hout,Wout] added after act (UNet skips, model.py:221) */
     float* act_out;         /* [B,Cout,Hout,Wout] or NULL: also store act(.) before the adds  */
                             /* (training: the activation's backward needs it)                */
-    int32_t dtype;          /* operand precision LDM_DT_* of the MFMA kernels (kinds 1 / 2): fp32, or */
-                            /* x and w rounded to fp16 / bf16 with fp32 accumulation (autocast)     */
+    int32_t dtype;          /* operand precision LDM_DT_* of the conv kernels: fp32, or x and w rounded */
+                            /* to fp16 / bf16 with fp32 accumulation (autocast); | LDM_DT_ROUND_OUT */
 } ldm_epilogue;
 
 typedef struct ldm_conv_plan {

@@ -176,7 +176,10 @@ struct EpiArgs {
     float* ddim_x;
     float* ddim_x0_log;
     float* ddim_eps_log;
-    int32_t lowp;   // operand precision LDM_DT_* (MFMA kernels)
+    int32_t lowp;   // operand precision LDM_DT_* (MFMA kernels; the VALU conv kernels round their operands too)
+    // LDM_DT_F16 / LDM_DT_BF16: round the conv output, the eval-BN output, the activation and each add to that
+    // type, as ATen's autocast does (its conv / linear outputs are 16-bit tensors); 0: fp32 outputs
+    int32_t round_out;
 };
 
 // conv.hip: implicit-GEMM conv with the full internal epilogue (incl. the fused DDIM update); y may be
@@ -251,6 +254,13 @@ __device__ __forceinline__ float ddim_update(float xv, float e, const float* coe
     const float nc = eta * (dxn - dxt);   // noise_contribution
     const float t1 = san * x0;
     return (t1 + dxn) + nc;
+}
+
+// v rounded to a 16-bit type (LDM_DT_F16 / LDM_DT_BF16, round to nearest even), or unchanged (0)
+__device__ __forceinline__ float round16(float v, int mode) {
+    if (mode == LDM_DT_F16) return (float)(_Float16)v;
+    if (mode == LDM_DT_BF16) return (float)(__bf16)v;
+    return v;
 }
 
 __device__ __forceinline__ float apply_act(float v, int act) {

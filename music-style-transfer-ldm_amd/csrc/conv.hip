@@ -258,18 +258,20 @@ __device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx
     a.y[oidx] = v < 0.f ? 0.f : v;
     return;
 #endif
+    const int ro = e.round_out;   // autocast output semantics (EpiArgs::round_out): 0 leaves every value as is
     if (e.bias || e.pos_bias) v = v + p.bias;
+    v = round16(v, ro);
     if (e.bn_w) {
         // aten batch_norm_cpu_collect_linear_and_constant_terms: alpha = invstd*w, beta = b - mean*alpha
         const float invstd = 1.0f / sqrtf(e.bn_v[m] + e.bn_eps);
         const float alpha = invstd * e.bn_w[m];
         const float beta = e.bn_b[m] - e.bn_m[m] * alpha;
-        v = v * alpha + beta;
+        v = round16(v * alpha + beta, ro);
     }
-    v = apply_act(v, e.act);
+    v = round16(apply_act(v, e.act), ro);
     if (e.act_out) e.act_out[oidx] = v;
-    if (e.bcast) v = v + p.bcast;
-    if (e.skip) v = v + p.skip;
+    if (e.bcast) v = round16(v + p.bcast, ro);
+    if (e.skip) v = round16(v + p.skip, ro);
     if (e.ddim_coef) {
         float x0;
         e.ddim_x[oidx] = ddim_update(p.x, v, e.ddim_coef, e.ddim_eta, x0);
@@ -887,9 +889,9 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
         const float* wq = wb + (size_t)ci * wci;
         float xv[kMaxTap], wv[kMaxTap];
 #pragma unroll
-        for (int t = 0; t < kMaxTap; ++t) {
-            xv[t] = t < nt ? xp[off[t]] : 0.f;
-            wv[t] = t < nt ? wq[wkk[t]] : 0.f;
+        for (int t = 0; t < kMaxTap; ++t) {   // (operands rounded to the autocast type, as the MFMA kernels do)
+            xv[t] = round16(t < nt ? xp[off[t]] : 0.f, a.ep.lowp);
+            wv[t] = round16(t < nt ? wq[wkk[t]] : 0.f, a.ep.lowp);
         }
 #pragma unroll
         for (int t = 0; t < kMaxTap; ++t)
@@ -903,7 +905,7 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
 // Cout x k*k weights in LDS; the stores stay coalesced (consecutive lanes = consecutive ox per channel).
 __global__ __launch_bounds__(256) void conv_cin1_kernel(ConvArgs a) {
     __shared__ float ws[64 * 16];
-    for (int i = threadIdx.x; i < a.Cout * a.KK; i += blockDim.x) ws[i] = a.w[i];   // [co][kh*kw]
+    for (int i = threadIdx.x; i < a.Cout * a.KK; i += blockDim.x) ws[i] = round16(a.w[i], a.ep.lowp);   // [co][kh*kw]
     __syncthreads();
     const int total = a.B * a.Hout * a.Wout;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -921,7 +923,7 @@ __global__ __launch_bounds__(256) void conv_cin1_kernel(ConvArgs a) {
         const int iy = oy * a.pt.sy + a.pt.dy[0][t];
         const int ix = ox * a.pt.sy + a.pt.dx[0][t];
         ok[t] = t < nt && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-        xv[t] = xb[ok[t] ? iy * a.Win + ix : 0];
+        xv[t] = round16(xb[ok[t] ? iy * a.Win + ix : 0], a.ep.lowp);
     }
     for (int co = 0; co < a.Cout; ++co) {
         float acc = 0.f;
@@ -954,9 +956,11 @@ __device__ __forceinline__ ChanEpi chan_epi(const ConvArgs& a, int m) {
     return c;
 }
 __device__ __forceinline__ float chan_apply(const ConvArgs& a, const ChanEpi& c, float v) {
+    const int ro = a.ep.round_out;
     if (a.ep.bias) v = v + c.bias;
-    if (a.ep.bn_w) v = v * c.alpha + c.beta;
-    return apply_act(v, a.ep.act);
+    v = round16(v, ro);
+    if (a.ep.bn_w) v = round16(v * c.alpha + c.beta, ro);
+    return round16(apply_act(v, a.ep.act), ro);
 }
 __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float (&v)[4]) {
     const float4 t = make_float4(v[0], v[1], v[2], v[3]);
@@ -971,7 +975,7 @@ template <int K>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
     __shared__ ChanEpi es[64];   // per-channel epilogue constants, formed once per block (not per lane and channel)
-    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = a.w[i];   // [co][ky*K + kx]
+    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = round16(a.w[i], a.ep.lowp);   // [co][ky*K + kx]
     for (int i = threadIdx.x; i < a.Cout; i += blockDim.x) es[i] = chan_epi(a, i);
     __syncthreads();
     const int W4 = a.Wout >> 2;
@@ -994,7 +998,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         for (int c = 0; c < NC; ++c) {
             const int ix = ix0 + c;
             const bool ok = rok && (unsigned)ix < (unsigned)a.Win;
-            win[ky][c] = ok ? xb[iy * a.Win + ix] : 0.f;
+            win[ky][c] = round16(ok ? xb[iy * a.Win + ix] : 0.f, a.ep.lowp);
         }
     }
     const size_t plane = (size_t)a.Hout * a.Wout;
@@ -1049,7 +1053,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = (rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f;
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16((rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f, a.ep.lowp);
         const float* wq = a.w + ci * 16;   // w [Cin][1][4][4]
 #pragma unroll
         for (int ry = 0; ry < 2; ++ry)
@@ -1059,7 +1063,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
                 for (int t = 0; t < 4; ++t) {
                     const int ia = t >> 1, ib = t & 1;
                     const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                    const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+                    const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj)
                         acc[ry][2 * jj + rx] = fmaf(xr[1 + dy][1 + jj + dx], w, acc[ry][2 * jj + rx]);
@@ -1111,6 +1115,8 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
             xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
             xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
             xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], a.ep.lowp);
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1124,7 +1130,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
                     for (int t = 0; t < 4; ++t) {
                         const int ia = t >> 1, ib = t & 1;
                         const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                        const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
 #pragma unroll
                         for (int jj = 0; jj < 4; ++jj)
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
@@ -1195,6 +1201,8 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
             xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
             xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
             xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], a.ep.lowp);
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1208,7 +1216,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
                     for (int t = 0; t < 4; ++t) {
                         const int ia = t >> 1, ib = t & 1;
                         const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                        const float w = wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)];
+                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
 #pragma unroll
                         for (int jj = 0; jj < 4; ++jj)
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
@@ -1684,8 +1692,10 @@ extern "C" int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* 
         e.bcast = ep->bcast_add;
         e.skip = ep->skip_add;
         e.act_out = ep->act_out;
-        e.lowp = ep->dtype;
-        LDM_REQUIRE(e.lowp >= LDM_DT_F32 && e.lowp <= LDM_DT_BF16, "conv forward: unknown operand precision");
+        e.lowp = ep->dtype & 0xff;
+        LDM_REQUIRE(e.lowp >= LDM_DT_F32 && e.lowp <= LDM_DT_BF16 && (ep->dtype & ~(0xff | LDM_DT_ROUND_OUT)) == 0,
+                    "conv forward: unknown operand precision");
+        e.round_out = (ep->dtype & LDM_DT_ROUND_OUT) ? e.lowp : 0;
     }
     return conv_forward_ex(*d, *plan, x, w, e, y, workspace, (hipStream_t)stream);
 }

@@ -192,11 +192,12 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, fl
     const float alpha = invstd * (weight ? weight[c] : 1.0f);
     const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    const int ro = act >> 8, ac = act & 0xff;   // LDM_ACT_ROUND_*: the output of a 16-bit input's BN (autocast)
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float v[W];
         ld<W>(src + o, v);
 #pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = apply_act(bn_affine(v[j], alpha, beta), act);
+        for (int j = 0; j < W; ++j) v[j] = apply_act(round16(bn_affine(v[j], alpha, beta), ro), ac);
         st<W>(x + o, v);
     });
     if (k == 0 && threadIdx.x == 0) {

@@ -241,13 +241,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
                 if (co >= a.Cout) continue;
                 float v = acc[i][j][q];
                 if (e.bias) v = v + e.bias[co];
+                v = round16(v, e.round_out);   // (autocast output semantics; 0: unchanged)
                 if (e.bn_w) {   // as epi_finish (conv.hip)
                     const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
                     const float alpha = invstd * e.bn_w[co];
                     const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-                    v = v * alpha + beta;
+                    v = round16(v * alpha + beta, e.round_out);
                 }
-                v = apply_act(v, e.act);
+                v = round16(apply_act(v, e.act), e.round_out);
                 const size_t o = obase + (size_t)co * a.Hout * a.Wout;
                 if (e.act_out) e.act_out[o] = v;
                 a.y[o] = v;
@@ -458,13 +459,14 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     const EpiArgs& e = a.ep;
     auto epi = [&](float v, int co) {
         if (e.bias) v = v + e.bias[co];
+        v = round16(v, e.round_out);   // (autocast output semantics; 0: unchanged)
         if (e.bn_w) {   // as epi_finish (conv.hip)
             const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
             const float alpha = invstd * e.bn_w[co];
             const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-            v = v * alpha + beta;
+            v = round16(v * alpha + beta, e.round_out);
         }
-        return apply_act(v, e.act);
+        return round16(apply_act(v, e.act), e.round_out);
     };
     if constexpr (NT == 4) {
         // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values

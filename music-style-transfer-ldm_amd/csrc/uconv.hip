@@ -699,19 +699,21 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
         if (!ot.ok) return;
         const floatx4 bias = pre_b[k];
         floatx4 o;
+        // 16-bit operands (a sampling loop inside torch.autocast): the conv output and each add rounded to that
+        // type as well, as the reference's autocast convs return 16-bit tensors; the DDIM update stays fp32
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float sv = v[r] + bias[r];
+            float sv = round16(v[r] + bias[r], DT);
             if (EPI & EPI_RELU) sv = sv < 0.f ? 0.f : sv;
             o[r] = sv;
         }
         if constexpr ((EPI & EPI_BCAST) != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = o[r] + pre_c[k][r];
+            for (int r = 0; r < 4; ++r) o[r] = round16(o[r] + pre_c[k][r], DT);
         }
         if constexpr ((EPI & EPI_SKIP) != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = o[r] + pre_s[k][r];
+            for (int r = 0; r < 4; ++r) o[r] = round16(o[r] + pre_s[k][r], DT);
         }
         if constexpr (ROLE == ROLE_CONSUMER) {
             if (poison) o = floatx4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};

@@ -61,6 +61,7 @@ class UNetWeights(ctypes.Structure):
 
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
+DT_ROUND_OUT = 0x100   # ldm_epilogue.dtype flag (ldm_capi.h LDM_DT_ROUND_OUT); act codes: LDM_ACT_ROUND_* = dt << 8
 
 # name -> (restype, argtypes).  Kept in one table so tests can check it against include/ldm_capi.h.
 SIGNATURES = {

@@ -6,6 +6,7 @@ backward kernels (ldm_amd.backward); a missing backward raises instead of silent
 """
 import torch
 
+from . import _lib as L
 from . import ops
 
 _BACKWARD = {}   # name -> callable(ctx, *grad_outputs) registered by ldm_amd.backward
@@ -80,6 +81,7 @@ def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0
         dt = ops.autocast_dt()
         y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, dtype=dt, **cfg)
         store["dtype"] = dt      # the backward convs run at the forward's autocast precision
+        store["round"] = bool(ops.autocast_out(dt) & L.DT_ROUND_OUT)   # ... and output semantics
         store["cfg"] = cfg
         store["bn"] = bn_eval
         store["wkey"] = wkey
@@ -112,7 +114,8 @@ def _conv_backward(ctx, gy):
             _, gb, _ = ops.act_backward(gv, "none", need_dv=False, need_bias=True)
     desc = _conv_desc(x, w, cfg)
     dt = ctx.store.get("dtype", 0)
-    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt) if nx else None
+    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt, round_out=ctx.store.get("round", False)) \
+        if nx else None
     gw = ops.conv_backward_weight(x, gv, desc, dtype=dt) if nw else None
     if gbc is not None:
         gbc = gbc.reshape(ctx.store["bc_shape"])
@@ -132,6 +135,7 @@ def in_proj(q_nchw, kv_nchw, ipw, ipb):
         q = ops.conv_forward(q_, wq, b_[:E], stride=1, padding=0, wkey=(ipw, "q"), dtype=dt)
         kv = ops.conv_forward(kv_, wkv, b_[E:], stride=1, padding=0, wkey=(ipw, "kv"), dtype=dt)
         store["dtype"] = dt
+        store["round"] = bool(ops.autocast_out(dt) & L.DT_ROUND_OUT)
         store["owner"] = ipw        # the packed-weight caches are keyed on the parameter itself
         store["saved"] = (q_, kv_, w_)
         return q, kv
@@ -154,8 +158,8 @@ def _in_proj_backward(ctx, gq, gkv):
                                                                   output_padding=0))
         if nb:
             ops.act_backward(g, "none", need_dv=False, need_bias=True, db_out=gb[lo:hi])
-        grads.append(ops.conv_backward_data(g, w[lo:hi].view(hi - lo, E, 1, 1), desc, (owner, tag), dtype=dt)
-                     if nx else None)
+        grads.append(ops.conv_backward_data(g, w[lo:hi].view(hi - lo, E, 1, 1), desc, (owner, tag), dtype=dt,
+                                            round_out=ctx.store.get("round", False)) if nx else None)
         if nw:
             ops.conv_backward_weight(x, g, desc, dw=gw[lo:hi].view(hi - lo, E, 1, 1), dtype=dt)
     return grads[0], grads[1], gw, gb

@@ -279,7 +279,7 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
     ep = L.Epilogue()
     ep.bias = _p(bias)
-    ep.dtype = dt
+    ep.dtype = autocast_out(dt)
     keep = []
     if bn is not None:
         g, b_, m, v, eps = bn
@@ -302,6 +302,20 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     L.call("ldm_conv_forward_ws", byref(desc), byref(plan), x.data_ptr(), _p(wbuf), byref(ep), y.data_ptr(),
            split_workspace(plan, x.device), stream_handle())
     return y
+
+
+def autocast_out(dt, round_out=None):
+    """The ldm_epilogue.dtype bits for operand precision dt.  round_out=None: inside a torch.autocast region
+    (and dt != 0) the outputs are rounded to dt as well (LDM_DT_ROUND_OUT), as ATen's autocast conv / linear /
+    BatchNorm return 16-bit tensors (the reference's train step, train.py:174); outside one (explicit-dtype
+    kernel calls) operands only.  True / False force it (the backward passes what its forward did).
+    LDM_AMD_AUTOCAST_OUT=0: operands only everywhere (rounds 1-3)."""
+    dt = int(dt)
+    if round_out is None:
+        round_out = torch.is_autocast_enabled("cuda")
+    if dt and round_out and os.environ.get("LDM_AMD_AUTOCAST_OUT", "1") != "0":
+        return dt | L.DT_ROUND_OUT
+    return dt
 
 
 def autocast_dt(device_type="cuda"):
@@ -328,15 +342,16 @@ def dual_desc(desc):
     return d
 
 
-def conv_backward_data(dy, weight, desc, wkey=None, dtype=0):
+def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False):
     """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc);
-    dtype = LDM_DT_* operand precision (the forward's autocast precision)."""
+    dtype = LDM_DT_* operand precision (the forward's autocast precision); round_out: dX rounded to it as well
+    (the reference's data gradient of a 16-bit conv is a 16-bit tensor)."""
     dd = dual_desc(desc)
     plan = tiled_plan(dd, int(dtype)) or get_plan(dd)
     wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
     dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
     ep = L.Epilogue()
-    ep.dtype = int(dtype)
+    ep.dtype = autocast_out(dtype, round_out)
     L.call("ldm_conv_forward_ws", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), byref(ep), dx.data_ptr(),
            split_workspace(plan, dy.device), stream_handle())
     return dx
@@ -505,10 +520,14 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
         sm = torch.empty(C, device=x.device, dtype=torch.float32)
         si = torch.empty(C, device=x.device, dtype=torch.float32)
     ws = reduce_workspace(B, C, H * W, x.device)
+    # inside an autocast region the BN output is rounded like the 16-bit output of the reference's BatchNorm on
+    # a 16-bit conv output (LDM_ACT_ROUND_*: the activation code's high bits)
+    rdt = autocast_out(autocast_dt())
+    act_code = L.ACT[act] | (((rdt & 0xff) << 8) if rdt & L.DT_ROUND_OUT else 0)
     pg = _sync_group(sync)
     if pg is None:
         L.call("ldm_batchnorm_train_out", x.data_ptr(), y.data_ptr(), B, C, H * W, _p(weight), _p(bias),
-               _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
+               _p(running_mean), _p(running_var), float(momentum), float(eps), act_code, _p(sm), _p(si),
                ws.data_ptr(), stream_handle())
     else:
         # SyncBatchNorm (torch.nn.SyncBatchNorm semantics): fp64 (sum x, sum x^2, count) all-reduced over the
@@ -521,7 +540,7 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
         L.call("ldm_batchnorm_stats", xp, B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
         _allreduce_sum(stats, pg.pg)
         L.call("ldm_batchnorm_apply_out", xp, yp, B, C, H * W, stats.data_ptr(), -1.0, _p(weight), _p(bias),
-               _p(running_mean), _p(running_var), float(momentum), float(eps), L.ACT[act], _p(sm), _p(si),
+               _p(running_mean), _p(running_var), float(momentum), float(eps), act_code, _p(sm), _p(si),
                stream_handle())
     return (sm, si) if save else None
 

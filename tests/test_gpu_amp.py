@@ -2,8 +2,9 @@
 against the reference run under torch.autocast("cpu", dtype) (tests/golden/make_goldens.py --amp).
 
 Our loop under torch.autocast("cuda", dtype) rounds every step-kernel operand (activations and weights) to
-fp16 / bf16 and accumulates, applies the epilogue and updates the sampler state in fp32; the reference
-rounds operands AND outputs of each conv / linear / attention matmul.  Both differ from the fp32 loop
+fp16 / bf16, accumulates in fp32 and (round 4) rounds each conv output and skip / time-embedding add to the
+16-bit type as the reference's autocast convs do, while the sampler state stays fp32; the reference also rounds
+its attention matmuls (ours keep them fp32: the folded cross-attentions).  Both differ from the fp32 loop
 by a few x 1e-4 (fp16) / 1e-3 (bf16) relative; the stated tolerances (max-norm relative, against the
 autocast golden) are 1e-3 for fp16 and 8e-3 for bf16, about 3x the reference's own autocast-vs-fp32 gap.
 Reference: model.py:409-465 (DDIM loop), :503-559 (content-style loop).
@@ -57,6 +58,8 @@ def test_ddim10_autocast(ldm, gamp, cuda, name):
     assert x.dtype == torch.float32
     assert logs["timesteps"] == gamp[f"amp10_{name}_times"].tolist()
     err = rel_err(npy(x), gamp[f"amp10_{name}_x"])
+    print(f"ours vs reference {name} {err:.2e}; reference {name} vs fp32 "
+          f"{rel_err(gamp[f'amp10_{name}_x'], gamp['amp10_fp32_x']):.2e}")
     assert err < TOLS[name], err
     # and it really ran at reduced precision: farther from the fp32 golden than the fp32 path's 1e-5
     assert rel_err(npy(x), gamp["amp10_fp32_x"]) > 1e-5
@@ -75,6 +78,7 @@ def test_content_style_100_fp16(ldm, gamp, cuda):
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
         x, _ = ldm.content_style_ddim_sample(zT, emb, timesteps=100, eta=1.0)
     err = rel_err(npy(x), gamp["cs100_fp16_x"])
+    print(f"ours vs reference fp16 {err:.2e}; reference fp16 vs fp32 {rel_err(gamp['cs100_fp16_x'], gamp['cs100_fp32_x']):.2e}")
     assert err < TOLS["fp16"], err
 
 
@@ -126,8 +130,11 @@ def test_content_style_100_fp16_b8(ldm, gamp8, cuda, path):
                                                for k in ((False, True) if l in (4, 5) else (False,))])
 def test_step_layer_lowp(cuda, name, layer, ksplit):
     """One step-kernel layer at fp16 / bf16 operands (weights packed in 16 bits, ldm_step_pack_weight_dt) ==
-    float64 conv of the operands rounded the same way (accumulation order aside: 1e-5), bias / ReLU / skip in
-    fp32; single-block and K-split forms."""
+    float64 conv of the operands rounded the same way, with the autocast output semantics: the conv output
+    (+ bias) and the skip add rounded to the 16-bit type (ReLU exact).  Accumulation order aside, each output
+    is within one ulp of the 16-bit type of the float64 value rounded the same way (a sum that lands within
+    fp32 noise of a 16-bit rounding boundary may round either way), and almost all are equal; single-block and
+    K-split forms."""
     import torch.nn.functional as F
     from ldm_amd import _lib as L
     LAYERS = [(32, 64, 0, 1), None, None, None, (512, 512, 0, 8), (512, 256, 2, 8)]
@@ -162,11 +169,16 @@ def test_step_layer_lowp(cuda, name, layer, ksplit):
     x64, w64 = rnd(x), rnd(w)
     ref = F.conv_transpose2d(x64, w64, stride=2, padding=1, output_padding=1) if mode == 2 else \
         F.conv2d(x64, w64, padding=1)
-    ref = ref + (bias.double().permute(2, 0, 1)[None] if posb else bias.double()[None, :, None, None])
+    ref = rnd(ref + (bias.double().permute(2, 0, 1)[None] if posb else bias.double()[None, :, None, None]))
     ref = ref.clamp_min(0)
     if sk is not None:
-        ref = ref + sk.double()
-    assert rel_err(npy(y.permute(0, 3, 1, 2)), ref.numpy()) < 1e-5
+        ref = rnd(ref + sk.double())
+    got = torch.from_numpy(npy(y.permute(0, 3, 1, 2)))
+    ulp = 2.0 ** -10 if name == "fp16" else 2.0 ** -7     # one ulp, relative to the value (upper bound)
+    diff = (got - ref).abs()
+    # two roundings (conv output, skip add): at most two ulps of the larger magnitude
+    assert bool((diff <= 2 * ulp * torch.maximum(ref.abs(), got.abs()) + 1e-30).all()), float(diff.max())
+    assert float((diff > 0).double().mean()) < 0.01       # (boundary cases only)
 
 
 TRAIN_GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",

@@ -13,7 +13,8 @@ the step's own gradients from the snapshot of the moments taken before it).
 Tolerances: fp32 (LDM_AMD_DTYPE=fp32, the bench's --dtype fp32): against float64 of the same step,
 max|y - y64| <= max(1e-4, 3 e32) max|y64|, e32 = the reference's own fp32-vs-float64 distance (north_star's
 1e-4, widened only where the reference's fp32 itself sits further out: 1.7e-4 on unet.enc1.weight).  bf16 (the bench default): per quantity within 2 e + 1e-3 of both the fp32 and the bf16
-reference, e = the reference's own bf16-vs-fp32 distance (the rule of test_gpu_amp.py).
+reference, e = the reference's own bf16-vs-fp32 distance (the rule of test_gpu_amp.py), tightened in round 4 with
+the autocast output semantics to 1.5 e + 1e-4 of the bf16 reference and 2 e + 1e-4 of the fp32 one.
 
 test_config3_every_conv_instance re-runs every conv forward / data-gradient / weight-gradient call of one
 bf16 step at its B=32 geometry (whatever kernel instance the plan picks: tconv_kernel, conv_mfma_kernel,
@@ -120,7 +121,11 @@ def test_config3_graphed_step_matches_reference(g3, cuda, dtype, monkeypatch):
             e = rel_err(bf, f32)
             tobf = rel_err(np.asarray(ours).reshape(np.shape(bf)), bf)
             rows.append(f"{name}: ref bf16-vs-fp32 {e:.2e}, ours-vs-fp32 {to32:.2e}, ours-vs-bf16 {tobf:.2e}")
-            if to32 > 2 * e + 1e-3 or tobf > 2 * e + 1e-3:
+            # with the autocast output semantics (16-bit conv / BN outputs, LDM_DT_ROUND_OUT) ours sits within
+            # 1.5 e + 1e-4 of the reference's bf16 step (round 3, operands only: 2 e + 1e-3) and within
+            # 2 e + 1e-4 of its fp32 step; measured: 12 of 14 quantities within e of the bf16 reference,
+            # decoder.decoder.6.weight at 1.41 e and style_encoder.enc6.bias at 1.07 e (profiles/r04/autocast)
+            if to32 > 2 * e + 1e-4 or tobf > 1.5 * e + 1e-4:
                 bad.append(name)
     print("\n".join(rows))
     assert not bad, (bad, rows)
@@ -171,9 +176,9 @@ class _Recorder:
                 add("fwd", d, dt, (kw.get("bcast") is not None, kw.get("skip") is not None))
             return y
 
-        def conv_backward_data(dy, weight, desc, wkey=None, dtype=0):
+        def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False):
             add("dgrad", desc, dtype)
-            return dgrad(dy, weight, desc, wkey, dtype)
+            return dgrad(dy, weight, desc, wkey, dtype, round_out)
 
         def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
             add("wgrad", desc, dtype)
