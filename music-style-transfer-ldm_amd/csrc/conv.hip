@@ -941,6 +941,22 @@ __global__ __launch_bounds__(256) void conv_cin1_kernel(ConvArgs a) {
 // routes anything else to the kernels above); arithmetic and accumulation order equal conv_cin1_kernel /
 // conv_direct_kernel's, so the results are the same bits.
 // ------------------------------------------------------------------------------------------------
+// the operand / output rounding modes of EpiArgs as compile-time constants: f(lp, ro) with integral_constants,
+// ro in {0, lp} (round_out is either off or the operand type)
+template <class F>
+static void lp_dispatch(const EpiArgs& e, F&& f) {
+    using Z = std::integral_constant<int, 0>;
+    using H = std::integral_constant<int, LDM_DT_F16>;
+    using Bf = std::integral_constant<int, LDM_DT_BF16>;
+    if (e.lowp == LDM_DT_BF16) {
+        if (e.round_out) f(Bf{}, Bf{}); else f(Bf{}, Z{});
+    } else if (e.lowp == LDM_DT_F16) {
+        if (e.round_out) f(H{}, H{}); else f(H{}, Z{});
+    } else {
+        f(Z{}, Z{});
+    }
+}
+
 struct ChanEpi {
     float bias, alpha, beta;
 };
@@ -955,8 +971,11 @@ __device__ __forceinline__ ChanEpi chan_epi(const ConvArgs& a, int m) {
     }
     return c;
 }
+// RO: the output rounding (a.ep.round_out) as a template argument, so that the VALU kernels below carry no
+// per-element mode test (they do a few FMAs per output; a runtime round16 costs as much as the conv)
+template <int RO>
 __device__ __forceinline__ float chan_apply(const ConvArgs& a, const ChanEpi& c, float v) {
-    const int ro = a.ep.round_out;
+    constexpr int ro = RO;
     if (a.ep.bias) v = v + c.bias;
     v = round16(v, ro);
     if (a.ep.bn_w) v = round16(v * c.alpha + c.beta, ro);
@@ -971,11 +990,11 @@ __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float 
 // Cin = 1, stride 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
 // 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (6 + K) input window in registers,
 // every output channel from it, weights in LDS.
-template <int K>
+template <int K, int LP, int RO>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
     __shared__ ChanEpi es[64];   // per-channel epilogue constants, formed once per block (not per lane and channel)
-    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = round16(a.w[i], a.ep.lowp);   // [co][ky*K + kx]
+    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = round16(a.w[i], LP);   // [co][ky*K + kx]
     for (int i = threadIdx.x; i < a.Cout; i += blockDim.x) es[i] = chan_epi(a, i);
     __syncthreads();
     const int W4 = a.Wout >> 2;
@@ -998,7 +1017,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         for (int c = 0; c < NC; ++c) {
             const int ix = ix0 + c;
             const bool ok = rok && (unsigned)ix < (unsigned)a.Win;
-            win[ky][c] = round16(ok ? xb[iy * a.Win + ix] : 0.f, a.ep.lowp);
+            win[ky][c] = round16(ok ? xb[iy * a.Win + ix] : 0.f, LP);
         }
     }
     const size_t plane = (size_t)a.Hout * a.Wout;
@@ -1016,7 +1035,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         const ChanEpi ce = es[co];
         float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[j]);
+        for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[j]);
         store4(a, o, v);
     }
 }
@@ -1028,6 +1047,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
 __host__ __device__ constexpr int ct4_tap(int r, int i) { return r == 0 ? (i == 0 ? 1 : 3) : (i == 0 ? 0 : 2); }
 __host__ __device__ constexpr int ct4_off(int r, int i) { return (r + 1 - ct4_tap(r, i)) >> 1; }
 
+template <int LP, int RO>
 __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
     const int W4 = a.Win >> 2;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1053,7 +1073,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16((rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f, a.ep.lowp);
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16((rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f, LP);
         const float* wq = a.w + ci * 16;   // w [Cin][1][4][4]
 #pragma unroll
         for (int ry = 0; ry < 2; ++ry)
@@ -1063,7 +1083,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
                 for (int t = 0; t < 4; ++t) {
                     const int ia = t >> 1, ib = t & 1;
                     const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                    const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
+                    const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], LP);
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj)
                         acc[ry][2 * jj + rx] = fmaf(xr[1 + dy][1 + jj + dx], w, acc[ry][2 * jj + rx]);
@@ -1077,7 +1097,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
         for (int h = 0; h < 2; ++h) {
             float v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[ry][4 * h + j]);
+            for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[ry][4 * h + j]);
             store4(a, o + 4 * h, v);
         }
     }
@@ -1086,6 +1106,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
 // The same layer with two input rows per lane (four output rows x 8 columns): per input channel a lane
 // reads its four window rows as one 16-byte run plus the two border columns (12 loads for two rows instead
 // of 36 single-float gathers), and the channel loop keeps two channels of loads in flight.  Hin even.
+template <int LP, int RO>
 __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
     const int W4 = a.Win >> 2, H2 = a.Hin >> 1;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1116,7 +1137,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
             xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
             xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], a.ep.lowp);
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1130,7 +1151,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
                     for (int t = 0; t < 4; ++t) {
                         const int ia = t >> 1, ib = t & 1;
                         const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
+                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], LP);
 #pragma unroll
                         for (int jj = 0; jj < 4; ++jj)
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
@@ -1158,7 +1179,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
             for (int h = 0; h < 2; ++h) {
                 float v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[u][ry][4 * h + j]);
+                for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[u][ry][4 * h + j]);
                 store4(a, o + 4 * h, v);
             }
         }
@@ -1168,6 +1189,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
 // quarter g * Cin / 4 .. of the channels for the 64 tiles of its block, then the quarters meet in LDS in wave
 // order.  At B = 32 the two-rows-per-lane kernel has 65,536 lanes, one 4-wave block per CU walking all 64
 // channels in a chain of dependent loads (119 us per launch); here 4x the waves walk a quarter each.
+template <int LP, int RO>
 __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
     __shared__ float part[3][32][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -1202,7 +1224,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
             xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
             xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], a.ep.lowp);
+            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1216,7 +1238,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
                     for (int t = 0; t < 4; ++t) {
                         const int ia = t >> 1, ib = t & 1;
                         const int dy = ct4_off(ry, ia), dx = ct4_off(rx, ib);
-                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], a.ep.lowp);
+                        const float w = round16(wq[ct4_tap(ry, ia) * 4 + ct4_tap(rx, ib)], LP);
 #pragma unroll
                         for (int jj = 0; jj < 4; ++jj)
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
@@ -1267,7 +1289,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
             for (int h = 0; h < 2; ++h) {
                 float v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = chan_apply(a, ce, acc[u][ry][4 * h + j]);
+                for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[u][ry][4 * h + j]);
                 store4(a, o + 4 * h, v);
             }
         }
@@ -1609,10 +1631,15 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             ((uintptr_t)y & 15) == 0 && (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Wout / 4);
             const int64_t lanes = (int64_t)d.B * d.Hout * (d.Wout / 4);
-            if (d.kh == 3)
-                hipLaunchKernelGGL(conv_cin1_x4_kernel<3>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
-            else
-                hipLaunchKernelGGL(conv_cin1_x4_kernel<4>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+            lp_dispatch(a.ep, [&](auto lp, auto ro) {
+                constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
+                if (d.kh == 3)
+                    hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
+                                       st, a);
+                else
+                    hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
+                                       st, a);
+            });
             LDM_CHECK_LAUNCH("conv_cin1_x4_kernel");
             return 0;
         }
@@ -1627,20 +1654,29 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             if (d.Hin % 2 == 0 && d.Cin % 8 == 0 && split) {
                 a.fd_dho = FastDiv::make(d.Hin / 2);
                 const int64_t tiles = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
-                hipLaunchKernelGGL(convT4_cout1_r2s_kernel, dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0, st, a);
+                lp_dispatch(a.ep, [&](auto lp, auto ro) {
+                    hipLaunchKernelGGL((convT4_cout1_r2s_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0,
+                                       st, a);
+                });
                 LDM_CHECK_LAUNCH("convT4_cout1_r2s_kernel");
                 return 0;
             }
             if (d.Hin % 2 == 0) {
                 a.fd_dho = FastDiv::make(d.Hin / 2);
                 const int64_t lanes = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
-                hipLaunchKernelGGL(convT4_cout1_r2_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+                lp_dispatch(a.ep, [&](auto lp, auto ro) {
+                    hipLaunchKernelGGL((convT4_cout1_r2_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
+                                       st, a);
+                });
                 LDM_CHECK_LAUNCH("convT4_cout1_r2_kernel");
                 return 0;
             }
             a.fd_dho = FastDiv::make(d.Hin);
             const int64_t lanes = (int64_t)d.B * d.Hin * (d.Win / 4);
-            hipLaunchKernelGGL(convT4_cout1_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+            lp_dispatch(a.ep, [&](auto lp, auto ro) {
+                    hipLaunchKernelGGL((convT4_cout1_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
+                                       st, a);
+                });
             LDM_CHECK_LAUNCH("convT4_cout1_kernel");
             return 0;
         }

@@ -222,6 +222,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 
     // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store
     const EpiArgs& e = a.ep;
+    const bool ro = e.round_out != 0;   // a select per value: DT is known here, the mode test is not per value
+    auto rnd = [ro](float v) { return ro ? round16(v, DT) : v; };
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int64_t n = n0 + wn * 64 + 32 * j + r;
@@ -241,14 +243,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
                 if (co >= a.Cout) continue;
                 float v = acc[i][j][q];
                 if (e.bias) v = v + e.bias[co];
-                v = round16(v, e.round_out);   // (autocast output semantics; 0: unchanged)
+                v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
                 if (e.bn_w) {   // as epi_finish (conv.hip)
                     const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
                     const float alpha = invstd * e.bn_w[co];
                     const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-                    v = round16(v * alpha + beta, e.round_out);
+                    v = rnd(v * alpha + beta);
                 }
-                v = round16(apply_act(v, e.act), e.round_out);
+                v = rnd(apply_act(v, e.act));
                 const size_t o = obase + (size_t)co * a.Hout * a.Wout;
                 if (e.act_out) e.act_out[o] = v;
                 a.y[o] = v;
@@ -457,16 +459,18 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
 
     // ---- epilogue: bias -> eval-BN -> act (-> act_out)
     const EpiArgs& e = a.ep;
+    const bool ro = e.round_out != 0;   // a select per value: DT is known here, the mode test is not per value
+    auto rnd = [ro](float v) { return ro ? round16(v, DT) : v; };
     auto epi = [&](float v, int co) {
         if (e.bias) v = v + e.bias[co];
-        v = round16(v, e.round_out);   // (autocast output semantics; 0: unchanged)
+        v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
         if (e.bn_w) {   // as epi_finish (conv.hip)
             const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
             const float alpha = invstd * e.bn_w[co];
             const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-            v = round16(v * alpha + beta, e.round_out);
+            v = rnd(v * alpha + beta);
         }
-        return round16(apply_act(v, e.act), e.round_out);
+        return rnd(apply_act(v, e.act));
     };
     if constexpr (NT == 4) {
         // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values

@@ -176,8 +176,12 @@ def test_step_layer_lowp(cuda, name, layer, ksplit):
     got = torch.from_numpy(npy(y.permute(0, 3, 1, 2)))
     ulp = 2.0 ** -10 if name == "fp16" else 2.0 ** -7     # one ulp, relative to the value (upper bound)
     diff = (got - ref).abs()
-    # two roundings (conv output, skip add): at most two ulps of the larger magnitude
-    assert bool((diff <= 2 * ulp * torch.maximum(ref.abs(), got.abs()) + 1e-30).all()), float(diff.max())
+    # two roundings (conv output, skip add): at most two ulps of the larger magnitude, or two subnormal steps
+    sub = 2.0 ** -24 if name == "fp16" else 2.0 ** -133     # the subnormal spacing (fp16 outputs below 6e-5)
+    bad = diff > 2 * ulp * torch.maximum(ref.abs(), got.abs()) + 2 * sub
+    i = int((diff / (torch.maximum(ref.abs(), got.abs()) + 1e-30)).argmax())
+    assert not bool(bad.any()), (int(bad.sum()), float(diff.max()), np.unravel_index(i, tuple(ref.shape)),
+                                 float(ref.flatten()[i]), float(got.flatten()[i]))
     assert float((diff > 0).double().mean()) < 0.01       # (boundary cases only)
 
 
