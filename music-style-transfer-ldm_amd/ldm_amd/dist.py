@@ -106,6 +106,7 @@ class _Bucket:
             off += p.numel()
         self.ready = set()
         self.work = None
+        self.streams = {}    # the streams that copied gradients in (the train step's branch streams)
 
 
 class GradAllReduce:
@@ -161,6 +162,14 @@ class GradAllReduce:
         return is_distributed() and tdist.get_backend(self.group) == "nccl"
 
     def _launch(self, b):
+        # gradients of a branch (e.g. the style encoder's, graphs.branch) were copied in on that branch's
+        # stream: the launching stream waits for every stream that wrote into the bucket
+        if b.flat.is_cuda:
+            cur = torch.cuda.current_stream(b.flat.device)
+            for st in b.streams.values():
+                if st.cuda_stream != cur.cuda_stream:
+                    cur.wait_stream(st)
+        b.streams.clear()
         if self._collective is not None:
             b.work = self._collective(b.flat, self.group)
             return
@@ -172,6 +181,9 @@ class GradAllReduce:
             return
         off = b.offsets[id(p)]
         b.flat[off: off + p.numel()].copy_(p.grad.reshape(-1))
+        if b.flat.is_cuda:
+            st = torch.cuda.current_stream(b.flat.device)
+            b.streams[st.cuda_stream] = st
         b.ready.add(id(p))
         if len(b.ready) == len(b.params):
             self._launch(b)

@@ -12,6 +12,9 @@ the process down from a thread with no Python frame — after the capture, e.g. 
 (round 3's intermittent abort).  In thread-local mode only the capturing thread is
 restricted, which is all the capture needs: nothing on this path calls the runtime from another thread.
 """
+import contextlib
+import os
+
 import torch
 
 CAPTURE_MODE = "thread_local"
@@ -20,3 +23,80 @@ CAPTURE_MODE = "thread_local"
 def capture(graph, stream=None, pool=None):
     """Context manager: capture into `graph` (torch.cuda.CUDAGraph) on `stream`, thread-local mode."""
     return torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=CAPTURE_MODE)
+
+
+_BRANCH_STREAMS = {}
+
+
+def _stream_switch(device, var, default):
+    """An env switch for the side-stream forms: "1" on, "0" off, unset: `default` ("capture": only while the
+    current stream is capturing a hipGraph).  Measured (profiles/r04/branch_streams): the replayed train step
+    runs the DAG's independent branches concurrently (4.96 -> 4.70 ms with the style-encoder branch), while an
+    eager step pays more in host-side stream bookkeeping than it gains (5.87 -> 6.97 ms)."""
+    if torch.device(device).type != "cuda":
+        return False
+    v = os.environ.get(var, default)
+    if v == "capture":
+        return torch.cuda.is_current_stream_capturing()
+    return v != "0"
+
+
+def branch_streams_enabled(device):
+    """Independent branches of the train step on their own streams (LDM_AMD_BRANCH_STREAMS)."""
+    return _stream_switch(device, "LDM_AMD_BRANCH_STREAMS", "capture")
+
+
+_POOL_SIZE = 8
+
+
+def prepare_streams(device):
+    """Create the side-stream pool of `device` (outside any capture: a stream is never created while a graph
+    is being captured)."""
+    key = str(torch.device(device))
+    if key not in _BRANCH_STREAMS:
+        _BRANCH_STREAMS[key] = ([torch.cuda.Stream(device=torch.device(device)) for _ in range(_POOL_SIZE)], {})
+
+
+def branch_stream(device, name):
+    """The side stream of branch `name` on `device` (a fixed stream of the pool per name), or None when the
+    pool does not exist yet and the current stream is capturing, or the pool is used up."""
+    key = str(torch.device(device))
+    if key not in _BRANCH_STREAMS:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        prepare_streams(device)
+    pool, names = _BRANCH_STREAMS[key]
+    i = names.get(name)
+    if i is None:
+        if len(names) >= len(pool):
+            return None
+        i = names[name] = len(names)
+    return pool[i]
+
+
+@contextlib.contextmanager
+def branch(device, name):
+    """Run the block on the side stream `name`, forked from the current stream: the block's work may overlap
+    what the current stream does next, until join() (or a consumer on another stream, which the autograd
+    engine orders after it).  Inside a graph capture the fork and the join become graph edges.  Yields the
+    stream to pass to join(); with branch streams off the block runs in place and join() does nothing."""
+    if not branch_streams_enabled(device):
+        yield None
+        return
+    main = torch.cuda.current_stream(torch.device(device))
+    side = branch_stream(device, name)
+    if side is None or side.cuda_stream == main.cuda_stream:
+        yield None
+        return
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        yield side
+
+
+def join(side, device):
+    """The current stream waits for everything queued on `side` so far.  Tensors a branch made and the current
+    stream reads afterwards need no record_stream: their blocks return to the branch's pool when freed, and
+    the branch's next allocation comes after its next fork, i.e. after a wait on the current stream."""
+    if side is None:
+        return
+    torch.cuda.current_stream(torch.device(device)).wait_stream(side)

@@ -360,9 +360,15 @@ def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False):
 _WS = {}
 
 
+def _stream_key(device):
+    d = torch.device(device)
+    return torch.cuda.current_stream(d).cuda_stream if d.type == "cuda" else 0
+
+
 def scratch(name, nfloats, device):
-    """Per-device scratch buffer reused across calls on the current stream (grown on demand)."""
-    key = (name, str(device))
+    """Per-(device, stream) scratch buffer reused across stream-ordered calls (grown on demand): the train
+    step runs independent branches on their own streams (graphs.branch), each with its own buffers."""
+    key = (name, str(device), _stream_key(device))
     buf = _WS.get(key)
     if buf is None or buf.numel() < nfloats:
         buf = torch.empty(max(int(nfloats), 1), device=device, dtype=torch.float32)
@@ -575,10 +581,11 @@ def loss_forward(kind, a, b=None):
         b = f32c(b)
         if b.shape != a.shape:
             raise RuntimeError(f"loss: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
-    ws = _LOSS_WS.get(str(a.device))
+    key = (str(a.device), _stream_key(a.device))
+    ws = _LOSS_WS.get(key)
     if ws is None:
         ws = torch.empty(512, device=a.device, dtype=torch.float64)
-        _LOSS_WS[str(a.device)] = ws
+        _LOSS_WS[key] = ws
     out = torch.empty((), device=a.device, dtype=torch.float32)
     L.call("ldm_loss_forward", kind, a.data_ptr(), _p(b), a.numel(), ws.data_ptr(), out.data_ptr(), stream_handle())
     return out

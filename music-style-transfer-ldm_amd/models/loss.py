@@ -35,6 +35,25 @@ _PERCEPTUAL_BACKEND = None
 _WARNED = set()
 
 
+_ZEROS = {}
+
+
+def _const_zero(device):
+    """The 0-d zero an absent offline term returns: one cached tensor per device, marked so that the sums
+    below skip adding it (x + w * 0 == x for every finite x: the same value, two fewer launches per use)."""
+    key = str(device)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = torch.zeros((), device=device, dtype=torch.float32)
+        z._ldm_const_zero = True
+        _ZEROS[key] = z
+    return z
+
+
+def is_const_zero(t):
+    return getattr(t, "_ldm_const_zero", False)
+
+
 def _warn_once(key, msg):
     if key not in _WARNED:
         _WARNED.add(key)
@@ -57,7 +76,7 @@ def perceptual_loss_old(original, reconstructed):
     if _PERCEPTUAL_BACKEND is None:
         _warn_once("lpips", "perceptual_loss_old: no LPIPS backend installed (weights are not available "
                             "offline); the perceptual term is 0. Use loss.set_perceptual_backend(fn).")
-        return torch.zeros((), device=original.device, dtype=torch.float32)
+        return _const_zero(original.device)
     from ldm_amd.lpips import LPIPSAlex
     if isinstance(_PERCEPTUAL_BACKEND, LPIPSAlex):
         return _PERCEPTUAL_BACKEND(original, reconstructed, unit=True).mean()
@@ -93,6 +112,8 @@ def compression_loss(original, reconstructed, latent, feature_extractor):
     perc = perceptual_loss(original, reconstructed, config["compression_feature_extractor"],
                            feature_extractor=feature_extractor)
     kl = kl_regularization_loss(latent)
+    if is_const_zero(perc):
+        return mse + 0.01 * kl
     return mse + 0.1 * perc + 0.01 * kl
 
 
@@ -141,7 +162,7 @@ class VGGishFeatureLoss(nn.Module):
         if self.features is None:
             _warn_once("vggish", "VGGishFeatureLoss: no VGGish weights (remote torch.hub in the reference); "
                                  "style loss is 0 (it is gradient-free in the reference, loss.py:78).")
-            return torch.zeros((), device=predicted.device, dtype=torch.float32)
+            return _const_zero(predicted.device)
         from ldm_amd import ops
         layers = list(self.features)
         ntaps = sum(isinstance(m, nn.ReLU) for m in layers)

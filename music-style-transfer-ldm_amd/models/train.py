@@ -28,12 +28,12 @@ try:
     from .config import config
     from . import _pathfix  # noqa: F401
     from .model import LDM, SpectrogramDecoder, SpectrogramEncoder
-    from .loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
+    from .loss import VGGishFeatureLoss, compression_loss, diffusion_loss, is_const_zero, style_loss
 except ImportError:   # reference-style flat imports (models/ on sys.path)
     from config import config
     import _pathfix  # noqa: F401
     from model import LDM, SpectrogramDecoder, SpectrogramEncoder
-    from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, style_loss
+    from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, is_const_zero, style_loss
 
 from ldm_amd import dist as hdist
 from ldm_amd import graphs as hgraphs
@@ -218,7 +218,10 @@ class LDMTrainer:
             denoisinsg_loss = diffusion_loss(noise_pred, noise)
             compression_loss_ = compression_loss(content_spec, reconstructed, z_0, self.model.feature_loss_net)
             style_loss_ = style_loss(reconstructed, style_spec, self.model.feature_loss_net)
-            total_loss = compression_loss_ + denoisinsg_loss + self.style_loss_weight * style_loss_
+            if is_const_zero(style_loss_):   # no VGGish weights offline: + w * 0 adds nothing
+                total_loss = compression_loss_ + denoisinsg_loss
+            else:
+                total_loss = compression_loss_ + denoisinsg_loss + self.style_loss_weight * style_loss_
         # the step's reconstruction (a static buffer of the graph when the step is replayed): for callers that
         # inspect the step's output, e.g. the parity tests; nothing in the step reads it
         self.last_outputs = {"reconstructed": reconstructed.detach()}
@@ -274,6 +277,7 @@ class LDMTrainer:
                 # ...except the batched re-pack's buffers: packed here, outside the graph, for the captured
                 # forward to read; the graph re-packs them at its end (after the optimizer) for the next replay
                 self._packset.repack()
+            hgraphs.prepare_streams(self.device)    # the branch streams exist before the capture starts
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with hgraphs.capture(g):
