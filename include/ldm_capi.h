@@ -64,6 +64,16 @@ enum { LDM_DT_F32 = 0, LDM_DT_F16 = 1, LDM_DT_BF16 = 2 };
  * LDM_ACT_ROUND_F16 / LDM_ACT_ROUND_BF16: the BatchNorm output likewise (a 16-bit input's BN output). */
 enum { LDM_DT_ROUND_OUT = 0x100 };
 enum { LDM_ACT_ROUND_F16 = LDM_DT_F16 << 8, LDM_ACT_ROUND_BF16 = LDM_DT_BF16 << 8 };
+/* 16-bit storage of the train step's large maps (ATen keeps the outputs of an autocast region in fp16 / bf16):
+ *  - conv entry points, or'ed into ldm_epilogue.dtype with LDM_DT_F16 / _BF16: the input x (LDM_DT_X16), the
+ *    output y and act_out (LDM_DT_Y16) are stored in that type; ldm_conv_backward_weight_dt's dtype takes
+ *    LDM_DT_X16 (x) and LDM_DT_DY16 (dy);
+ *  - BatchNorm / activation-backward entry points: bits 16-17 of the act code name the 16-bit type
+ *    (LDM_DT_F16 / _BF16 << LDM_ST_SHIFT), and LDM_ST_* which of the call's tensors are stored in it: X16 the
+ *    BatchNorm input x (activation backward: act_out), Y16 the BatchNorm output y, DY16 the incoming gradient,
+ *    DX16 the outgoing gradient (dx / dv).  The pointers stay typed float* in the signatures. */
+enum { LDM_DT_X16 = 0x200, LDM_DT_Y16 = 0x400, LDM_DT_DY16 = 0x800 };
+enum { LDM_ST_SHIFT = 16, LDM_ST_X16 = 1 << 18, LDM_ST_Y16 = 1 << 19, LDM_ST_DY16 = 1 << 20, LDM_ST_DX16 = 1 << 21 };
 
 typedef struct ldm_epilogue {
     const float* bias;      /* [Cout] or NULL                                                */
@@ -105,6 +115,10 @@ int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan* plan, cons
                          float* packed, void* stream);
 /* y = epilogue(conv(x, w)).  `w` is the packed buffer for MFMA plans, the torch weight for direct.
  * Plans with ks > 1 need ldm_conv_forward_ws. */
+/* The 16-bit storage flags (LDM_DT_X16 | LDM_DT_Y16) ldm_conv_forward takes for (d, plan) at a 16-bit operand
+ * precision: both on kind-3 plans, a 16-bit output on the Cin = 1 stride-2 kernel, a 16-bit input on the
+ * 64 -> 1 k4 s2 transposed conv; else 0. */
+int32_t ldm_conv_storage16(const ldm_conv_desc* d, const ldm_conv_plan* plan);
 int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
                      const ldm_epilogue* ep, float* y, void* stream);
 /* The same with a caller-owned workspace of plan->ws_floats floats (may be NULL when that is 0).
@@ -137,6 +151,9 @@ int ldm_batchnorm_train_out(const float* x, float* y, int32_t B, int32_t C, int3
  * all-reduce with zero sums and still updates the running statistics). */
 int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
                         void* stream);
+/* ldm_batchnorm_stats with a storage code (LDM_ST_X16 | type << LDM_ST_SHIFT: a 16-bit input) */
+int ldm_batchnorm_stats_code(const float* x, int32_t code, int32_t B, int32_t C, int32_t HW, double* stats,
+                             float* workspace, void* stream);
 int ldm_batchnorm_apply(float* x, int32_t B, int32_t C, int32_t HW, const double* stats, double count,
                         const float* weight, const float* bias, float* running_mean, float* running_var,
                         float momentum, float eps, int32_t act, float* save_mean, float* save_invstd, void* stream);
@@ -380,6 +397,9 @@ int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d);
  * shapes it does not cover run the fp32 kernel). */
 int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                 int32_t accumulate, float* workspace, int32_t dtype, void* stream);
+/* The 16-bit storage flags (LDM_DT_X16 | LDM_DT_DY16) ldm_conv_backward_weight_dt takes for d at a 16-bit
+ * operand precision (0: neither; the caller then passes fp32 tensors). */
+int32_t ldm_conv_wgrad_storage16(const ldm_conv_desc* d);
 int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
                              float* workspace, void* stream);
 /* Backward of the fused epilogue act(v) (+bcast[b,c]) (+skip): dv = dy*act'(v) (from act_out = act(v);

@@ -516,6 +516,8 @@ extern "C" int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d) {
     return (int64_t)S * a.M * a.N;
 }
 
+extern "C" int32_t ldm_conv_wgrad_storage16(const ldm_conv_desc* d) { return d ? wgrad2_storage16(*d) : 0; }
+
 extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                         int32_t accumulate, float* workspace, void* stream) {
     return ldm_conv_backward_weight_dt(d, x, dy, dw, accumulate, workspace, LDM_DT_F32, stream);
@@ -524,7 +526,10 @@ extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, 
 extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                            int32_t accumulate, float* workspace, int32_t dtype, void* stream) {
     LDM_REQUIRE(d && x && dy && dw && workspace, "wgrad: null argument");
+    const int st16 = dtype & (LDM_DT_X16 | LDM_DT_DY16);
+    dtype &= ~(LDM_DT_X16 | LDM_DT_DY16);
     LDM_REQUIRE(dtype >= LDM_DT_F32 && dtype <= LDM_DT_BF16, "wgrad: unknown operand precision");
+    LDM_REQUIRE(!st16 || dtype != LDM_DT_F32, "wgrad: 16-bit storage needs a 16-bit dtype");
     WgradArgs a;
     int kk;
     int rc = wgrad_setup(*d, a, kk);
@@ -534,8 +539,12 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     hipStream_t st = (hipStream_t)stream;
     const int MN = a.M * a.N;
     int S2 = 0;
-    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st);   // the tap-shared form (wgrad.hip) where it applies
+    // 16-bit storage (LDM_DT_X16 / LDM_DT_DY16) as Dense / Gath flags: Dense = dy (conv) or x (convT)
+    const int d16 = (st16 & (d->transposed ? LDM_DT_X16 : LDM_DT_DY16)) ? 1 : 0;
+    const int g16 = (st16 & (d->transposed ? LDM_DT_DY16 : LDM_DT_X16)) ? 1 : 0;
+    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st, d16 | (g16 << 1));   // (wgrad.hip) where it applies
     if (rc > 0) return rc;
+    LDM_REQUIRE(rc == 0 || !st16, "wgrad: 16-bit storage on a layer without the tap-shared form (ldm_conv_wgrad_storage16)");
     if (rc == 0) {
         wgrad_reduce((const float*)workspace, S2, MN, dw, accumulate, st);
         LDM_CHECK_LAUNCH("wgrad_reduce_kernel");

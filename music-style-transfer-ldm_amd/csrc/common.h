@@ -180,6 +180,8 @@ struct EpiArgs {
     // LDM_DT_F16 / LDM_DT_BF16: round the conv output, the eval-BN output, the activation and each add to that
     // type, as ATen's autocast does (its conv / linear outputs are 16-bit tensors); 0: fp32 outputs
     int32_t round_out;
+    // 16-bit storage (LDM_DT_X16 / LDM_DT_Y16, in the lowp type): the input x, and the output y with act_out
+    int32_t x16, y16;
 };
 
 // conv.hip: implicit-GEMM conv with the full internal epilogue (incl. the fused DDIM update); y may be
@@ -241,7 +243,8 @@ int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 // wgrad.hip: the tap-shared weight-gradient kernel (ldm_conv_backward_weight where it applies)
 bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats);
 int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
-               hipStream_t st);
+               hipStream_t st, int st16 = 0);
+int wgrad2_storage16(const ldm_conv_desc& d);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile
 // with fp contract off).  Returns x_next; x0 out.
@@ -261,6 +264,78 @@ __device__ __forceinline__ float round16(float v, int mode) {
     if (mode == LDM_DT_F16) return (float)(_Float16)v;
     if (mode == LDM_DT_BF16) return (float)(__bf16)v;
     return v;
+}
+
+// ---- 16-bit activation storage (the train step's large maps inside an autocast region: ATen stores them as
+// fp16 / bf16 tensors).  ST = the 16-bit type (LDM_DT_F16 / LDM_DT_BF16); a tensor is read / written in it
+// when its flag `h` is set, else as fp32.  Stores convert round-to-nearest-even (a value already rounded to the
+// type, as the autocast output semantics leave it, is stored exactly).
+template <int ST>
+__device__ __forceinline__ float from16(unsigned short u) {
+    if constexpr (ST == LDM_DT_F16) return (float)__builtin_bit_cast(_Float16, u);
+    else return __builtin_bit_cast(float, (unsigned)u << 16);
+}
+template <int ST>
+__device__ __forceinline__ unsigned short to16s(float v) {
+    if constexpr (ST == LDM_DT_F16) return __builtin_bit_cast(unsigned short, (_Float16)v);
+    else return __builtin_bit_cast(unsigned short, (__bf16)v);
+}
+// W consecutive values at element offset o of p (fp32, or 16-bit when ST != 0 and h)
+template <int ST, int W>
+__device__ __forceinline__ void ld_st(const void* p, size_t o, bool h, float (&v)[W]) {
+    if (ST != 0 && h) {
+        const unsigned short* q = reinterpret_cast<const unsigned short*>(p) + o;
+        if constexpr (W == 4) {
+            const uint2 t = *reinterpret_cast<const uint2*>(q);
+            v[0] = from16<ST>((unsigned short)(t.x & 0xffff)), v[1] = from16<ST>((unsigned short)(t.x >> 16));
+            v[2] = from16<ST>((unsigned short)(t.y & 0xffff)), v[3] = from16<ST>((unsigned short)(t.y >> 16));
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) v[j] = from16<ST>(q[j]);
+        }
+    } else {
+        const float* q = reinterpret_cast<const float*>(p) + o;
+        if constexpr (W == 4) {
+            const float4 t = *reinterpret_cast<const float4*>(q);
+            v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) v[j] = q[j];
+        }
+    }
+}
+template <int ST, int W>
+__device__ __forceinline__ void st_st(void* p, size_t o, bool h, const float (&v)[W]) {
+    if (ST != 0 && h) {
+        unsigned short* q = reinterpret_cast<unsigned short*>(p) + o;
+        if constexpr (W == 4) {
+            uint2 t;
+            t.x = (unsigned)to16s<ST>(v[0]) | ((unsigned)to16s<ST>(v[1]) << 16);
+            t.y = (unsigned)to16s<ST>(v[2]) | ((unsigned)to16s<ST>(v[3]) << 16);
+            *reinterpret_cast<uint2*>(q) = t;
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) q[j] = to16s<ST>(v[j]);
+        }
+    } else {
+        float* q = reinterpret_cast<float*>(p) + o;
+        if constexpr (W == 4) {
+            *reinterpret_cast<float4*>(q) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) q[j] = v[j];
+        }
+    }
+}
+template <int ST>
+__device__ __forceinline__ float ld1_st(const void* p, size_t o, bool h) {
+    if (ST != 0 && h) return from16<ST>(reinterpret_cast<const unsigned short*>(p)[o]);
+    return reinterpret_cast<const float*>(p)[o];
+}
+template <int ST>
+__device__ __forceinline__ void st1_st(void* p, size_t o, bool h, float v) {
+    if (ST != 0 && h) reinterpret_cast<unsigned short*>(p)[o] = to16s<ST>(v);
+    else reinterpret_cast<float*>(p)[o] = v;
 }
 
 __device__ __forceinline__ float apply_act(float v, int act) {

@@ -981,16 +981,23 @@ __device__ __forceinline__ float chan_apply(const ConvArgs& a, const ChanEpi& c,
     if (a.ep.bn_w) v = round16(v * c.alpha + c.beta, ro);
     return round16(apply_act(v, a.ep.act), ro);
 }
+// YS: 0 fp32 outputs, else the 16-bit storage type of y / act_out (LDM_DT_Y16)
+template <int YS = 0>
 __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float (&v)[4]) {
-    const float4 t = make_float4(v[0], v[1], v[2], v[3]);
-    if (a.ep.act_out) *reinterpret_cast<float4*>(a.ep.act_out + o) = t;
-    *reinterpret_cast<float4*>(a.y + o) = t;
+    if constexpr (YS != 0) {
+        if (a.ep.act_out) st_st<YS, 4>(a.ep.act_out, o, true, v);
+        st_st<YS, 4>(a.y, o, true, v);
+    } else {
+        const float4 t = make_float4(v[0], v[1], v[2], v[3]);
+        if (a.ep.act_out) *reinterpret_cast<float4*>(a.ep.act_out + o) = t;
+        *reinterpret_cast<float4*>(a.y + o) = t;
+    }
 }
 
 // Cin = 1, stride 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
 // 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (6 + K) input window in registers,
 // every output channel from it, weights in LDS.
-template <int K, int LP, int RO>
+template <int K, int LP, int RO, int YS>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
     __shared__ ChanEpi es[64];   // per-channel epilogue constants, formed once per block (not per lane and channel)
@@ -1036,7 +1043,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[j]);
-        store4(a, o, v);
+        store4<YS>(a, o, v);
     }
 }
 
@@ -1047,7 +1054,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
 __host__ __device__ constexpr int ct4_tap(int r, int i) { return r == 0 ? (i == 0 ? 1 : 3) : (i == 0 ? 0 : 2); }
 __host__ __device__ constexpr int ct4_off(int r, int i) { return (r + 1 - ct4_tap(r, i)) >> 1; }
 
-template <int LP, int RO>
+template <int LP, int RO, int XS>
 __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
     const int W4 = a.Win >> 2;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1073,7 +1080,10 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16((rok[i] && cok[c]) ? xp[i * a.Win + c] : 0.f, LP);
+            for (int c = 0; c < 6; ++c)
+                xr[i][c] = (rok[i] && cok[c]) ? (XS ? ld1_st<XS>(a.x, (size_t)(xp - a.x) + i * a.Win + c, true)
+                                                    : round16(xp[i * a.Win + c], LP))
+                                              : 0.f;
         const float* wq = a.w + ci * 16;   // w [Cin][1][4][4]
 #pragma unroll
         for (int ry = 0; ry < 2; ++ry)
@@ -1106,7 +1116,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_kernel(ConvArgs a) {
 // The same layer with two input rows per lane (four output rows x 8 columns): per input channel a lane
 // reads its four window rows as one 16-byte run plus the two border columns (12 loads for two rows instead
 // of 36 single-float gathers), and the channel loop keeps two channels of loads in flight.  Hin even.
-template <int LP, int RO>
+template <int LP, int RO, int XS>
 __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
     const int W4 = a.Win >> 2, H2 = a.Hin >> 1;
     const int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1132,12 +1142,21 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float* row = p + i * a.Win;
-            const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
-            xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
-            xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
-            xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+            if constexpr (XS != 0) {   // 16-bit storage: the operands are in the MFMA-free VALU type already
+                const size_t ro_ = (size_t)(row - a.x);
+                float m[4] = {0.f, 0.f, 0.f, 0.f};
+                if (rok[i]) ld_st<XS, 4>(a.x, ro_, true, m);
+                xr[i][0] = (rok[i] && lok) ? ld1_st<XS>(a.x, ro_ - 1, true) : 0.f;
+                xr[i][1] = m[0], xr[i][2] = m[1], xr[i][3] = m[2], xr[i][4] = m[3];
+                xr[i][5] = (rok[i] && hok) ? ld1_st<XS>(a.x, ro_ + 4, true) : 0.f;
+            } else {
+                const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
+                xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
+                xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
+                xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
+                for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
+            }
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1189,7 +1208,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
 // quarter g * Cin / 4 .. of the channels for the 64 tiles of its block, then the quarters meet in LDS in wave
 // order.  At B = 32 the two-rows-per-lane kernel has 65,536 lanes, one 4-wave block per CU walking all 64
 // channels in a chain of dependent loads (119 us per launch); here 4x the waves walk a quarter each.
-template <int LP, int RO>
+template <int LP, int RO, int XS>
 __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
     __shared__ float part[3][32][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -1219,12 +1238,21 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float* row = p + i * a.Win;
-            const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
-            xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
-            xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
-            xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
+            if constexpr (XS != 0) {   // 16-bit storage: the operands are in the MFMA-free VALU type already
+                const size_t ro_ = (size_t)(row - a.x);
+                float m[4] = {0.f, 0.f, 0.f, 0.f};
+                if (rok[i]) ld_st<XS, 4>(a.x, ro_, true, m);
+                xr[i][0] = (rok[i] && lok) ? ld1_st<XS>(a.x, ro_ - 1, true) : 0.f;
+                xr[i][1] = m[0], xr[i][2] = m[1], xr[i][3] = m[2], xr[i][4] = m[3];
+                xr[i][5] = (rok[i] && hok) ? ld1_st<XS>(a.x, ro_ + 4, true) : 0.f;
+            } else {
+                const float4 m = rok[i] ? *reinterpret_cast<const float4*>(row) : make_float4(0.f, 0.f, 0.f, 0.f);
+                xr[i][0] = (rok[i] && lok) ? row[-1] : 0.f;
+                xr[i][1] = m.x, xr[i][2] = m.y, xr[i][3] = m.z, xr[i][4] = m.w;
+                xr[i][5] = (rok[i] && hok) ? row[4] : 0.f;
 #pragma unroll
-            for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
+                for (int c = 0; c < 6; ++c) xr[i][c] = round16(xr[i][c], LP);
+            }
         }
     };
     auto mac = [&](const float (&xr)[4][6], const float* wq) {
@@ -1631,19 +1659,22 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             ((uintptr_t)y & 15) == 0 && (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Wout / 4);
             const int64_t lanes = (int64_t)d.B * d.Hout * (d.Wout / 4);
+            LDM_REQUIRE(!ep.x16, "conv: the Cin = 1 kernel reads fp32 inputs only");
             lp_dispatch(a.ep, [&](auto lp, auto ro) {
                 constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
-                if (d.kh == 3)
-                    hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       st, a);
-                else
-                    hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       st, a);
+                const dim3 g((unsigned)((lanes + 255) / 256));
+                if (LP != 0 && ep.y16) {
+                    if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, LP>), g, dim3(256), 0, st, a);
+                    else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, LP>), g, dim3(256), 0, st, a);
+                } else {
+                    if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, 0>), g, dim3(256), 0, st, a);
+                    else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, 0>), g, dim3(256), 0, st, a);
+                }
             });
             LDM_CHECK_LAUNCH("conv_cin1_x4_kernel");
             return 0;
         }
-        if (simple_epi && d.transposed && d.Cout == 1 && d.kh == 4 && d.kw == 4 && d.stride == 2 && d.pad == 1 &&
+        if (simple_epi && !ep.y16 && d.transposed && d.Cout == 1 && d.kh == 4 && d.kw == 4 && d.stride == 2 && d.pad == 1 &&
             d.out_pad == 0 && d.Win % 4 == 0 && a.pt.nphase == 4 && ((uintptr_t)y & 15) == 0 &&
             (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Win / 4);
@@ -1655,8 +1686,11 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
                 a.fd_dho = FastDiv::make(d.Hin / 2);
                 const int64_t tiles = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
                 lp_dispatch(a.ep, [&](auto lp, auto ro) {
-                    hipLaunchKernelGGL((convT4_cout1_r2s_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0,
-                                       st, a);
+                    constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
+                    if (LP != 0 && ep.x16)
+                        hipLaunchKernelGGL((convT4_cout1_r2s_kernel<LP, RO, LP>), dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0, st, a);
+                    else
+                        hipLaunchKernelGGL((convT4_cout1_r2s_kernel<LP, RO, 0>), dim3((unsigned)((tiles + 63) / 64)), dim3(256), 0, st, a);
                 });
                 LDM_CHECK_LAUNCH("convT4_cout1_r2s_kernel");
                 return 0;
@@ -1665,8 +1699,11 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
                 a.fd_dho = FastDiv::make(d.Hin / 2);
                 const int64_t lanes = (int64_t)d.B * (d.Hin / 2) * (d.Win / 4);
                 lp_dispatch(a.ep, [&](auto lp, auto ro) {
-                    hipLaunchKernelGGL((convT4_cout1_r2_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       st, a);
+                    constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
+                    if (LP != 0 && ep.x16)
+                        hipLaunchKernelGGL((convT4_cout1_r2_kernel<LP, RO, LP>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+                    else
+                        hipLaunchKernelGGL((convT4_cout1_r2_kernel<LP, RO, 0>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
                 });
                 LDM_CHECK_LAUNCH("convT4_cout1_r2_kernel");
                 return 0;
@@ -1674,12 +1711,16 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             a.fd_dho = FastDiv::make(d.Hin);
             const int64_t lanes = (int64_t)d.B * d.Hin * (d.Win / 4);
             lp_dispatch(a.ep, [&](auto lp, auto ro) {
-                    hipLaunchKernelGGL((convT4_cout1_kernel<decltype(lp)::value, decltype(ro)::value>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       st, a);
+                    constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
+                    if (LP != 0 && ep.x16)
+                        hipLaunchKernelGGL((convT4_cout1_kernel<LP, RO, LP>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+                    else
+                        hipLaunchKernelGGL((convT4_cout1_kernel<LP, RO, 0>), dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
                 });
             LDM_CHECK_LAUNCH("convT4_cout1_kernel");
             return 0;
         }
+        LDM_REQUIRE(!ep.x16 && !ep.y16, "conv: 16-bit storage on a path without it (ldm_conv_storage16)");
         if (d.Cin == 1 && !d.transposed && d.Cout <= 64 && a.KK <= 16) {
             const int64_t pix = (int64_t)d.B * d.Hout * d.Wout;
             hipLaunchKernelGGL(conv_cin1_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, st, a);
@@ -1691,6 +1732,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
         return 0;
     }
     LDM_REQUIRE(plan_ok(d, p.kind, p.tm, p.tn, p.wk, p.ks), "conv forward: invalid plan");
+    LDM_REQUIRE(!ep.x16 && !ep.y16, "conv: 16-bit storage on a path without it (ldm_conv_storage16)");
     if (a.ks > 1) {   // (balance: a.ks = the largest per-phase split)
         PhaseTable pt2;
         LDM_REQUIRE(build_phase_table(d, pt2) == 0 && p.ws_floats == split_ws_floats(d, p, pt2),
@@ -1729,11 +1771,31 @@ extern "C" int ldm_conv_forward_ws(const ldm_conv_desc* d, const ldm_conv_plan* 
         e.skip = ep->skip_add;
         e.act_out = ep->act_out;
         e.lowp = ep->dtype & 0xff;
-        LDM_REQUIRE(e.lowp >= LDM_DT_F32 && e.lowp <= LDM_DT_BF16 && (ep->dtype & ~(0xff | LDM_DT_ROUND_OUT)) == 0,
+        LDM_REQUIRE(e.lowp >= LDM_DT_F32 && e.lowp <= LDM_DT_BF16 &&
+                        (ep->dtype & ~(0xff | LDM_DT_ROUND_OUT | LDM_DT_X16 | LDM_DT_Y16)) == 0,
                     "conv forward: unknown operand precision");
         e.round_out = (ep->dtype & LDM_DT_ROUND_OUT) ? e.lowp : 0;
+        e.x16 = (ep->dtype & LDM_DT_X16) ? 1 : 0;
+        e.y16 = (ep->dtype & LDM_DT_Y16) ? 1 : 0;
+        LDM_REQUIRE(e.lowp != LDM_DT_F32 || (!e.x16 && !e.y16), "conv forward: 16-bit storage needs a 16-bit dtype");
     }
     return conv_forward_ex(*d, *plan, x, w, e, y, workspace, (hipStream_t)stream);
+}
+
+// The 16-bit storage flags (LDM_DT_X16 / LDM_DT_Y16) ldm_conv_forward takes for (d, plan) at a 16-bit operand
+// precision: kind 3 both; the Cin = 1 stride-2 kernel a 16-bit output; the 64 -> 1 k4 s2 transposed conv a
+// 16-bit input (simple epilogues, 16-byte aligned tensors, as those kernels require); else none.
+extern "C" int32_t ldm_conv_storage16(const ldm_conv_desc* d, const ldm_conv_plan* plan) {
+    if (!d || !plan) return 0;
+    if (plan->kind == 3) return LDM_DT_X16 | LDM_DT_Y16;
+    if (plan->kind != 0 || d->layout != 0) return 0;
+    if (d->Cin == 1 && !d->transposed && d->Cout <= 64 && d->kh == d->kw && (d->kh == 3 || d->kh == 4) &&
+        d->stride == 2 && d->Wout % 4 == 0)
+        return LDM_DT_Y16;
+    if (d->transposed && d->Cout == 1 && d->kh == 4 && d->kw == 4 && d->stride == 2 && d->pad == 1 && d->out_pad == 0 &&
+        d->Win % 4 == 0)
+        return LDM_DT_X16;
+    return 0;
 }
 
 extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,

@@ -12,6 +12,8 @@
 // slices in order), so results are bitwise reproducible run to run.  BatchNorm statistics are fp64
 // (sum x, sum x^2) so the per-rank sums can be all-reduced for SyncBatchNorm between the two stages
 // (ldm_batchnorm_stats -> all-reduce -> ldm_batchnorm_apply; likewise the backward).
+#include <type_traits>
+
 #include "common.h"
 
 namespace ldm {
@@ -106,25 +108,26 @@ __device__ __forceinline__ float bn_affine(float v, float alpha, float beta) { r
 
 // g * act'(output) of the BN backward: from the saved output y, or, when y is NULL (act NONE / RELU), from
 // the input x through the forward's affine map (alpha = invstd * w, beta = b - mean * alpha)
-__device__ __forceinline__ float bn_act_grad(int act, float g, const float* y, float yv, float xv, float alpha,
+__device__ __forceinline__ float bn_act_grad(int act, float g, bool has_y, float yv, float xv, float alpha,
                                              float beta) {
-    if (y) return g * act_grad(act, yv);
+    if (has_y) return g * act_grad(act, yv);
     if (act == LDM_ACT_RELU) return bn_affine(xv, alpha, beta) > 0.f ? g : 0.f;
     return g;
 }
 
 // ---- BatchNorm forward ---------------------------------------------------------------------------
-template <int W>
-__global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const float* __restrict__ x, int C, int HW,
+template <int W, int ST>
+__global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const void* __restrict__ x, int sf, int C, int HW,
                                                                     int64_t n, int64_t S,
                                                                     double* __restrict__ part) {
+    const bool xh = sf & LDM_ST_X16;
     __shared__ double red[kThreads / 64];
     const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     double s = 0.0, q = 0.0;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float v[W];
-        ld<W>(x + o, v);
+        ld_st<ST, W>(x, o, xh, v);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             s += (double)v[j];
@@ -160,8 +163,8 @@ __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double*
     if (out1) out1[c] = (float)b;
 }
 
-template <int W>
-__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, float* x, int C,
+template <int W, int ST>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, void* x, int sf, int C,
                                                             int HW, int64_t n, int64_t S,
                                                             const double* __restrict__ stats, double count_arg,
                                                             const float* __restrict__ weight,
@@ -192,13 +195,14 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, fl
     const float alpha = invstd * (weight ? weight[c] : 1.0f);
     const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
-    const int ro = act >> 8, ac = act & 0xff;   // LDM_ACT_ROUND_*: the output of a 16-bit input's BN (autocast)
+    const int ro = (act >> 8) & 0xff, ac = act & 0xff;   // LDM_ACT_ROUND_*: the output of a 16-bit input's BN (autocast)
+    const bool xh = sf & LDM_ST_X16, yh = sf & LDM_ST_Y16;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float v[W];
-        ld<W>(src + o, v);
+        ld_st<ST, W>(src, o, xh, v);
 #pragma unroll
         for (int j = 0; j < W; ++j) v[j] = apply_act(round16(bn_affine(v[j], alpha, beta), ro), ac);
-        st<W>(x + o, v);
+        st_st<ST, W>(x, o, yh, v);
     });
     if (k == 0 && threadIdx.x == 0) {
         if (rmean) rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
@@ -212,10 +216,10 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float* src, fl
 }
 
 // ---- BatchNorm backward: g = dy*act'(y); sums (sum g, sum g*xhat); dx = w*invstd*(g - sg/N - xhat*sgx/N)
-template <int W>
-__global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const float* __restrict__ dy,
-                                                                  const float* __restrict__ y,
-                                                                  const float* __restrict__ x,
+template <int W, int ST>
+__global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __restrict__ dy,
+                                                                  const void* __restrict__ y,
+                                                                  const void* __restrict__ x, int sf,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ invstd,
                                                                   const float* __restrict__ w,
@@ -229,14 +233,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const float* _
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     float sg = 0.f, sgx = 0.f;
+    const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float g[W], yv[W] = {}, xv[W];
-        ld<W>(dy + o, g);
-        if (y) ld<W>(y + o, yv);
-        ld<W>(x + o, xv);
+        ld_st<ST, W>(dy, o, dyh, g);
+        if (y) ld_st<ST, W>(y, o, yh, yv);
+        ld_st<ST, W>(x, o, xh, xv);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            const float gj = bn_act_grad(act, g[j], y, yv[j], xv[j], alpha, beta);
+            const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
             sg += gj;
             sgx += gj * ((xv[j] - mu) * is);
         }
@@ -249,16 +254,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const float* _
     }
 }
 
-template <int W>
-__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __restrict__ dy,
-                                                                const float* __restrict__ y,
-                                                                const float* __restrict__ x,
+template <int W, int ST>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __restrict__ dy,
+                                                                const void* __restrict__ y,
+                                                                const void* __restrict__ x, int sf,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ invstd,
                                                                 const float* __restrict__ w,
                                                                 const float* __restrict__ bias, int act, int C, int HW,
                                                                 int64_t n, int64_t S, const double* __restrict__ sums,
-                                                                double count_arg, float* __restrict__ dx,
+                                                                double count_arg, void* __restrict__ dx,
                                                                 const double* __restrict__ part, int P,
                                                                 float* __restrict__ dweight, float* __restrict__ dbias) {
     const int k = blockIdx.x, c = blockIdx.y;
@@ -284,27 +289,29 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float* __r
     const float alpha = is * (w ? w[c] : 1.0f);
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
+    const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16, dxh = sf & LDM_ST_DX16;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float g[W], yv[W] = {}, xv[W], d[W];
-        ld<W>(dy + o, g);
-        if (y) ld<W>(y + o, yv);
-        ld<W>(x + o, xv);
+        ld_st<ST, W>(dy, o, dyh, g);
+        if (y) ld_st<ST, W>(y, o, yh, yv);
+        ld_st<ST, W>(x, o, xh, xv);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            const float gj = bn_act_grad(act, g[j], y, yv[j], xv[j], alpha, beta);
+            const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
             d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
         }
-        st<W>(dx + o, d);
+        st_st<ST, W>(dx, o, dxh, d);
     });
 }
 
 // ---- fused-epilogue activation backward: dv = dy*act'(v); partial sums of dv and dy per (b,c,slice)
-template <int W>
-__global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
-                                                           const float* __restrict__ aval,
-                                                           const float* __restrict__ pre, int act, int C, int HW,
-                                                           int64_t S, float* dv,
+template <int W, int ST>
+__global__ __launch_bounds__(kThreads) void act_bwd_kernel(const void* dy,
+                                                           const void* __restrict__ aval,
+                                                           const float* __restrict__ pre, int act, int sf, int C,
+                                                           int HW, int64_t S, void* dv,
                                                            float* __restrict__ part) {
+    const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
     __shared__ float red[kThreads / 64];
     const int k = blockIdx.x, plane = blockIdx.y, Q = gridDim.x;
     const int b = plane / C, c = plane - b * C;
@@ -314,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
     float sd = 0.f, sg = 0.f;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float g[W], d[W];
-        ld<W>(dy + o, g);
+        ld_st<ST, W>(dy, o, dyh, g);
         if (act == LDM_ACT_GELU) {
             float v[W];
             ld<W>(pre + o, v);
@@ -326,14 +333,14 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
             }
         } else if (aval) {
             float a[W];
-            ld<W>(aval + o, a);
+            ld_st<ST, W>(aval, o, ah, a);
 #pragma unroll
             for (int j = 0; j < W; ++j) d[j] = g[j] * act_grad(act, a[j]);
         } else {
 #pragma unroll
             for (int j = 0; j < W; ++j) d[j] = g[j];
         }
-        if (dv) st<W>(dv + o, d);
+        if (dv) st_st<ST, W>(dv, o, dvh, d);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             sd += d[j];
@@ -355,10 +362,11 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const float* dy,
 // elements (8192 blocks, 10-12 us per launch).  Here TP = HW / 4 threads own one plane (one float4 each) and
 // a block holds 256 / TP planes; the plane's sums reduce over its TP lanes (shuffles within the segment, then
 // the plane's waves in order through LDS when TP > 64).  One partial per plane (Q = 1) for the finalize.
-template <int TP>
-__global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const float* __restrict__ dy,
-                                                                  const float* __restrict__ aval, int act, int nplanes,
-                                                                  float* dv, float* __restrict__ part) {
+template <int TP, int ST>
+__global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const void* __restrict__ dy,
+                                                                  const void* __restrict__ aval, int act, int sf,
+                                                                  int nplanes, void* dv, float* __restrict__ part) {
+    const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
     constexpr int PPB = kThreads / TP;
     __shared__ float red[2][kThreads / 64];
     const int pl = blockIdx.x * PPB + (int)threadIdx.x / TP;
@@ -367,17 +375,17 @@ __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const float* _
     if (pl < nplanes) {
         const size_t o = (size_t)pl * (TP * 4) + (size_t)t * 4;
         float g[4], d[4];
-        ld<4>(dy + o, g);
+        ld_st<ST, 4>(dy, o, dyh, g);
         if (aval) {
             float a[4];
-            ld<4>(aval + o, a);
+            ld_st<ST, 4>(aval, o, ah, a);
 #pragma unroll
             for (int j = 0; j < 4; ++j) d[j] = g[j] * act_grad(act, a[j]);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) d[j] = g[j];
         }
-        if (dv) st<4>(dv + o, d);
+        if (dv) st_st<ST, 4>(dv, o, dvh, d);
         sd = ((d[0] + d[1]) + d[2]) + d[3];
         sg = ((g[0] + g[1]) + g[2]) + g[3];
     }
@@ -462,29 +470,31 @@ static int finalize_lanes(int Q) {
 // Small planes (HW <= 16: the Linear layers, HW = 1, and the 2x8 projections): one block per channel
 // over its B*HW elements (dv elementwise, dbias by a block sum, dbcast[b] by the first B lanes over their
 // HW elements) -- one launch instead of the sliced kernel's B*C tiny blocks plus the finalize pass.
-__global__ __launch_bounds__(kThreads) void act_bwd_small_kernel(const float* __restrict__ dy,
-                                                                 const float* __restrict__ aval,
-                                                                 const float* __restrict__ pre, int act, int B, int C,
-                                                                 int HW, float* __restrict__ dv,
+template <int ST>
+__global__ __launch_bounds__(kThreads) void act_bwd_small_kernel(const void* __restrict__ dy,
+                                                                 const void* __restrict__ aval,
+                                                                 const float* __restrict__ pre, int act, int sf, int B,
+                                                                 int C, int HW, void* __restrict__ dv,
                                                                  float* __restrict__ dbias, float* __restrict__ dbcast) {
     __shared__ float red[kThreads / 64];
     const int c = blockIdx.x;
+    const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
     auto dval = [&](size_t o) {
-        const float g = dy[o];
+        const float g = ld1_st<ST>(dy, o, dyh);
         if (act == LDM_ACT_GELU) {
             const float v = pre[o];
             const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752440f));
             const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
             return g * (cdf + v * pdf);
         }
-        return aval ? g * act_grad(act, aval[o]) : g;
+        return aval ? g * act_grad(act, ld1_st<ST>(aval, o, ah)) : g;
     };
     float sd = 0.f;
     for (int e = threadIdx.x; e < B * HW; e += blockDim.x) {
         const int b = e / HW, i = e - b * HW;
         const size_t o = ((size_t)b * C + c) * HW + i;
         const float d = dval(o);
-        if (dv) dv[o] = d;
+        if (dv) st1_st<ST>(dv, o, dvh, d);
         sd += d;
     }
     if (dbias) {
@@ -495,7 +505,7 @@ __global__ __launch_bounds__(kThreads) void act_bwd_small_kernel(const float* __
         for (int b = threadIdx.x; b < B; b += blockDim.x) {
             const size_t o = ((size_t)b * C + c) * HW;
             float sg = 0.f;
-            for (int i = 0; i < HW; ++i) sg += dy[o + i];
+            for (int i = 0; i < HW; ++i) sg += ld1_st<ST>(dy, o + i, dyh);
             dbcast[(size_t)b * C + c] = sg;
         }
     }
@@ -504,6 +514,24 @@ __global__ __launch_bounds__(kThreads) void act_bwd_small_kernel(const float* __
 bool vec_ok(int HW, const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr) {
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     return HW % 4 == 0 && al(a) && al(b) && al(c) && al(d);
+}
+
+// the storage fields of an act code (ldm_capi.h LDM_ST_*): 16-bit type, per-tensor flags, and the act + round
+// bits the kernels read
+struct StCode {
+    int st, sf, act;
+};
+inline StCode st_code(int32_t code) {
+    StCode c{(code >> LDM_ST_SHIFT) & 3, code & (LDM_ST_X16 | LDM_ST_Y16 | LDM_ST_DY16 | LDM_ST_DX16), code & 0xffff};
+    if (c.st != LDM_DT_F16 && c.st != LDM_DT_BF16) c.st = 0, c.sf = 0;
+    return c;
+}
+// f(integral_constant<int, ST>) for the code's storage type
+template <class F>
+void st_dispatch(const StCode& c, F&& f) {
+    if (c.st == LDM_DT_F16) f(std::integral_constant<int, LDM_DT_F16>{});
+    else if (c.st == LDM_DT_BF16) f(std::integral_constant<int, LDM_DT_BF16>{});
+    else f(std::integral_constant<int, 0>{});
 }
 
 }  // namespace
@@ -520,24 +548,45 @@ extern "C" int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW)
     return bn > ac ? bn : ac;
 }
 
-extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
-                                   void* stream) {
-    LDM_REQUIRE(stats && workspace && B >= 0 && C > 0 && HW > 0 && (x || B == 0), "batchnorm_stats: bad argument");
+static int bn_stats_launch(const void* x, const StCode& sc, int32_t B, int32_t C, int32_t HW, double* part,
+                           void* stream) {
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
-    double* part = reinterpret_cast<double*>(workspace);
-    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "batchnorm_stats: workspace must be 8-byte aligned");
     const dim3 grid(P, C);
-    if (vec_ok(HW, x))
-        hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
-    else
-        hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
+    const bool v4 = vec_ok(HW, x);
+    st_dispatch(sc, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (v4)
+            hipLaunchKernelGGL((bn_stats_partial_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, sc.sf,
+                               C, HW, n, S, part);
+        else
+            hipLaunchKernelGGL((bn_stats_partial_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, sc.sf,
+                               C, HW, n, S, part);
+    });
     LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
+    return 0;
+}
+
+// SyncBatchNorm stage 1 with a storage code (LDM_ST_X16 | type << LDM_ST_SHIFT for a 16-bit input)
+extern "C" int ldm_batchnorm_stats_code(const float* x, int32_t code, int32_t B, int32_t C, int32_t HW, double* stats,
+                                        float* workspace, void* stream) {
+    LDM_REQUIRE(stats && workspace && B >= 0 && C > 0 && HW > 0 && (x || B == 0), "batchnorm_stats: bad argument");
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "batchnorm_stats: workspace must be 8-byte aligned");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    double* part = reinterpret_cast<double*>(workspace);
+    const int rc = bn_stats_launch(x, st_code(code), B, C, HW, part, stream);   // (B = 0: zero partials)
+    if (rc) return rc;
     hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
                        (hipStream_t)stream, part, C, P, stats, nullptr, nullptr, (double)n);
     LDM_CHECK_LAUNCH("slices_finalize_kernel");
     return 0;
+}
+
+extern "C" int ldm_batchnorm_stats(const float* x, int32_t B, int32_t C, int32_t HW, double* stats, float* workspace,
+                                   void* stream) {
+    return ldm_batchnorm_stats_code(x, 0, B, C, HW, stats, workspace, stream);
 }
 
 // part != NULL: the statistics are summed from bn_stats_partial_kernel's slice partials inside the apply
@@ -549,14 +598,19 @@ static int bn_apply_launch(const float* x, float* y, int32_t B, int32_t C, int32
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
     const dim3 grid(P, C);
-    if (vec_ok(HW, x, y))
-        hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
-                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd,
-                           part, part ? P : 0);
-    else
-        hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, C, HW, n, S, stats,
-                           count, weight, bias, running_mean, running_var, momentum, eps, act, save_mean, save_invstd,
-                           part, part ? P : 0);
+    const StCode sc = st_code(act);
+    const bool v4 = vec_ok(HW, x, y);
+    st_dispatch(sc, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (v4)
+            hipLaunchKernelGGL((bn_apply_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, sc.sf, C, HW,
+                               n, S, stats, count, weight, bias, running_mean, running_var, momentum, eps, sc.act,
+                               save_mean, save_invstd, part, part ? P : 0);
+        else
+            hipLaunchKernelGGL((bn_apply_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, sc.sf, C, HW,
+                               n, S, stats, count, weight, bias, running_mean, running_var, momentum, eps, sc.act,
+                               save_mean, save_invstd, part, part ? P : 0);
+    });
     LDM_CHECK_LAUNCH("bn_apply_kernel");
     return 0;
 }
@@ -588,14 +642,11 @@ extern "C" int ldm_batchnorm_train_out(const float* x, float* y, int32_t B, int3
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
     double* part = reinterpret_cast<double*>(workspace);
-    const dim3 grid(P, C);
     // rank-local: partials, then the apply sums them itself (two launches; the SyncBatchNorm path keeps the
     // finalize stage, whose sums it all-reduces)
-    if (vec_ok(HW, x))
-        hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
-    else
-        hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, x, C, HW, n, S, part);
-    LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
+    (void)P, (void)S;
+    const int rc = bn_stats_launch(x, st_code(act), B, C, HW, part, stream);
+    if (rc) return rc;
     return bn_apply_launch(x, y, B, C, HW, nullptr, (double)n, weight, bias, running_mean, running_var, momentum, eps,
                            act, save_mean, save_invstd, part, stream);
 }
@@ -610,26 +661,43 @@ extern "C" int ldm_batchnorm_train(float* x, int32_t B, int32_t C, int32_t HW, c
 // y may be NULL when act is NONE or RELU (bn_act_grad: the mask is re-evaluated from x)
 static bool bn_need_y(int act) { return act != LDM_ACT_NONE && act != LDM_ACT_RELU; }
 
+// the kernels' partial stage (dx == NULL) / apply stage of the BN backward under storage code sc
+static int bn_bwd_partial_launch(const void* dy, const void* y, const void* x, const float* save_mean,
+                                  const float* save_invstd, const float* weight, const float* bias, const StCode& sc,
+                                  int act, int32_t B, int32_t C, int32_t HW, double* part, void* stream) {
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    const int64_t S = slice_len(n, P);
+    const dim3 grid(P, C);
+    const bool v4 = vec_ok(HW, dy, y, x);
+    st_dispatch(sc, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (v4)
+            hipLaunchKernelGGL((bn_bwd_partial_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
+                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, part);
+        else
+            hipLaunchKernelGGL((bn_bwd_partial_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
+                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, part);
+    });
+    LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
+    return 0;
+}
+
 extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, const float* x, const float* save_mean,
                                              const float* save_invstd, const float* weight, const float* bias,
-                                             int32_t act, int32_t B, int32_t C, int32_t HW, double* sums,
+                                             int32_t act_code, int32_t B, int32_t C, int32_t HW, double* sums,
                                              float* dweight, float* dbias, float* workspace, void* stream) {
+    const StCode sc = st_code(act_code);
+    const int act = sc.act & 0xff;
     LDM_REQUIRE(save_mean && save_invstd && sums && workspace && B >= 0 && C > 0 && HW > 0 &&
                     ((dy && x && (y || !bn_need_y(act))) || B == 0),
                 "bn_backward_reduce: bad argument");
     LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward_reduce: workspace must be 8-byte aligned");
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
     double* part = reinterpret_cast<double*>(workspace);
-    const dim3 grid(P, C);
-    if (vec_ok(HW, dy, y, x))
-        hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, part);
-    else
-        hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, part);
-    LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
+    const int rc = bn_bwd_partial_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, part, stream);
+    if (rc) return rc;
     // local sums: db = sum g, dw = sum g*xhat (SyncBatchNorm keeps the parameter grads local)
     hipLaunchKernelGGL(slices_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
                        (hipStream_t)stream, part, C, P, sums, dbias, dweight, (double)n);
@@ -638,77 +706,82 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
 }
 
 // part != NULL: the sums come from bn_bwd_partial_kernel's slice partials, and dweight / dbias are written here
-static int bn_bwd_apply_launch(const float* dy, const float* y, const float* x, const float* save_mean,
-                               const float* save_invstd, const float* weight, const float* bias, int32_t act, int32_t B,
-                               int32_t C, int32_t HW, const double* sums, double count, float* dx, const double* part,
-                               float* dweight, float* dbias, void* stream) {
+static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, const float* save_mean,
+                               const float* save_invstd, const float* weight, const float* bias, const StCode& sc,
+                               int act, int32_t B, int32_t C, int32_t HW, const double* sums, double count, void* dx,
+                               const double* part, float* dweight, float* dbias, void* stream) {
     if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     const int64_t S = slice_len(n, P);
     const dim3 grid(P, C);
-    if (vec_ok(HW, dy, y, x, dx))
-        hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part, part ? P : 0, dweight,
-                           dbias);
-    else
-        hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part, part ? P : 0, dweight,
-                           dbias);
+    const bool v4 = vec_ok(HW, dy, y, x, dx);
+    st_dispatch(sc, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (v4)
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
+                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part,
+                               part ? P : 0, dweight, dbias);
+        else
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
+                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part,
+                               part ? P : 0, dweight, dbias);
+    });
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
     return 0;
 }
 
 extern "C" int ldm_batchnorm_backward_apply(const float* dy, const float* y, const float* x, const float* save_mean,
                                             const float* save_invstd, const float* weight, const float* bias,
-                                            int32_t act, int32_t B, int32_t C, int32_t HW, const double* sums,
+                                            int32_t act_code, int32_t B, int32_t C, int32_t HW, const double* sums,
                                             double count, float* dx, void* stream) {
+    const StCode sc = st_code(act_code);
+    const int act = sc.act & 0xff;
     LDM_REQUIRE(save_mean && save_invstd && sums && B >= 0 && C > 0 && HW > 0 &&
                     ((dy && x && dx && (y || !bn_need_y(act))) || B == 0),
                 "bn_backward_apply: bad argument");
-    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums, count, dx, nullptr,
-                               nullptr, nullptr, stream);
+    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, sums, count, dx,
+                               nullptr, nullptr, nullptr, stream);
 }
 
 extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, const float* save_mean,
-                                      const float* save_invstd, const float* weight, const float* bias, int32_t act,
+                                      const float* save_invstd, const float* weight, const float* bias, int32_t act_code,
                                       int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
                                       float* workspace, void* stream) {
     LDM_REQUIRE(workspace && B > 0 && C > 0 && HW > 0, "bn_backward: bad argument");
+    const StCode sc = st_code(act_code);
+    const int act = sc.act & 0xff;
     const int64_t n = (int64_t)B * HW;
     double* sums = reinterpret_cast<double*>(workspace) + (size_t)C * bn_slices(n, C) * 2;
     if (!dx)   // parameter grads only: partials + finalize
-        return ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, sums,
+        return ldm_batchnorm_backward_reduce(dy, y, x, save_mean, save_invstd, weight, bias, act_code, B, C, HW, sums,
                                              dweight, dbias, workspace, stream);
     LDM_REQUIRE(dy && x && save_mean && save_invstd && (y || !bn_need_y(act)), "bn_backward: bad argument");
     LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward: workspace must be 8-byte aligned");
-    const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
     double* part = reinterpret_cast<double*>(workspace);
-    const dim3 grid(P, C);
-    if (vec_ok(HW, dy, y, x))
-        hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, part);
-    else
-        hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x, save_mean,
-                           save_invstd, weight, bias, act, C, HW, n, S, part);
-    LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
+    const int rc = bn_bwd_partial_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, part, stream);
+    if (rc) return rc;
     // the apply sums the partials itself and writes dweight / dbias (no finalize launch)
-    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, act, B, C, HW, nullptr, (double)n, dx,
-                               part, dweight, dbias, stream);
+    return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, nullptr, (double)n,
+                               dx, part, dweight, dbias, stream);
 }
 
-extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
-                                int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
+extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
+                                int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
                                 void* stream) {
+    const StCode sc = st_code(act_code);
+    const int act = sc.act & 0xff;
     LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
     LDM_REQUIRE(act != LDM_ACT_GELU || pre_act, "act_backward: GELU needs the pre-activation");
     LDM_REQUIRE(act == LDM_ACT_NONE || act == LDM_ACT_GELU || act_out, "act_backward: needs the activation output");
     const bool sums = dbias || dbcast;
     const float* aval0 = act == LDM_ACT_NONE || act == LDM_ACT_GELU ? nullptr : act_out;
+    hipStream_t st = (hipStream_t)stream;
     if (HW <= 16) {
-        hipLaunchKernelGGL(act_bwd_small_kernel, dim3(C), dim3(kThreads), 0,
-                           (hipStream_t)stream, dy, aval0, pre_act, act, B, C, HW, dv, dbias, dbcast);
+        st_dispatch(sc, [&](auto stc) {
+            hipLaunchKernelGGL((act_bwd_small_kernel<decltype(stc)::value>), dim3(C), dim3(kThreads), 0, st, dy, aval0,
+                               pre_act, act, sc.sf, B, C, HW, dv, dbias, dbcast);
+        });
         LDM_CHECK_LAUNCH("act_bwd_small_kernel");
         return 0;
     }
@@ -720,14 +793,16 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         float* part = sums ? workspace : nullptr;
         const int tp = HW / 4;
         const unsigned blocks = (unsigned)((nplanes + kThreads / tp - 1) / (kThreads / tp));
-        hipStream_t st = (hipStream_t)stream;
-        switch (tp) {
-            case 16: hipLaunchKernelGGL(act_bwd_planes_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
-            case 32: hipLaunchKernelGGL(act_bwd_planes_kernel<32>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
-            case 64: hipLaunchKernelGGL(act_bwd_planes_kernel<64>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
-            case 128: hipLaunchKernelGGL(act_bwd_planes_kernel<128>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
-            default: hipLaunchKernelGGL(act_bwd_planes_kernel<256>, dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, nplanes, dvp, part); break;
-        }
+        st_dispatch(sc, [&](auto stc) {
+            constexpr int ST = decltype(stc)::value;
+            switch (tp) {
+                case 16: hipLaunchKernelGGL((act_bwd_planes_kernel<16, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 32: hipLaunchKernelGGL((act_bwd_planes_kernel<32, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 64: hipLaunchKernelGGL((act_bwd_planes_kernel<64, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 128: hipLaunchKernelGGL((act_bwd_planes_kernel<128, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                default: hipLaunchKernelGGL((act_bwd_planes_kernel<256, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+            }
+        });
         LDM_CHECK_LAUNCH("act_bwd_planes_kernel");
         if (sums) {
             hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, 1, dbias, dbcast);
@@ -738,17 +813,21 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
     const int Q = act_slices(B, C, HW);
     const int64_t S = ((HW + Q - 1) / Q + 3) & ~3;
     const dim3 grid(Q, B * C);
-    const float* aval = act == LDM_ACT_NONE || act == LDM_ACT_GELU ? nullptr : act_out;
+    const float* aval = aval0;
     float* part = sums ? workspace : nullptr;
-    if (vec_ok(HW, dy, aval, pre_act, dv))
-        hipLaunchKernelGGL(act_bwd_kernel<4>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, aval, pre_act, act, C,
-                           HW, S, dv, part);
-    else
-        hipLaunchKernelGGL(act_bwd_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, dy, aval, pre_act, act, C,
-                           HW, S, dv, part);
+    const bool v4 = vec_ok(HW, dy, aval, pre_act, dv);
+    st_dispatch(sc, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (v4)
+            hipLaunchKernelGGL((act_bwd_kernel<4, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
+                               HW, S, dv, part);
+        else
+            hipLaunchKernelGGL((act_bwd_kernel<1, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
+                               HW, S, dv, part);
+    });
     LDM_CHECK_LAUNCH("act_bwd_kernel");
     if (sums) {
-        hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, (hipStream_t)stream, part, B, C, Q,
+        hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, Q,
                            finalize_lanes(Q), dbias, dbcast);
         LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
     }

@@ -77,7 +77,7 @@ __device__ __forceinline__ floatx16 mma(const u16x8& a, const u16x8& b, const fl
                                                        0, 0, 0);
 }
 
-template <int BM, int DT>
+template <int BM, int DT, int XS>
 __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
     constexpr int MT = BM / 64;   // 32-row tiles per wave (2 waves along M)
     __shared__ __attribute__((aligned(16))) unsigned short bt[2][BN * KP];
@@ -114,29 +114,45 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
         gqy = a.fd_w.div(rr);
         gqx = rr - gqy * a.pt.Wq;
     }
+    // XS: x stored in 16 bits (LDM_DT_X16, the operand type DT): 2-byte gathers, staged without conversion
+    constexpr int XB = XS ? 2 : 4;   // bytes per input element
+    using GT = std::conditional_t<XS != 0, unsigned short, float>;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
-    const int gbase = (gb * a.Cin + gk * 16) * HWin;   // floats
-    auto gather = [&](int c, float (&gv)[16]) {
+        uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * XB), 0x00020000);
+    const int gbase = (gb * a.Cin + gk * 16) * HWin;   // elements
+    auto gather = [&](int c, GT (&gv)[16]) {
         const int cc = c / ntap;   // channel-chunk major, tap minor: the taps of a window run back to back
         const int t = c - cc * ntap;   // (wave-uniform)
         const int ci0 = cc * KC;
         const int iy = gqy * a.pt.sy + a.pt.dy[ph][t];
         const int ix = gqx * a.pt.sy + a.pt.dx[ph][t];
         const bool ok = gval && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-        const int voff = ok ? (gbase + ci0 * HWin + iy * a.Win + ix) * 4 : kOOB;
+        const int voff = ok ? (gbase + ci0 * HWin + iy * a.Win + ix) * XB : kOOB;
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-            gv[j] = (TCONV_DIAG & 1) ? (float)(voff + j)
-                                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, uni(j * HWin * 4), 0));
+        for (int j = 0; j < 16; ++j) {
+            if constexpr (XS != 0)
+                gv[j] = (TCONV_DIAG & 1) ? (GT)(voff + j)
+                                         : __builtin_amdgcn_raw_buffer_load_b16(xr, voff, uni(j * HWin * XB), 0);
+            else
+                gv[j] = (TCONV_DIAG & 1) ? (float)(voff + j)
+                                         : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, uni(j * HWin * XB), 0));
+        }
     };
-    auto stage = [&](int buf, const float (&gv)[16]) {
-        floatx8 lo, hi;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) lo[j] = gv[j], hi[j] = gv[8 + j];
+    auto stage = [&](int buf, const GT (&gv)[16]) {
         u16x8* dst = reinterpret_cast<u16x8*>(&bt[buf][gp * KP + gk * 16]);
-        dst[0] = to16<DT>(lo);
-        dst[1] = to16<DT>(hi);
+        if constexpr (XS != 0) {
+            u16x8 lo, hi;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) lo[j] = gv[j], hi[j] = gv[8 + j];
+            dst[0] = lo;
+            dst[1] = hi;
+        } else {
+            floatx8 lo, hi;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) lo[j] = gv[j], hi[j] = gv[8 + j];
+            dst[0] = to16<DT>(lo);
+            dst[1] = to16<DT>(hi);
+        }
     };
 
     // ---- A fragments: rows mbase + 32 i + r, k = 16 s + 8 h .. +7 of chunk c
@@ -163,7 +179,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
-    float gv[2][16];
+    GT gv[2][16];
     gather(0, gv[0]);
     loadA(0, aset[0]);
     loadA(min(1, nch - 1), aset[1]);
@@ -252,8 +268,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
                 }
                 v = rnd(apply_act(v, e.act));
                 const size_t o = obase + (size_t)co * a.Hout * a.Wout;
-                if (e.act_out) e.act_out[o] = v;
-                a.y[o] = v;
+                if (e.act_out) st1_st<DT>(e.act_out, o, e.y16, v);
+                st1_st<DT>(a.y, o, e.y16, v);
             }
     }
 }
@@ -316,7 +332,7 @@ __host__ __device__ constexpr int pk1_phase(int i) { return i < 1 ? 0 : (i < 3 ?
 __host__ __device__ constexpr int pk1_tap(int i) { return i < 1 ? i : (i < 3 ? i - 1 : (i < 5 ? i - 3 : i - 5)); }
 __host__ __device__ constexpr int pk1_ntap(int p) { return p == 0 ? 1 : (p == 3 ? 4 : 2); }
 
-template <int BM, int NT, int SY, int DT, int NS, int PK = 0>
+template <int BM, int NT, int SY, int DT, int NS, int PK = 0, int XS = 0>
 __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     constexpr int MT = BM / 64;
     constexpr int NACC = PK ? 4 : 1;
@@ -344,8 +360,10 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     const int imgsz = a.imgsz;   // 16-bit elements per image buffer (+ a 48-B dummy row after it)
 
     // ---- window super-units of this thread: 4 channels x one 16-byte column quad of one window row
+    // XS: x stored in 16 bits (the operand type DT): a quad is one 8-byte load, parked without conversion
+    constexpr int XB = XS ? 2 : 4;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * 4), 0x00020000);
+        uni_ptr(a.x), (short)0, uni(a.B * a.Cin * HWin * XB), 0x00020000);
     int svo[NS], slp[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -357,18 +375,24 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         const int q = rr >> 2, cg = rr & 3;
         const int iy = iyb + wr, ix = ixb + 4 * q;
         const bool ok = valid && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-        svo[s] = ok ? ((b * a.Cin + 4 * cg) * HWin + iy * a.Win + ix) * 4 : kOOB;
+        svo[s] = ok ? ((b * a.Cin + 4 * cg) * HWin + iy * a.Win + ix) * XB : kOOB;
         // (a slot past the window writes to the dummy row after the image: the store stays branch-free)
         slp[s] = valid ? (wr * a.rowp + (SY == 2 ? 2 * q : 4 * q)) * WP + 4 * cg : imgsz;
     }
-    floatx4 wv[NS][4];
+    using WV = std::conditional_t<XS != 0, uint2, floatx4>;   // one channel's column quad
+    WV wv[NS][4];
     auto load_win = [&](int w) {   // channels 16 w + 4 cg + i of every super-unit
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                wv[s][i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           xr, svo[s], uni((w * WCH + i) * HWin * 4), 0));
+            for (int i = 0; i < 4; ++i) {
+                if constexpr (XS != 0)
+                    wv[s][i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                             xr, svo[s], uni((w * WCH + i) * HWin * XB), 0));
+                else
+                    wv[s][i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                               xr, svo[s], uni((w * WCH + i) * HWin * XB), 0));
+            }
     };
     auto store_win = [&](int buf) {
         unsigned short* base = img + buf * (imgsz + WP);
@@ -376,13 +400,20 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         for (int s = 0; s < NS; ++s) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                floatx4 v{wv[s][0][k], wv[s][1][k], wv[s][2][k], wv[s][3][k]};
                 const int col = slp[s] == imgsz ? 0 : (SY == 2 ? ((k & 1) * a.half + (k >> 1)) : k);
                 uint2 pk;
-                if constexpr (DT == 1)
-                    pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, halfx4));
-                else
-                    pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+                if constexpr (XS != 0) {
+                    // column k of channels 0..3: the k-th 16-bit half of each channel's quad
+                    auto el = [&](int i) { return (k < 2 ? wv[s][i].x : wv[s][i].y) >> (16 * (k & 1)) & 0xffffu; };
+                    pk.x = el(0) | (el(1) << 16);
+                    pk.y = el(2) | (el(3) << 16);
+                } else {
+                    floatx4 v{wv[s][0][k], wv[s][1][k], wv[s][2][k], wv[s][3][k]};
+                    if constexpr (DT == 1)
+                        pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, halfx4));
+                    else
+                        pk = __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+                }
                 *reinterpret_cast<uint2*>(base + slp[s] + col * WP) = pk;
             }
         }
@@ -491,8 +522,8 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
                     if (co >= a.Cout) continue;
                     const float v = epi(acc[0][i][j][q], co);
                     const size_t o = obase + (size_t)co * a.Hout * a.Wout;
-                    if (e.act_out) e.act_out[o] = v;
-                    a.y[o] = v;
+                    if (e.act_out) st1_st<DT>(e.act_out, o, e.y16, v);
+                    st1_st<DT>(a.y, o, e.y16, v);
                 }
         }
     } else {
@@ -544,8 +575,14 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
                 const int ox = PK ? 2 * qx0 + c0 : qx0 + c0;
                 const floatx4 v = *reinterpret_cast<const floatx4*>(stg + cl * pitch + rest4);
                 const size_t o = ((size_t)b * a.Cout + co) * HWo + (size_t)oy * a.Wout + ox;
-                if (e.act_out) *reinterpret_cast<floatx4*>(e.act_out + o) = v;
-                *reinterpret_cast<floatx4*>(a.y + o) = v;
+                if (e.y16) {   // 16-bit storage: 8-byte stores of the four values
+                    const float vv[4] = {v[0], v[1], v[2], v[3]};
+                    if (e.act_out) st_st<DT, 4>(e.act_out, o, true, vv);
+                    st_st<DT, 4>(a.y, o, true, vv);
+                } else {
+                    if (e.act_out) *reinterpret_cast<floatx4*>(e.act_out + o) = v;
+                    *reinterpret_cast<floatx4*>(a.y + o) = v;
+                }
             }
         });
     }
@@ -596,15 +633,15 @@ static int layout(const ldm_conv_desc& d, int bm, PhaseTable& pt, int& Mpad, int
 // ---- the window form's geometry and launch ------------------------------------------------------------
 // Tap count and stride of one launch of the window form (template NT, SY); its image sizes (NS super-unit
 // slots per thread, LDS bytes) are checked here against the instance.
-template <int BM, int NT, int SY, int DT, int NS, int PK = 0>
-static int launch_w(WArgs& a, hipStream_t st) {
+template <int BM, int NT, int SY, int DT, int NS, int PK, int XS>
+static int launch_wx(WArgs& a, hipStream_t st) {
     LDM_REQUIRE(a.nsu <= NS * 256, "tconvw: window larger than the instance's register slots");
     // the image double buffer, or the epilogue's staged output tile if larger (BM channels x the pass's floats)
     const int cq = 1 << a.cq_log2;
     const size_t stage = NT == 4 ? 0 : (size_t)BM * ((PK ? 2 * BN : BN) + 4) * 4;
     const size_t lds = std::max((size_t)2 * (a.imgsz + WP) * 2, stage);
     (void)cq;
-    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK>;
+    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS>;
     if (lds > 64 * 1024) {
         static bool opted = false;
         if (!opted) {
@@ -617,6 +654,12 @@ static int launch_w(WArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(256), lds, st, a);
     LDM_CHECK_LAUNCH("tconvw_kernel");
     return 0;
+}
+
+template <int BM, int NT, int SY, int DT, int NS, int PK = 0>
+static int launch_w(WArgs& a, hipStream_t st) {
+    if (a.ep.x16) return launch_wx<BM, NT, SY, DT, NS, PK, DT>(a, st);
+    return launch_wx<BM, NT, SY, DT, NS, PK, 0>(a, st);
 }
 
 // Window geometry of the phases `phs` (same tap count) of a kind-3 conv; false when the tile / window shape
@@ -860,17 +903,20 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
             if (rc != 1) return rc;
         }
     }
+    const dim3 g((unsigned)blocks);
+#define TCK(BM_, DT_)                                                                          \
+    do {                                                                                       \
+        if (ep.x16) hipLaunchKernelGGL((tc::tconv_kernel<BM_, DT_, DT_>), g, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((tc::tconv_kernel<BM_, DT_, 0>), g, dim3(256), 0, s, a);        \
+    } while (0)
     if (p.tm == 2) {
-        if (p.tn == LDM_DT_F16)
-            hipLaunchKernelGGL((tc::tconv_kernel<128, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((tc::tconv_kernel<128, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+        if (p.tn == LDM_DT_F16) TCK(128, 1);
+        else TCK(128, 2);
     } else {
-        if (p.tn == LDM_DT_F16)
-            hipLaunchKernelGGL((tc::tconv_kernel<64, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((tc::tconv_kernel<64, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+        if (p.tn == LDM_DT_F16) TCK(64, 1);
+        else TCK(64, 2);
     }
+#undef TCK
     LDM_CHECK_LAUNCH("tconv_kernel");
     return 0;
 }

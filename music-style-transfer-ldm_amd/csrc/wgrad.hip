@@ -40,6 +40,7 @@ struct Args {
     int32_t wr, wca, e;   // window rows, row pitch (floats, multiple of 4), column shift of the aligned origin
     int32_t pitch_c;      // floats per channel in the window (wr * wca)
     int32_t lowp;         // LDM_DT_*: operands rounded to fp16 / bf16, fp32 accumulation
+    int32_t dense16;      // wgrad_c1_kernel XS != 0: Dense stored in 16 bits (register-staged, see wgrad_lp_kernel)
 };
 
 template <int B_, int E_, class F>
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // kernel spent 15/16 of its window DMAs and MFMAs on padding channels there).  Block = 4 waves x 16 rows
 // (m) x 16 columns (taps; k = 3 leaves 7 idle); the lane of column t reads its tap's window value, so the
 // whole 16 x 16 x (64 positions) product of a chunk is 4 (16 in f32) MFMAs per wave.
-template <int S, int KK, int DT>
+template <int S, int KK, int DT, int XS = 0>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
     constexpr int T = KK * KK, BM = 64, AF = BM * kKQ;
     static_assert(T <= 16, "taps per column tile");
@@ -229,10 +230,58 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
     const int bufF = buf_floats(AF, 1, a.pitch_c);
     const int ch_begin = blockIdx.z * a.per_split;
     const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const bool d16 = XS != 0 && a.dense16;
     const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * (d16 ? 2 : 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         uni_ptr(a.gath), (short)0, uni(a.B * a.Hg * a.Wg * 4), 0x00020000);
+
+    // XS != 0: the Dense rows register-staged (16-bit quads widened when parked at the DMA's addresses); the
+    // window (the fp32 input of a Cin = 1 layer) keeps its DMA
+    uint4 rd[XS ? BM / 16 : 1];
+    auto fetch_dense = [&](int ch) {
+        const int b = ch / a.cps;
+        const int r = ch - b * a.cps;
+        int qy0, qx0;
+        if (a.cols == a.Wq) {
+            qy0 = r * a.rows, qx0 = 0;
+        } else {
+            const int segs = a.Wq / kKQ;
+            qy0 = r / segs, qx0 = (r - qy0 * segs) * kKQ;
+        }
+#pragma unroll
+        for (int i = 0; i < BM / 16; ++i) {
+            const int gi = wave + 4 * i;
+            const int row = gi * 4 + (lane >> 4);
+            const int p = lane & 15;
+            const int sp = p ^ (row & 15);
+            const int m = m0 + row;
+            const int ql = sp * 4;
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const bool ok = m < a.M && qy < a.Hq;
+            const int el = ((b * a.M + m) * HQ + qy * a.Wq + qx);
+            if (d16) {
+                const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(dr, ok ? el * 2 : kOOB, 0, 0));
+                rd[i] = uint4{t.x, t.y, 0u, 0u};
+            } else {
+                rd[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? el * 4 : kOOB, 0, 0));
+            }
+        }
+    };
+    auto park_dense = [&](int buf) {
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+#pragma unroll
+        for (int i = 0; i < BM / 16; ++i) {
+            const int gi = wave + 4 * i;
+            floatx4 v;
+            if (d16)
+                v = floatx4{from16<XS>((unsigned short)(rd[i].x & 0xffff)), from16<XS>((unsigned short)(rd[i].x >> 16)),
+                            from16<XS>((unsigned short)(rd[i].y & 0xffff)), from16<XS>((unsigned short)(rd[i].y >> 16))};
+            else
+                v = __builtin_bit_cast(floatx4, rd[i]);
+            *reinterpret_cast<floatx4*>(base + gi * 1024 + lane * 16) = v;
+        }
+    };
 
     auto issue = [&](int ch, int buf) {
         int b, qy0, qx0;
@@ -245,7 +294,7 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
             qy0 = r / segs, qx0 = (r - qy0 * segs) * kKQ;
         }
         char* base = reinterpret_cast<char*>(smem + buf * bufF);
-        for (int gi = wave; gi < BM / 4; gi += 4) {
+        for (int gi = wave; gi < (XS ? 0 : BM / 4); gi += 4) {
             const int row = gi * 4 + (lane >> 4);
             const int p = lane & 15;
             const int sp = p ^ (row & 15);
@@ -282,12 +331,21 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
         boff[u] = AF + (rl * S + ky) * a.wca + a.e + xl * S + kx;
     }
 
-    if (ch_begin < ch_end) issue(ch_begin, 0);
+    if (ch_begin < ch_end) {
+        issue(ch_begin, 0);
+        if constexpr (XS != 0) {
+            fetch_dense(ch_begin);
+            park_dense(0);
+        }
+    }
     for (int ch = ch_begin; ch < ch_end; ++ch) {
         const int buf = (ch - ch_begin) & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+        if (ch + 1 < ch_end) {
+            issue(ch + 1, buf ^ 1);
+            if constexpr (XS != 0) fetch_dense(ch + 1);
+        }
         const float* sb = smem + buf * bufF;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -301,6 +359,9 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(Args a) {
             } else {
                 acc = mma16_lowp<DT>(fa, bv, acc);
             }
+        }
+        if constexpr (XS != 0) {
+            if (ch + 1 < ch_end) park_dense(buf ^ 1);
         }
     }
     // D: row m = m0 + 16*wave + 4*lg + r, column = tap col
@@ -354,7 +415,10 @@ struct LpArgs {
     int32_t B, M, C, Hq, Wq, Hg, Wg;
     int32_t cols, rows, cps, nchunk, per_split;
     int32_t wr, wca, pitch_c;   // window rows, row pitch, channel pitch (floats)
+    int32_t dense16, gath16;    // 16-bit storage of dense / gath (the register-staged instances, XS != 0)
 };
+// window pieces per lane of the register-staged instances (checked by lp_plan)
+constexpr int kLpStagedPieces = 12;
 
 __host__ __device__ constexpr int lp_nb(int S, int KK) { return (3 + 7 * S + KK + 3) / 4; }   // b128 reads per k-step
 __host__ __device__ inline int lp_buf_floats(int bm, int qc, int pitch_c) {
@@ -366,7 +430,11 @@ template <int PPR>
 __host__ __device__ constexpr int lp_swz(int row) { return (row >> 1) & (PPR - 1); }
 
 // QC positions per chunk: 32 (two k-steps), or 16 (one; the 2 x 8 planes of the UNet bottom)
-template <int S, int KK, int BM, int WM, int QC, int DT>
+// XS = 0: both tiles arrive by LDS DMA (fp32 tensors).  XS = the 16-bit storage type (LDM_DT_X16 / _DY16
+// tensors): the tiles are register-staged instead (a DMA cannot widen 16-bit elements to the floats the
+// compute side reads): the next chunk's pieces are loaded into registers during this chunk's MFMAs, widened
+// and parked in LDS at the addresses the DMA would have written, so the compute side is the same.
+template <int S, int KK, int BM, int WM, int QC, int DT, int XS = 0>
 __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
     constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp_nb(S, KK);
     constexpr int PPR = QC / 4, RPI = 64 / PPR, NKS = QC / 16;   // pieces per row, rows per DMA instr, k-steps
@@ -381,10 +449,11 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
     const int bufF = lp_buf_floats(BM, QC, a.pitch_c);
     const int ch_begin = blockIdx.z * a.per_split;
     const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const bool d16 = XS != 0 && a.dense16, g16 = XS != 0 && a.gath16;
     const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * (d16 ? 2 : 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 4), 0x00020000);
+        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * (g16 ? 2 : 4)), 0x00020000);
 
     // chunk ch -> sample, first row, first column; its DMAs into buffer buf
     auto issue = [&](int ch, int buf) {
@@ -425,6 +494,79 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
         }
     };
 
+    // ---- register-staged form (XS != 0): the same pieces as issue(), loaded as 16-byte fp32 quads or 8-byte
+    //      16-bit quads (element offsets as issue()'s), widened to floats when parked
+    constexpr int ND = (BM / RPI + NW - 1) / NW, NWPC = kLpStagedPieces;
+    uint4 rd[XS ? ND : 1], rw[XS ? NWPC : 1];
+    auto fetch = [&](int ch) {
+        const int b = ch / a.cps;
+        const int rr = ch - b * a.cps;
+        int qy0, qx0;
+        if (a.cols == a.Wq) {
+            qy0 = rr * a.rows, qx0 = 0;
+        } else {
+            const int segs = a.Wq / QC;
+            qy0 = rr / segs, qx0 = (rr - qy0 * segs) * QC;
+        }
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const int gi = wave + i * NW;
+            const int row = gi * RPI + lane / PPR;
+            const int sp = (lane % PPR) ^ lp_swz<PPR>(row);
+            const int ql = sp * 4;
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const int m = m0 + row;
+            const int el = ((b * a.M + m) * HQ + qy * a.Wq + qx);
+            const bool ok = gi < BM / RPI && m < a.M;
+            if (d16) {
+                const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(dr, ok ? el * 2 : kOOB, 0, 0));
+                rd[i] = uint4{t.x, t.y, 0u, 0u};
+            } else {
+                rd[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? el * 4 : kOOB, 0, 0));
+            }
+        }
+        const int wq4 = a.wca >> 2, pq = a.pitch_c >> 2;
+        const int npiece = kLC * pq;
+        const int row0 = qy0 * S - 1, colA = qx0 * S - 4;
+#pragma unroll
+        for (int i = 0; i < NWPC; ++i) {
+            const int pc = (wave + i * NW) * 64 + lane;
+            const int cl = pc / pq;
+            const int rem = pc - cl * pq;
+            const int wrow = rem / wq4, wp = rem - wrow * wq4;
+            const int c = c0 + cl, iy = row0 + wrow, ix = colA + wp * 4;
+            const bool ok = pc < npiece && c < a.C && wrow < a.wr && (unsigned)iy < (unsigned)a.Hg &&
+                            (unsigned)ix < (unsigned)a.Wg;
+            const int el = (((b * a.C + c) * a.Hg + iy) * a.Wg + ix);
+            if (g16) {
+                const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(gr, ok ? el * 2 : kOOB, 0, 0));
+                rw[i] = uint4{t.x, t.y, 0u, 0u};
+            } else {
+                rw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(gr, ok ? el * 4 : kOOB, 0, 0));
+            }
+        }
+    };
+    auto widen = [&](const uint4& v, bool h16) {
+        if (!h16) return __builtin_bit_cast(floatx4, v);
+        return floatx4{from16<XS>((unsigned short)(v.x & 0xffff)), from16<XS>((unsigned short)(v.x >> 16)),
+                       from16<XS>((unsigned short)(v.y & 0xffff)), from16<XS>((unsigned short)(v.y >> 16))};
+    };
+    auto park = [&](int buf) {
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const int gi = wave + i * NW;
+            if (gi < BM / RPI) *reinterpret_cast<floatx4*>(base + gi * 1024 + lane * 16) = widen(rd[i], d16);
+        }
+        const int npiece = kLC * (a.pitch_c >> 2);
+#pragma unroll
+        for (int i = 0; i < NWPC; ++i) {
+            const int gi = wave + i * NW;
+            if (gi * 64 < npiece)
+                *reinterpret_cast<floatx4*>(base + BM * QC * 4 + gi * 1024 + lane * 16) = widen(rw[i], g16);
+        }
+    };
+
     floatx16 acc[MF][KK];
 #pragma unroll
     for (int f = 0; f < MF; ++f)
@@ -448,13 +590,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
         boff[ks] = BM * QC + r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S;
     }
 
-    if (ch_begin < ch_end) issue(ch_begin, 0);
-    for (int ch = ch_begin; ch < ch_end; ++ch) {
-        const int buf = (ch - ch_begin) & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // chunk ch landed; every wave is done with the other buffer
-        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
-        const float* sb = smem + buf * bufF;
+    auto compute = [&](const float* sb) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             floatx8 fa[MF];
@@ -478,6 +614,29 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
 #pragma unroll
                 for (int f = 0; f < MF; ++f) acc[f][kx] = mma32x16<DT>(fa[f], fb, acc[f][kx]);
             }
+        }
+    };
+    if constexpr (XS == 0) {
+        if (ch_begin < ch_end) issue(ch_begin, 0);
+        for (int ch = ch_begin; ch < ch_end; ++ch) {
+            const int buf = (ch - ch_begin) & 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // chunk ch landed; every wave is done with the other buffer
+            if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+            compute(smem + buf * bufF);
+        }
+    } else {
+        if (ch_begin < ch_end) {
+            fetch(ch_begin);
+            park(0);
+        }
+        for (int ch = ch_begin; ch < ch_end; ++ch) {
+            const int buf = (ch - ch_begin) & 1;
+            __syncthreads();   // chunk ch parked by every wave; every wave is done with the other buffer
+            const bool more = ch + 1 < ch_end;
+            if (more) fetch(ch + 1);   // in flight during this chunk's MFMAs
+            compute(smem + buf * bufF);
+            if (more) park(buf ^ 1);
         }
     }
 
@@ -556,9 +715,9 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     return true;
 }
 
-template <int S, int KK, int BM, int WM, int QC, int DT>
-int launch_lp_dt(const LpPlan& p, hipStream_t st) {
-    auto kfn = wgrad_lp_kernel<S, KK, BM, WM, QC, DT>;
+template <int S, int KK, int BM, int WM, int QC, int DT, int XS>
+int launch_lp_xs(const LpPlan& p, hipStream_t st) {
+    auto kfn = wgrad_lp_kernel<S, KK, BM, WM, QC, DT, XS>;
     static bool opted = false;
     if (!opted) {
         LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -568,6 +727,11 @@ int launch_lp_dt(const LpPlan& p, hipStream_t st) {
     hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * KK), p.lds_bytes, st, p.a);
     LDM_CHECK_LAUNCH("wgrad_lp_kernel");
     return 0;
+}
+template <int S, int KK, int BM, int WM, int QC, int DT>
+int launch_lp_dt(const LpPlan& p, hipStream_t st) {
+    if (p.a.dense16 || p.a.gath16) return launch_lp_xs<S, KK, BM, WM, QC, DT, DT>(p, st);
+    return launch_lp_xs<S, KK, BM, WM, QC, DT, 0>(p, st);
 }
 template <int S, int KK, int QC, int DT>
 int launch_lp_bm(const LpPlan& p, hipStream_t st) {
@@ -654,9 +818,11 @@ int launch_dt(const Plan& p, hipStream_t st) {
 
 template <int S, int KK, int DT>
 int launch_c1_dt(const Plan& p, hipStream_t st) {
-    auto kfn = wgrad_c1_kernel<S, KK, DT>;
     dim3 grid(1, (p.a.M + 63) / 64, p.splits);
-    hipLaunchKernelGGL(kfn, grid, dim3(256), p.lds_bytes, st, p.a);
+    if (DT != 0 && p.a.dense16)
+        hipLaunchKernelGGL((wgrad_c1_kernel<S, KK, DT, DT>), grid, dim3(256), p.lds_bytes, st, p.a);
+    else
+        hipLaunchKernelGGL((wgrad_c1_kernel<S, KK, DT, 0>), grid, dim3(256), p.lds_bytes, st, p.a);
     LDM_CHECK_LAUNCH("wgrad_c1_kernel");
     return 0;
 }
@@ -698,20 +864,44 @@ bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats) {
 
 // Runs the tap-shared kernel into `partial` ([splits][M][N]); returns the split count through `splits`,
 // or -1 when the form does not apply.
+// the register-staged instances hold at most kLpStagedPieces window pieces per lane
+static bool lp_staged_fits(const wg::LpPlan& lp) {
+    const int nw = lp.WM * lp.KK;
+    const int npiece = wg::kLC * (lp.a.pitch_c >> 2);
+    return (npiece + 64 * nw - 1) / (64 * nw) <= wg::kLpStagedPieces;
+}
+
+// Which tensors of the weight gradient of d may be stored in 16 bits (LDM_DT_X16 | LDM_DT_DY16) at a 16-bit
+// operand precision: the double-rate form's register-staged instances take both, the one-channel kernel
+// (Cin = 1 layers) a 16-bit Dense (dy of a conv); else none.
+int wgrad2_storage16(const ldm_conv_desc& d) {
+    wg::Plan p;
+    if (!wg::plan(d, p)) return 0;
+    wg::LpPlan lp;
+    if (!wgrad_lp_disabled() && wg::lp_plan(d, lp) && lp_staged_fits(lp)) return LDM_DT_X16 | LDM_DT_DY16;
+    if (p.BC == 1) return d.transposed ? LDM_DT_X16 : LDM_DT_DY16;
+    return 0;
+}
+
+// st16: bit 0 Dense, bit 1 Gath stored in 16 bits (-2: not on this layer's forms)
 int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
-               hipStream_t st) {
+               hipStream_t st, int st16) {
     wg::Plan p;
     if (!wg::plan(d, p)) return -1;
     if (dtype != LDM_DT_F32 && !wgrad_lp_disabled()) {   // 16-bit operands: the double-rate MFMA form
         wg::LpPlan lp;
-        if (wg::lp_plan(d, lp)) {
+        if (wg::lp_plan(d, lp) && (!st16 || lp_staged_fits(lp))) {
             lp.a.dense = dense;
             lp.a.gath = gath;
             lp.a.partial = partial;
+            lp.a.dense16 = st16 & 1;
+            lp.a.gath16 = (st16 >> 1) & 1;
             splits = lp.splits;
             return dtype == LDM_DT_F16 ? wg::launch_lp<1>(lp, st) : wg::launch_lp<2>(lp, st);
         }
     }
+    if (st16 && (p.BC != 1 || (st16 & 2) || dtype == LDM_DT_F32)) return -2;
+    p.a.dense16 = st16 & 1;
     p.a.lowp = dtype;
     p.a.dense = dense;
     p.a.gath = gath;

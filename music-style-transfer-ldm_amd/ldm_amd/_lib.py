@@ -62,6 +62,9 @@ class UNetWeights(ctypes.Structure):
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
 DT_ROUND_OUT = 0x100   # ldm_epilogue.dtype flag (ldm_capi.h LDM_DT_ROUND_OUT); act codes: LDM_ACT_ROUND_* = dt << 8
+# 16-bit storage (ldm_capi.h): conv / wgrad dtype flags, and the BatchNorm / activation-backward act-code fields
+DT_X16, DT_Y16, DT_DY16 = 0x200, 0x400, 0x800
+ST_SHIFT, ST_X16, ST_Y16, ST_DY16, ST_DX16 = 16, 1 << 18, 1 << 19, 1 << 20, 1 << 21
 
 # name -> (restype, argtypes).  Kept in one table so tests can check it against include/ldm_capi.h.
 SIGNATURES = {
@@ -155,6 +158,9 @@ SIGNATURES = {
                                   c_fp, c_int32, c_float, c_fp, c_fp, c_int64, c_fp, c_vp]),
     # backward / optimiser
     "ldm_conv_tiled_plan": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, ctypes.POINTER(ConvPlan)]),
+    "ldm_conv_storage16": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan)]),
+    "ldm_conv_wgrad_storage16": (c_int32, [ctypes.POINTER(ConvDesc)]),
+    "ldm_batchnorm_stats_code": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),
     "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
     "ldm_conv_backward_weight_dt": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_int32, c_vp]),
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),

@@ -79,7 +79,11 @@ def conv(x, weight, bias, *, stride, padding, transposed=False, output_padding=0
             d = _conv_desc(x_, w_, cfg)
             aout = torch.empty((d.B, d.Cout, d.Hout, d.Wout), device=x_.device, dtype=torch.float32)
         dt = ops.autocast_dt()
-        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, dtype=dt, **cfg)
+        # the large maps of an autocast region stored in 16 bits, as ATen's (ops.store16_dtype)
+        d = _conv_desc(x_, w_, cfg)
+        odt = ops.store16_dtype(d.B * d.Cout * d.Hout * d.Wout, dt)
+        y = ops.conv_forward(x_, w_, b_, bn=bn_eval, bcast=bc_, skip=sk_, wkey=wkey, act_out=aout, dtype=dt,
+                             out_dtype=odt, **cfg)
         store["dtype"] = dt      # the backward convs run at the forward's autocast precision
         store["round"] = bool(ops.autocast_out(dt) & L.DT_ROUND_OUT)   # ... and output semantics
         store["cfg"] = cfg
@@ -102,7 +106,7 @@ def _conv_backward(ctx, gy):
     act = cfg["act"]
     if act == "gelu":
         raise NotImplementedError("conv backward with a fused GELU epilogue (apply GELU as its own op)")
-    gy = ops.f32c(gy)
+    gy = gy.contiguous()   # (a 16-bit map's gradient stays 16-bit: the kernels below read it as stored)
     need_v = nx or nw or nb
     gv, gb, gbc = ops.act_backward(gy, act, act_out=a, need_dv=need_v, need_bias=nb and bn is None,
                                    need_bcast=nbc)
@@ -114,8 +118,8 @@ def _conv_backward(ctx, gy):
             _, gb, _ = ops.act_backward(gv, "none", need_dv=False, need_bias=True)
     desc = _conv_desc(x, w, cfg)
     dt = ctx.store.get("dtype", 0)
-    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt, round_out=ctx.store.get("round", False)) \
-        if nx else None
+    gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt, round_out=ctx.store.get("round", False),
+                                out_dtype=x.dtype) if nx else None
     gw = ops.conv_backward_weight(x, gv, desc, dtype=dt) if nw else None
     if gbc is not None:
         gbc = gbc.reshape(ctx.store["bc_shape"])
@@ -240,7 +244,8 @@ def batchnorm(x, bn_module, act="none"):
     sync = sync_group_for(m) if m.training else False
 
     def fwd_train(store, x_, w_, b_):
-        xc = ops.f32c(x_)
+        # a 16-bit input map (16-bit storage) gives a 16-bit output, as ATen's BatchNorm under autocast
+        xc = x_.contiguous() if x_.dtype in ops.T16 else ops.f32c(x_)
         y = torch.empty_like(xc)
         sm, si = ops.batchnorm_train_(xc, w_, b_, rm, rv, momentum if momentum is not None else 0.0, m.eps,
                                       act, save=True, sync=sync, out=y)

@@ -48,6 +48,68 @@ def f32c(t):
     return t.contiguous()
 
 
+# ---- 16-bit storage of the train step's large maps -------------------------------------------------------
+# Inside a torch.autocast region ATen stores conv / BatchNorm / activation outputs as fp16 / bf16 tensors (and
+# autograd their gradients likewise).  Maps of at least LDM_AMD_STORE16_MIN elements (default 2^22: the VAE and
+# style-encoder maps at the train batch) are stored that way here too, where the kernels that produce and read
+# them take 16-bit storage (ldm_conv_storage16 / ldm_conv_wgrad_storage16; BatchNorm and the activation
+# backward always); anything else reads a 16-bit tensor through an fp32 copy.  LDM_AMD_STORE16=0: fp32 maps.
+T16 = {torch.float16: 1, torch.bfloat16: 2}
+TORCH16 = {1: torch.float16, 2: torch.bfloat16}
+
+
+def store16_dtype(numel, dt):
+    """The torch dtype a new map of `numel` elements is stored in at operand precision dt (fp32 or 16-bit)."""
+    if dt in TORCH16 and os.environ.get("LDM_AMD_STORE16", "1") != "0" and \
+            numel >= int(os.environ.get("LDM_AMD_STORE16_MIN", str(1 << 22))):
+        return TORCH16[dt]
+    return torch.float32
+
+
+def in16(t, dt, ok=True):
+    """(contiguous tensor, is16) as a kernel reads t: a 16-bit t of type dt as it is when ok, else fp32."""
+    if t.dtype == torch.float32:
+        return t.contiguous(), False
+    if ok and T16.get(t.dtype) == dt:
+        return t.contiguous(), True
+    return f32c(t), False
+
+
+def st_code(dt, **flags):
+    """BatchNorm / activation-backward storage bits of an act code: the 16-bit type and the LDM_ST_* flags
+    (x16, y16, dy16, dx16) that are set."""
+    names = {"x16": L.ST_X16, "y16": L.ST_Y16, "dy16": L.ST_DY16, "dx16": L.ST_DX16}
+    bits = 0
+    for k, v in flags.items():
+        if v:
+            bits |= names[k]
+    return ((int(dt) << L.ST_SHIFT) | bits) if bits else 0
+
+
+_ST16_CACHE = {}
+
+
+def conv_storage16(desc, plan, dt):
+    """LDM_DT_X16 | LDM_DT_Y16 bits the conv kernels take for (desc, plan) at operand precision dt."""
+    if not dt:
+        return 0
+    key = ("f", desc.key(), plan.kind, plan.tm, plan.tn)
+    v = _ST16_CACHE.get(key)
+    if v is None:
+        v = _ST16_CACHE[key] = int(L.load().ldm_conv_storage16(byref(desc), byref(plan)))
+    return v
+
+
+def wgrad_storage16(desc, dt):
+    if not dt:
+        return 0
+    key = ("w", desc.key())
+    v = _ST16_CACHE.get(key)
+    if v is None:
+        v = _ST16_CACHE[key] = int(L.load().ldm_conv_wgrad_storage16(byref(desc)))
+    return v
+
+
 # ------------------------------------------------------------------------------------------------
 # plans and packed weights
 # ------------------------------------------------------------------------------------------------
@@ -253,11 +315,13 @@ class PackSet:
 # convolution with fused epilogue
 # ------------------------------------------------------------------------------------------------
 def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False, output_padding=0, bn=None,
-                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None, act_out=None, dtype=None):
+                 act="none", bcast=None, skip=None, out=None, plan=None, wkey=None, act_out=None, dtype=None,
+                 out_dtype=None):
     """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps).
-    act_out (preallocated, output-shaped) also receives act(.) before the adds."""
-    require_device(x, weight, bias, bcast, skip)
-    x = f32c(x)
+    act_out (preallocated, output-shaped) also receives act(.) before the adds.  x may be a 16-bit map of the
+    operand type; out_dtype = that 16-bit type asks for a 16-bit y where the kernel stores one (else fp32)."""
+    require_device(x, dtype=None)
+    require_device(weight, bias, bcast, skip)
     B, Cin, H, W = x.shape
     if transposed:
         cin_w, Cout, kh, kw = weight.shape
@@ -276,10 +340,14 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
         plan = tiled_plan(desc, dt)
     plan = plan or get_plan(desc)
     wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
-    y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device, dtype=torch.float32)
+    st = conv_storage16(desc, plan, dt)
+    x, xh = in16(x, dt, st & L.DT_X16)
+    y16 = out is None and act_out is None and T16.get(out_dtype) == dt and bool(st & L.DT_Y16)
+    y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device,
+                                                dtype=out_dtype if y16 else torch.float32)
     ep = L.Epilogue()
     ep.bias = _p(bias)
-    ep.dtype = autocast_out(dt)
+    ep.dtype = autocast_out(dt) | (L.DT_X16 if xh else 0) | (L.DT_Y16 if y16 else 0)
     keep = []
     if bn is not None:
         g, b_, m, v, eps = bn
@@ -342,16 +410,22 @@ def dual_desc(desc):
     return d
 
 
-def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False):
+def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False, out_dtype=None):
     """dX of the conv/convT `desc` for the pre-epilogue gradient dy (forward kernel on the dual desc);
     dtype = LDM_DT_* operand precision (the forward's autocast precision); round_out: dX rounded to it as well
-    (the reference's data gradient of a 16-bit conv is a 16-bit tensor)."""
+    (the reference's data gradient of a 16-bit conv is a 16-bit tensor); out_dtype: a 16-bit dX where the
+    kernel stores one (the gradient of a 16-bit map; fp32 otherwise)."""
     dd = dual_desc(desc)
-    plan = tiled_plan(dd, int(dtype)) or get_plan(dd)
+    dtype = int(dtype)
+    plan = tiled_plan(dd, dtype) or get_plan(dd)
     wbuf = packed_weight(weight, dd, plan, *(wkey or ()))
-    dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device, dtype=torch.float32)
+    st = conv_storage16(dd, plan, dtype)
+    dy, dyh = in16(dy, dtype, st & L.DT_X16)
+    d16 = T16.get(out_dtype) == dtype and bool(st & L.DT_Y16)
+    dx = torch.empty((desc.B, desc.Cin, desc.Hin, desc.Win), device=dy.device,
+                     dtype=out_dtype if d16 else torch.float32)
     ep = L.Epilogue()
-    ep.dtype = autocast_out(dtype, round_out)
+    ep.dtype = autocast_out(dtype, round_out) | (L.DT_X16 if dyh else 0) | (L.DT_Y16 if d16 else 0)
     L.call("ldm_conv_forward_ws", byref(dd), byref(plan), dy.data_ptr(), _p(wbuf), byref(ep), dx.data_ptr(),
            split_workspace(plan, dy.device), stream_handle())
     return dx
@@ -396,8 +470,10 @@ def split_workspace(plan, device):
 def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
     """dW (torch layout) of conv/convT `desc` from its input x and pre-epilogue gradient dy; dtype =
     LDM_DT_* operand precision."""
-    x = f32c(x)
-    dy = f32c(dy)
+    dtype = int(dtype)
+    st = wgrad_storage16(desc, dtype)
+    x, xh = in16(x, dtype, st & L.DT_X16)
+    dy, dyh = in16(dy, dtype, st & L.DT_DY16)
     if desc.transposed:
         shape = (desc.Cin, desc.Cout, desc.kh, desc.kw)
     else:
@@ -406,14 +482,19 @@ def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
         dw = torch.empty(shape, device=x.device, dtype=torch.float32)
     ws = scratch("wgrad", L.load().ldm_conv_wgrad_workspace_floats(byref(desc)), x.device)
     L.call("ldm_conv_backward_weight_dt", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate),
-           ws.data_ptr(), int(dtype), stream_handle())
+           ws.data_ptr(), dtype | (L.DT_X16 if xh else 0) | (L.DT_DY16 if dyh else 0), stream_handle())
     return dw
 
 
 def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=False, need_bcast=False, db_out=None):
     """(dv, dbias, dbcast) of y = act(v) (+bcast[b,c]) (+skip) for NCHW dy; db_out (contiguous [C]) receives
-    dbias in place of a new tensor."""
-    dy = f32c(dy)
+    dbias in place of a new tensor.  dy and act_out may be 16-bit maps (one 16-bit type); dv is stored like dy."""
+    st = T16.get(dy.dtype) or (T16.get(act_out.dtype) if act_out is not None else None) or 0
+    dy, dyh = in16(dy, st)
+    if act_out is not None:
+        act_out, ah = in16(act_out, st)
+    else:
+        ah = False
     B, C = dy.shape[0], dy.shape[1]
     HW = dy.numel() // max(1, B * C)
     dv = (dy if act == "none" else torch.empty_like(dy)) if need_dv else None
@@ -425,8 +506,9 @@ def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=Fa
     if act == "none" and not need_bias and not need_bcast:
         return dv, None, None
     ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
-    L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(pre_act), L.ACT[act], B, C, HW,
-           _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), stream_handle())
+    code = L.ACT[act] | st_code(st, x16=ah, dy16=dyh, dx16=dyh and dv is not None)
+    L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)), code, B, C,
+           HW, _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), stream_handle())
     return dv, db, dbc
 
 
@@ -470,32 +552,38 @@ def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=Tr
     per-rank sums and the per-rank element count travel in ONE fp64 all-reduce of 2C+1 values; the apply
     stage reads the global count on the device (reduce.hip), so there is no host synchronisation.  For act
     none / relu the output y is not read (the ReLU mask is re-evaluated from x, weight and bias)."""
-    dy = f32c(dy)
+    # 16-bit maps (one 16-bit type): dy, x, y as stored; dx stored like x (the gradient of the BN input)
+    st = T16.get(dy.dtype) or T16.get(x.dtype) or 0
+    dy, dyh = in16(dy, st)
+    x, xh = in16(x, st)
     B, C = dy.shape[0], dy.shape[1]
     HW = max(1, math.prod(dy.shape[2:]))
-    dx = torch.empty_like(dy) if need_dx else None
+    dx = torch.empty(dy.shape, device=dy.device, dtype=x.dtype) if need_dx else None
     dw = torch.empty(C, device=dy.device, dtype=torch.float32) if need_w else None
     db = torch.empty(C, device=dy.device, dtype=torch.float32) if need_b else None
     ws = reduce_workspace(B, C, HW, dy.device)
+    yh = False
     if act in ("none", "relu"):
         y = None
+    elif y is not None:
+        y, yh = in16(y, st)
+    code = L.ACT[act] | st_code(st, x16=xh, y16=yh, dy16=dyh, dx16=xh and need_dx)
     pg = _sync_group(sync)
-    x = f32c(x)
     if pg is None:
         L.call("ldm_batchnorm_backward", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
-               save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW, _p(dx), _p(dw), _p(db),
+               save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, _p(dx), _p(dw), _p(db),
                ws.data_ptr(), stream_handle())
         return dx, dw, db
     # SyncBatchNorm: local sums (+ local count) -> all-reduce -> dx with the global count (parameter
     # grads stay local, as in torch.nn.SyncBatchNorm)
     sums = torch.empty(2 * C + 1, device=dy.device, dtype=torch.float64)
     L.call("ldm_batchnorm_backward_reduce", _p(dy if B else None), _p(y if B else None), _p(x if B else None),
-           save_mean.data_ptr(), save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW,
+           save_mean.data_ptr(), save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW,
            sums.data_ptr(), _p(dw), _p(db), ws.data_ptr(), stream_handle())
     _allreduce_sum(sums, pg.pg)
     if dx is not None and B:
         L.call("ldm_batchnorm_backward_apply", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
-               save_invstd.data_ptr(), _p(weight), _p(bias), L.ACT[act], B, C, HW, sums.data_ptr(), -1.0,
+               save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, sums.data_ptr(), -1.0,
                dx.data_ptr(), stream_handle())
     return dx, dw, db
 
@@ -516,10 +604,14 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
                      out=None):
     """Train-mode BatchNorm2d (+activation), in place on x, or from x into `out` when given; updates running
     stats like nn.BatchNorm2d."""
-    require_device(x, weight, bias, running_mean, running_var)
-    assert x.is_contiguous() and x.dtype == torch.float32
+    require_device(x, dtype=None)
+    require_device(weight, bias, running_mean, running_var)
+    assert x.is_contiguous() and (x.dtype == torch.float32 or x.dtype in T16)
     y = x if out is None else out
-    assert y.is_contiguous() and y.shape == x.shape and y.dtype == torch.float32
+    assert y.is_contiguous() and y.shape == x.shape and (y.dtype == torch.float32 or y.dtype in T16)
+    st = T16.get(x.dtype) or T16.get(y.dtype) or 0
+    assert x.dtype in (torch.float32, TORCH16.get(st)) and y.dtype in (torch.float32, TORCH16.get(st)), \
+        "batchnorm: one 16-bit storage type per call"
     B, C, H, W = x.shape
     sm = si = None
     if save:
@@ -529,7 +621,8 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
     # inside an autocast region the BN output is rounded like the 16-bit output of the reference's BatchNorm on
     # a 16-bit conv output (LDM_ACT_ROUND_*: the activation code's high bits)
     rdt = autocast_out(autocast_dt())
-    act_code = L.ACT[act] | (((rdt & 0xff) << 8) if rdt & L.DT_ROUND_OUT else 0)
+    act_code = L.ACT[act] | (((rdt & 0xff) << 8) if rdt & L.DT_ROUND_OUT else 0) | \
+        st_code(st, x16=x.dtype != torch.float32, y16=y.dtype != torch.float32)
     pg = _sync_group(sync)
     if pg is None:
         L.call("ldm_batchnorm_train_out", x.data_ptr(), y.data_ptr(), B, C, H * W, _p(weight), _p(bias),
@@ -543,7 +636,8 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
         stats = torch.empty(2 * C + 1, device=x.device, dtype=torch.float64)
         xp = x.data_ptr() if B else None
         yp = y.data_ptr() if B else None
-        L.call("ldm_batchnorm_stats", xp, B, C, H * W, stats.data_ptr(), ws.data_ptr(), stream_handle())
+        L.call("ldm_batchnorm_stats_code", xp, st_code(st, x16=x.dtype != torch.float32), B, C, H * W,
+               stats.data_ptr(), ws.data_ptr(), stream_handle())
         _allreduce_sum(stats, pg.pg)
         L.call("ldm_batchnorm_apply_out", xp, yp, B, C, H * W, stats.data_ptr(), -1.0, _p(weight), _p(bias),
                _p(running_mean), _p(running_var), float(momentum), float(eps), act_code, _p(sm), _p(si),

@@ -1,0 +1,164 @@
+"""16-bit storage of the train step's large maps (ldm_capi.h LDM_DT_X16 / _Y16 / _DY16, LDM_ST_*): every
+kernel that reads or writes a map in 16 bits gives the SAME result as its fp32-storage form on the same values.
+
+Inputs are bf16 / fp16-representable (a 16-bit map holds exactly those), so a 16-bit read is exact; the kernels
+then compute in fp32 as before, and a 16-bit write is the round-to-nearest-even of the fp32 result.  So, bit for
+bit: outputs stored in 16 bits == the fp32-storage outputs rounded to the type; fp32 outputs (weight / BN
+parameter gradients, statistics) == the fp32-storage outputs.  Covers the kind-3 convs (window and gather
+forms, forward and data gradient), the Cin = 1 / Cout = 1 VALU convs, the weight gradient's register-staged
+instances (double-rate and one-channel), BatchNorm forward / backward (rank-local and the SyncBatchNorm stages
+with a stub group) and the activation backward.  Reference semantics: torch.autocast keeps these maps as
+16-bit tensors (train.py:174; models/model.py:10-88 layers)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+T = {1: torch.float16, 2: torch.bfloat16}
+
+
+def _rand(shape, seed, lo=-1.0, hi=1.0):
+    g = np.random.Generator(np.random.PCG64(seed))
+    return torch.from_numpy(g.uniform(lo, hi, shape).astype(np.float32))
+
+
+def _q(t, dt):
+    """t rounded to the 16-bit type (as a 16-bit tensor) and its exact fp32 copy."""
+    t16 = t.to(T[dt])
+    return t16, t16.float()
+
+
+def _same(a16, b32, dt):
+    """a (16-bit) == b (fp32) rounded to the type, bitwise."""
+    assert a16.dtype == T[dt], a16.dtype
+    assert torch.equal(a16, b32.to(T[dt])), float((a16.float() - b32.to(T[dt]).float()).abs().max())
+
+
+CONV = {   # (B, Cin, H, W, Cout, k, stride, pad, out_pad, transposed)
+    "w_k3s2": (2, 64, 64, 256, 128, 3, 2, 1, 0, False),          # tconvw, stride 2
+    "w_k3s1": (4, 32, 16, 64, 256, 3, 1, 1, 0, False),           # tconvw, stride 1
+    "g_convT_k4": (2, 128, 32, 64, 64, 4, 2, 1, 0, True),        # tconv gather form (4 taps, one M tile)
+    "w_convT_k4_128": (2, 128, 32, 128, 64, 4, 2, 1, 0, True),
+    "k4s2_dgrad": (2, 128, 64, 128, 64, 4, 2, 1, 0, False),
+}
+
+
+@pytest.mark.parametrize("dt", [2, 1])
+@pytest.mark.parametrize("case", sorted(CONV))
+def test_kind3_conv_store16(cuda, case, dt):
+    from ldm_amd import ops
+    B, Cin, H, W, Cout, k, s, p, op, tr = CONV[case]
+    x16, x32 = _q(_rand((B, Cin, H, W), 11), dt)
+    w = _rand((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), 12, -0.1, 0.1).to(cuda)
+    b = _rand((Cout,), 13, -0.1, 0.1).to(cuda)
+    kw = dict(stride=s, padding=p, transposed=tr, output_padding=op, act="relu", dtype=dt)
+    y32 = ops.conv_forward(x32.to(cuda), w, b, **kw)
+    y16 = ops.conv_forward(x16.to(cuda), w, b, out_dtype=T[dt], **kw)
+    torch.cuda.synchronize()
+    _same(y16, y32, dt)
+    # the data gradient (forward kernel on the dual descriptor) and the weight gradient from 16-bit maps
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, s, p, op, tr)
+    g16, g32 = _q(_rand(tuple(y32.shape), 14), dt)
+    dx32 = ops.conv_backward_data(g32.to(cuda), w, desc, dtype=dt)
+    dx16 = ops.conv_backward_data(g16.to(cuda), w, desc, dtype=dt, out_dtype=T[dt])
+    dw32 = ops.conv_backward_weight(x32.to(cuda), g32.to(cuda), desc, dtype=dt)
+    dw16 = ops.conv_backward_weight(x16.to(cuda), g16.to(cuda), desc, dtype=dt)
+    torch.cuda.synchronize()
+    _same(dx16, dx32, dt)
+    assert ops.wgrad_storage16(desc, dt), "the double-rate weight gradient must take 16-bit maps here"
+    assert torch.equal(dw16, dw32)
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_cin1_and_cout1_store16(cuda, k):
+    """The Cin = 1 first layers (16-bit output), the 64 -> 1 output convT (16-bit input), the data gradient of
+    the latter (a Cin = 1 conv: 16-bit output) and the one-channel weight gradients (16-bit Dense)."""
+    from ldm_amd import ops
+    dt = 2
+    x = _rand((4, 1, 64, 256), 21)                      # fp32 mel
+    w1 = _rand((64, 1, k, k), 22, -0.3, 0.3).to(cuda)
+    b1 = _rand((64,), 23, -0.1, 0.1).to(cuda)
+    kw = dict(stride=2, padding=1, act="relu", dtype=dt)
+    y32 = ops.conv_forward(x.to(cuda), w1, b1, **kw)
+    y16 = ops.conv_forward(x.to(cuda), w1, b1, out_dtype=T[dt], **kw)
+    torch.cuda.synchronize()
+    _same(y16, y32, dt)
+    d1 = ops.make_desc(4, 1, 64, 256, 64, k, k, 2, 1)
+    g16, g32 = _q(_rand(tuple(y32.shape), 24), dt)
+    assert ops.wgrad_storage16(d1, dt) & 0x800
+    assert torch.equal(ops.conv_backward_weight(x.to(cuda), g16.to(cuda), d1, dtype=dt),
+                       ops.conv_backward_weight(x.to(cuda), g32.to(cuda), d1, dtype=dt))
+    # decoder output layer: convT 64 -> 1, k4 s2 p1, tanh
+    h16, h32 = _q(_rand((4, 64, 32, 128), 25, 0.0, 1.0), dt)
+    w2 = _rand((64, 1, 4, 4), 26, -0.2, 0.2).to(cuda)
+    b2 = _rand((1,), 27, -0.1, 0.1).to(cuda)
+    kt = dict(stride=2, padding=1, transposed=True, act="tanh", dtype=dt)
+    o32 = ops.conv_forward(h32.to(cuda), w2, b2, **kt)
+    o16 = ops.conv_forward(h16.to(cuda), w2, b2, **kt)
+    torch.cuda.synchronize()
+    assert o16.dtype == torch.float32 and torch.equal(o16, o32)
+    d2 = ops.make_desc(4, 64, 32, 128, 1, 4, 4, 2, 1, 0, True)
+    r = _rand(tuple(o32.shape), 28).to(cuda)
+    _same(ops.conv_backward_data(r, w2, d2, dtype=dt, out_dtype=T[dt]), ops.conv_backward_data(r, w2, d2, dtype=dt), dt)
+    assert torch.equal(ops.conv_backward_weight(h16.to(cuda), r, d2, dtype=dt),
+                       ops.conv_backward_weight(h32.to(cuda), r, d2, dtype=dt))
+
+
+class _StubGroup:
+    """A world-1 stand-in for a SyncBatchNorm group: the two-stage kernels with an identity all-reduce."""
+
+    def ldm_allreduce_sum(self, t):
+        pass
+
+
+@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_batchnorm_store16(cuda, act, sync):
+    from ldm_amd import ops
+    dt = 2
+    B, C, H, W = 4, 64, 32, 64
+    x16, x32 = _q(_rand((B, C, H, W), 31, -2.0, 3.0), dt)
+    w = _rand((C,), 32, 0.5, 1.5).to(cuda)
+    b = _rand((C,), 33, -0.2, 0.2).to(cuda)
+    grp = _StubGroup() if sync else False
+    outs = {}
+    for name, xin in (("32", x32), ("16", x16)):
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        xd = xin.to(cuda)
+        y = torch.empty_like(xd)
+        sm, si = ops.batchnorm_train_(xd, w, b, rm, rv, 0.1, 1e-5, act, save=True, sync=grp, out=y)
+        outs[name] = (xd, y, sm, si, rm, rv)
+    torch.cuda.synchronize()
+    _same(outs["16"][1], outs["32"][1], dt)
+    for i in (2, 3, 4, 5):
+        assert torch.equal(outs["16"][i], outs["32"][i]), i
+    g16, g32 = _q(_rand((B, C, H, W), 34), dt)
+    r32 = ops.batchnorm_backward(g32.to(cuda), None, outs["32"][0], outs["32"][2], outs["32"][3], w, act, sync=grp, bias=b)
+    r16 = ops.batchnorm_backward(g16.to(cuda), None, outs["16"][0], outs["16"][2], outs["16"][3], w, act, sync=grp, bias=b)
+    torch.cuda.synchronize()
+    _same(r16[0], r32[0], dt)
+    assert torch.equal(r16[1], r32[1]) and torch.equal(r16[2], r32[2])
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 32, 64), (8, 32, 16, 16), (32, 64, 3, 3)])
+def test_act_backward_store16(cuda, shape):
+    """The sliced, per-plane and small-plane activation-backward kernels with 16-bit dy / act_out / dv."""
+    from ldm_amd import ops
+    dt = 2
+    a16, a32 = _q(torch.relu(_rand(shape, 41)), dt)
+    g16, g32 = _q(_rand(shape, 42), dt)
+    dv32, db32, dc32 = ops.act_backward(g32.to(cuda), "relu", act_out=a32.to(cuda), need_bias=True, need_bcast=True)
+    dv16, db16, dc16 = ops.act_backward(g16.to(cuda), "relu", act_out=a16.to(cuda), need_bias=True, need_bcast=True)
+    torch.cuda.synchronize()
+    _same(dv16, dv32, dt)
+    assert torch.equal(db16, db32) and torch.equal(dc16, dc32)
+
+
+def test_store16_policy():
+    """Which maps are stored in 16 bits: >= LDM_AMD_STORE16_MIN elements at a 16-bit operand precision."""
+    from ldm_amd import ops
+    assert ops.store16_dtype(1 << 22, 2) == torch.bfloat16
+    assert ops.store16_dtype(1 << 22, 1) == torch.float16
+    assert ops.store16_dtype((1 << 22) - 1, 2) == torch.float32
+    assert ops.store16_dtype(1 << 24, 0) == torch.float32

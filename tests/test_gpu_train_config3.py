@@ -176,9 +176,9 @@ class _Recorder:
                 add("fwd", d, dt, (kw.get("bcast") is not None, kw.get("skip") is not None))
             return y
 
-        def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False):
+        def conv_backward_data(dy, weight, desc, wkey=None, dtype=0, round_out=False, **kw):
             add("dgrad", desc, dtype)
-            return dgrad(dy, weight, desc, wkey, dtype, round_out)
+            return dgrad(dy, weight, desc, wkey, dtype, round_out, **kw)
 
         def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
             add("wgrad", desc, dtype)

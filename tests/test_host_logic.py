@@ -169,3 +169,39 @@ def test_lpips_alex_state_dict_forms():
     assert _torch.equal(m3.net.conv(1).weight, sd["net.slice2.3.weight"])
     with _pytest.raises(KeyError):
         LPIPSAlex.from_state_dict({k: v for k, v in tv.items() if not k.startswith("lin4")})
+
+
+def test_store16_policy_and_codes(monkeypatch):
+    """16-bit storage of large maps (ops.store16_dtype, in16, st_code; ldm_capi.h LDM_ST_* / LDM_DT_*16) and
+    which conv forms take it (host-side plan queries, no GPU): every large-map layer of the B = 32 train step."""
+    from ldm_amd import _lib as L
+    from ldm_amd import ops
+    assert ops.store16_dtype(1 << 22, 2) == torch.bfloat16 and ops.store16_dtype(1 << 22, 1) == torch.float16
+    assert ops.store16_dtype((1 << 22) - 1, 2) == torch.float32 and ops.store16_dtype(1 << 24, 0) == torch.float32
+    monkeypatch.setenv("LDM_AMD_STORE16", "0")
+    assert ops.store16_dtype(1 << 24, 2) == torch.float32
+    monkeypatch.delenv("LDM_AMD_STORE16")
+    t, h = ops.in16(torch.zeros(4, dtype=torch.bfloat16), 2)
+    assert h and t.dtype == torch.bfloat16
+    t, h = ops.in16(torch.zeros(4, dtype=torch.bfloat16), 1)          # another 16-bit type: read as fp32
+    assert not h and t.dtype == torch.float32
+    t, h = ops.in16(torch.zeros(4, dtype=torch.bfloat16), 2, ok=False)
+    assert not h and t.dtype == torch.float32
+    assert ops.st_code(2, x16=True, dx16=True) == (2 << L.ST_SHIFT) | L.ST_X16 | L.ST_DX16
+    assert ops.st_code(2) == 0
+    layers = [(1, 128, 512, 64, 3, 2, 0, False), (64, 64, 256, 128, 3, 2, 0, False), (128, 32, 128, 32, 3, 2, 0, False),
+              (32, 16, 64, 128, 4, 2, 0, True), (128, 32, 128, 64, 4, 2, 0, True), (64, 64, 256, 1, 4, 2, 0, True),
+              (128, 32, 128, 256, 3, 2, 0, False), (256, 16, 64, 256, 3, 2, 0, False)]
+    for Cin, H, W, Cout, k, s, op, tr in layers:
+        d = ops.make_desc(32, Cin, H, W, Cout, k, k, s, 1, op, tr)
+        dd = ops.dual_desc(d)
+        pf = ops.tiled_plan(d, 2) or ops.get_plan(d)
+        pd = ops.tiled_plan(dd, 2) or ops.get_plan(dd)
+        big_in, big_out = 32 * Cin * H * W >= 1 << 22, 32 * Cout * d.Hout * d.Wout >= 1 << 22
+        f, b, w = ops.conv_storage16(d, pf, 2), ops.conv_storage16(dd, pd, 2), ops.wgrad_storage16(d, 2)
+        if big_out:   # (a Cin = 1 first layer has no data gradient: its input is the mel)
+            assert f & L.DT_Y16 and (Cin == 1 or b & L.DT_X16) and w & L.DT_DY16, \
+                (Cin, Cout, f, b, w)
+        if big_in and Cin > 1:
+            assert f & L.DT_X16 and b & L.DT_Y16 and w & L.DT_X16, (Cin, Cout, f, b, w)
+        assert ops.conv_storage16(d, pf, 0) == 0 and ops.wgrad_storage16(d, 0) == 0
