@@ -518,8 +518,8 @@ _CNT = {}
 
 def reduce_counters(C, device):
     """Per-(device, stream) zeroed int32 arrival counters for the finalize-in-launch reductions (the kernels
-    return them to zero; LDM_AMD_FUSED_FINALIZE=0: None, the two-launch form)."""
-    if os.environ.get("LDM_AMD_FUSED_FINALIZE", "1") == "0":
+    return them to zero; LDM_AMD_FUSED_FINALIZE=1 turns them on, else None: the two-launch form)."""
+    if os.environ.get("LDM_AMD_FUSED_FINALIZE", "0") == "0":
         return None
     key = (str(device), _stream_key(device))
     buf = _CNT.get(key)
