@@ -407,11 +407,6 @@ int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float
  * dv may alias dy.  workspace: ldm_reduce_workspace_floats(B,C,HW) floats (NULL when no sums). */
 int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B, int32_t C,
                      int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace, void* stream);
-/* ldm_act_backward with the bias / broadcast sums finalized inside the same launch: counters = C int32 zeros
- * (returned to zero by the launch; one set per stream), NULL = the two-launch form. */
-int ldm_act_backward_ex(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B,
-                        int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
-                        int32_t* counters, void* stream);
 /* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
  * y = its output, x = its input, weight / bias its affine parameters (NULL = 1 / 0); dx / dweight / dbias
  * may be NULL.  y may be NULL when act is NONE or RELU: the ReLU mask is then re-evaluated from x with the

@@ -304,70 +304,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
     });
 }
 
-// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy for one channel c, by one 256-thread block.  A
-// plane's Q slice partials go to QP lanes (QP = Q rounded up to a power of two, at most 64; lane stride past
-// 64), so a wave takes 64 / QP planes per step (wave w the planes from w * 64 / QP on, stepping by 256 / QP) and
-// sums each plane by a segmented shuffle tree; the plane sums meet in a full-wave tree, the four wave sums in
-// wave order.  A fixed partition and order, so bitwise reproducible (a single thread walking B*Q partials
-// serially took 150 us for the decoder's one-channel output layer at B = 32; one plane per wave step left the
-// Q = 1 finalize of the plane kernels at 8 serial load round trips per wave).  ld(i) reads part[i].
-template <class LD>
-__device__ __forceinline__ void finalize_channel(LD&& ld, int B, int C, int Q, int QP, int c, float* __restrict__ dbias,
-                                                 float* __restrict__ dbcast, float* wsum) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int ppw = 64 / QP, sub = lane / QP, k0 = lane % QP;
-    float sb = 0.f;
-    for (int b0 = wave * ppw; b0 < B; b0 += (kThreads / 64) * ppw) {
-        const int b = b0 + sub;
-        const size_t pl = (size_t)b * C + c;
-        float sd = 0.f, sg = 0.f;
-        if (b < B)
-            for (int k = k0; k < Q; k += QP) {
-                sd += ld((pl * Q + k) * 2 + 0);
-                sg += ld((pl * Q + k) * 2 + 1);
-            }
-        for (int o = QP / 2; o > 0; o >>= 1) {
-            sd += __shfl_xor(sd, o);
-            sg += __shfl_xor(sg, o);
-        }
-        if (k0 == 0 && b < B) {
-            sb += sd;
-            if (dbcast) dbcast[pl] = sg;
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) sb += __shfl_xor(sb, o);
-    if (lane == 0) wsum[wave] = sb;
-    __syncthreads();
-    if (threadIdx.x == 0 && dbias) {
-        float s = 0.f;
-        for (int w = 0; w < kThreads / 64; ++w) s += wsum[w];
-        dbias[c] = s;
-    }
-}
-
-// The finalize in the launch that wrote the partials (no second launch): partials are stored and read as
-// agent-scope relaxed atomics (write-through / cache-bypassing on gfx950), each store drained (vmcnt(0)) before
-// the block's barrier, and a per-channel arrival counter (zero between launches; the last arriver resets it)
-// names the block that finalizes the channel — the hand-off of the K-split step kernels (uconv.hip).
-__device__ __forceinline__ void part_store(float* part, size_t i, float v) {
-    __hip_atomic_store(part + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float part_load(const float* part, size_t i) {
-    return __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // ---- fused-epilogue activation backward: dv = dy*act'(v); partial sums of dv and dy per (b,c,slice)
 template <int W, int ST>
 __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const void* dy,
                                                            const void* __restrict__ aval,
                                                            const float* __restrict__ pre, int act, int sf, int C,
                                                            int HW, int64_t S, void* dv,
-                                                           float* __restrict__ part, int* __restrict__ cnt, int B,
-                                                           int QP, float* __restrict__ dbias,
-                                                           float* __restrict__ dbcast) {
+                                                           float* __restrict__ part) {
     const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
     __shared__ float red[kThreads / 64];
-    __shared__ int flag;
     const int k = blockIdx.x, plane = blockIdx.y, Q = gridDim.x;
     const int b = plane / C, c = plane - b * C;
     const int64_t e0 = (int64_t)b * HW + (int64_t)k * S;
@@ -405,27 +350,10 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const void* dy,
     if (part) {
         sd = block_sum(sd, red);
         sg = block_sum(sg, red);
-        if (!cnt) {
-            if (threadIdx.x == 0) {
-                part[((size_t)plane * Q + k) * 2 + 0] = sd;
-                part[((size_t)plane * Q + k) * 2 + 1] = sg;
-            }
-            return;
-        }
         if (threadIdx.x == 0) {
-            part_store(part, ((size_t)plane * Q + k) * 2 + 0, sd);
-            part_store(part, ((size_t)plane * Q + k) * 2 + 1, sg);
+            part[((size_t)plane * Q + k) * 2 + 0] = sd;
+            part[((size_t)plane * Q + k) * 2 + 1] = sg;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int old = __hip_atomic_fetch_add(cnt + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old == B * Q - 1;
-            if (last) __hip_atomic_store(cnt + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag = last;
-        }
-        __syncthreads();
-        if (flag) finalize_channel([&](size_t i) { return part_load(part, i); }, B, C, Q, QP, c, dbias, dbcast, red);
     }
 }
 
@@ -437,9 +365,7 @@ __global__ __launch_bounds__(kThreads) void act_bwd_kernel(const void* dy,
 template <int TP, int ST>
 __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const void* __restrict__ dy,
                                                                   const void* __restrict__ aval, int act, int sf,
-                                                                  int nplanes, void* dv, float* __restrict__ part,
-                                                                  int* __restrict__ cnt, int B, int C,
-                                                                  float* __restrict__ dbias, float* __restrict__ dbcast) {
+                                                                  int nplanes, void* dv, float* __restrict__ part) {
     const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
     constexpr int PPB = kThreads / TP;
     __shared__ float red[2][kThreads / 64];
@@ -487,50 +413,53 @@ __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const void* __
             }
         }
     }
-    if (!cnt) {
-        if (part && t == 0 && pl < nplanes) {
-            part[(size_t)pl * 2 + 0] = sd;
-            part[(size_t)pl * 2 + 1] = sg;
-        }
-        return;
-    }
-    // fused finalize (part != NULL here): a plane's partial, then its channel's arrival (B planes per channel);
-    // the block finalizes every channel whose last plane it held, in plane order
-    __shared__ int won[PPB];
-    if (t == 0 && pl < nplanes) {
-        part_store(part, (size_t)pl * 2 + 0, sd);
-        part_store(part, (size_t)pl * 2 + 1, sg);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-        int w = -1;
-        if (pl < nplanes) {
-            const int c = pl % C;
-            const int old = __hip_atomic_fetch_add(cnt + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old == B - 1) {
-                __hip_atomic_store(cnt + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                w = c;
-            }
-        }
-        won[(int)threadIdx.x / TP] = w;
-    }
-    __syncthreads();
-    for (int i = 0; i < PPB; ++i) {
-        const int c = won[i];
-        if (c >= 0) {
-            finalize_channel([&](size_t j) { return part_load(part, j); }, B, C, 1, 1, c, dbias, dbcast, red[0]);
-            __syncthreads();   // (wsum reused by the next channel)
-        }
+    if (part && t == 0 && pl < nplanes) {
+        part[(size_t)pl * 2 + 0] = sd;
+        part[(size_t)pl * 2 + 1] = sg;
     }
 }
 
-// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy (finalize_channel, above)
+// dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy.  One block per channel: a plane's Q slice
+// partials go to QP lanes (QP = Q rounded up to a power of two, at most 64; lane stride past 64), so a wave
+// takes 64 / QP planes per step (wave w the planes from w * 64 / QP on, stepping by 256 / QP) and sums each
+// plane by a segmented shuffle tree; the plane sums meet in a full-wave tree, the four wave sums in wave
+// order.  A fixed partition and order, so bitwise reproducible (a single thread walking B*Q partials
+// serially took 150 us for the decoder's one-channel output layer at B = 32; one plane per wave step left
+// the Q = 1 finalize of the plane kernels at 8 serial load round trips per wave).
 __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float* __restrict__ part, int B, int C,
                                                                     int Q, int QP, float* __restrict__ dbias,
                                                                     float* __restrict__ dbcast) {
     __shared__ float wsum[kThreads / 64];
-    finalize_channel([&](size_t i) { return part[i]; }, B, C, Q, QP, blockIdx.x, dbias, dbcast, wsum);
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ppw = 64 / QP, sub = lane / QP, k0 = lane % QP;
+    float sb = 0.f;
+    for (int b0 = wave * ppw; b0 < B; b0 += (kThreads / 64) * ppw) {
+        const int b = b0 + sub;
+        const size_t pl = (size_t)b * C + c;
+        float sd = 0.f, sg = 0.f;
+        if (b < B)
+            for (int k = k0; k < Q; k += QP) {
+                sd += part[(pl * Q + k) * 2 + 0];
+                sg += part[(pl * Q + k) * 2 + 1];
+            }
+        for (int o = QP / 2; o > 0; o >>= 1) {
+            sd += __shfl_xor(sd, o);
+            sg += __shfl_xor(sg, o);
+        }
+        if (k0 == 0 && b < B) {
+            sb += sd;
+            if (dbcast) dbcast[pl] = sg;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) sb += __shfl_xor(sb, o);
+    if (lane == 0) wsum[wave] = sb;
+    __syncthreads();
+    if (threadIdx.x == 0 && dbias) {
+        float s = 0.f;
+        for (int w = 0; w < kThreads / 64; ++w) s += wsum[w];
+        dbias[c] = s;
+    }
 }
 static int finalize_lanes(int Q) {
     int qp = 1;
@@ -840,12 +769,6 @@ extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const flo
 extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
                                 int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
                                 void* stream) {
-    return ldm_act_backward_ex(dy, act_out, pre_act, act_code, B, C, HW, dv, dbias, dbcast, workspace, nullptr, stream);
-}
-
-extern "C" int ldm_act_backward_ex(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
-                                   int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast,
-                                   float* workspace, int32_t* counters, void* stream) {
     const StCode sc = st_code(act_code);
     const int act = sc.act & 0xff;
     LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
@@ -870,23 +793,18 @@ extern "C" int ldm_act_backward_ex(const float* dy, const float* act_out, const 
         float* part = sums ? workspace : nullptr;
         const int tp = HW / 4;
         const unsigned blocks = (unsigned)((nplanes + kThreads / tp - 1) / (kThreads / tp));
-        int* cnt = sums ? counters : nullptr;   // counters: the finalize in the same launch
         st_dispatch(sc, [&](auto stc) {
             constexpr int ST = decltype(stc)::value;
-#define ABP(TP_)                                                                                               \
-    hipLaunchKernelGGL((act_bwd_planes_kernel<TP_, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, \
-                       nplanes, dvp, part, cnt, B, C, dbias, dbcast)
             switch (tp) {
-                case 16: ABP(16); break;
-                case 32: ABP(32); break;
-                case 64: ABP(64); break;
-                case 128: ABP(128); break;
-                default: ABP(256); break;
+                case 16: hipLaunchKernelGGL((act_bwd_planes_kernel<16, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 32: hipLaunchKernelGGL((act_bwd_planes_kernel<32, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 64: hipLaunchKernelGGL((act_bwd_planes_kernel<64, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                case 128: hipLaunchKernelGGL((act_bwd_planes_kernel<128, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
+                default: hipLaunchKernelGGL((act_bwd_planes_kernel<256, ST>), dim3(blocks), dim3(kThreads), 0, st, dy, aval0, act, sc.sf, nplanes, dvp, part); break;
             }
-#undef ABP
         });
         LDM_CHECK_LAUNCH("act_bwd_planes_kernel");
-        if (sums && !cnt) {
+        if (sums) {
             hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, 1, dbias, dbcast);
             LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
         }
@@ -898,19 +816,17 @@ extern "C" int ldm_act_backward_ex(const float* dy, const float* act_out, const 
     const float* aval = aval0;
     float* part = sums ? workspace : nullptr;
     const bool v4 = vec_ok(HW, dy, aval, pre_act, dv);
-    int* cnt = sums ? counters : nullptr;   // counters: the finalize in the same launch
-    const int QP = finalize_lanes(Q);
     st_dispatch(sc, [&](auto stc) {
         constexpr int ST = decltype(stc)::value;
         if (v4)
             hipLaunchKernelGGL((act_bwd_kernel<4, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
-                               HW, S, dv, part, cnt, B, QP, dbias, dbcast);
+                               HW, S, dv, part);
         else
             hipLaunchKernelGGL((act_bwd_kernel<1, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
-                               HW, S, dv, part, cnt, B, QP, dbias, dbcast);
+                               HW, S, dv, part);
     });
     LDM_CHECK_LAUNCH("act_bwd_kernel");
-    if (sums && !cnt) {
+    if (sums) {
         hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, Q,
                            finalize_lanes(Q), dbias, dbcast);
         LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");

@@ -417,8 +417,21 @@ struct LpArgs {
     int32_t wr, wca, pitch_c;   // window rows, row pitch, channel pitch (floats)
     int32_t dense16, gath16;    // 16-bit storage of dense / gath (the register-staged instances, XS != 0)
 };
-// window pieces per lane of the register-staged instances (checked by lp_plan)
-constexpr int kLpStagedPieces = 12;
+// window pieces per lane of a register-staged instance: the largest window lp_plan makes for (S, KK, QC) over
+// the instance's NW waves (the window of one chunk: 32 channels x the padded channel pitch, in 4-float pieces)
+__host__ __device__ constexpr int lp_pitch(int S, int KK, int rows, int cols) {
+    const int wr = (rows - 1) * S + KK, wca = (3 + (cols - 1) * S + KK + 3) / 4 * 4;
+    int pc = wr * wca;
+    while (pc % 64 != 4) pc += 4;
+    return pc;
+}
+__host__ __device__ constexpr int lp_staged_pieces(int S, int KK, int QC, int NW) {
+    const int p1 = QC == 32 ? lp_pitch(S, KK, 1, 32) : lp_pitch(S, KK, 1, 16);
+    const int p2 = QC == 32 ? lp_pitch(S, KK, 2, 16) : lp_pitch(S, KK, 2, 8);
+    const int pc = p1 > p2 ? p1 : p2;
+    return (32 * (pc / 4) + 64 * NW - 1) / (64 * NW);
+}
+constexpr int kLpStagedPieces = 12;   // (upper bound over the instances)
 
 __host__ __device__ constexpr int lp_nb(int S, int KK) { return (3 + 7 * S + KK + 3) / 4; }   // b128 reads per k-step
 __host__ __device__ inline int lp_buf_floats(int bm, int qc, int pitch_c) {
@@ -496,7 +509,8 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
 
     // ---- register-staged form (XS != 0): the same pieces as issue(), loaded as 16-byte fp32 quads or 8-byte
     //      16-bit quads (element offsets as issue()'s), widened to floats when parked
-    constexpr int ND = (BM / RPI + NW - 1) / NW, NWPC = kLpStagedPieces;
+    constexpr int ND = (BM / RPI + NW - 1) / NW, NWPC = lp_staged_pieces(S, KK, QC, NW);
+    static_assert(NWPC <= kLpStagedPieces, "staged window pieces");
     uint4 rd[XS ? ND : 1], rw[XS ? NWPC : 1];
     auto fetch = [&](int ch) {
         const int b = ch / a.cps;
@@ -868,7 +882,7 @@ bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats) {
 static bool lp_staged_fits(const wg::LpPlan& lp) {
     const int nw = lp.WM * lp.KK;
     const int npiece = wg::kLC * (lp.a.pitch_c >> 2);
-    return (npiece + 64 * nw - 1) / (64 * nw) <= wg::kLpStagedPieces;
+    return (npiece + 64 * nw - 1) / (64 * nw) <= wg::lp_staged_pieces(lp.S, lp.KK, lp.QC, nw);
 }
 
 // Which tensors of the weight gradient of d may be stored in 16 bits (LDM_DT_X16 | LDM_DT_DY16) at a 16-bit

@@ -166,8 +166,6 @@ SIGNATURES = {
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),
-    "ldm_act_backward_ex": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
-                                      c_vp, c_vp]),
     "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
                                          c_int32, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_backward_reduce": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,

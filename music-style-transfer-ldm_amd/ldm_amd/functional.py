@@ -7,7 +7,6 @@ backward kernels (ldm_amd.backward); a missing backward raises instead of silent
 import torch
 
 from . import _lib as L
-from . import graphs as hgraphs
 from . import ops
 
 _BACKWARD = {}   # name -> callable(ctx, *grad_outputs) registered by ldm_amd.backward
@@ -119,19 +118,9 @@ def _conv_backward(ctx, gy):
             _, gb, _ = ops.act_backward(gv, "none", need_dv=False, need_bias=True)
     desc = _conv_desc(x, w, cfg)
     dt = ctx.store.get("dtype", 0)
-    side, gw = None, None
-    if nx and nw and hgraphs.wgrad_stream_enabled(x.device):
-        # the weight gradient on a side stream next to the data gradient (both only read gv and the saved
-        # tensors), joined before the node returns
-        with hgraphs.branch(x.device, "wgrad") as side:
-            if side is not None:
-                gw = ops.conv_backward_weight(x, gv, desc, dtype=dt)
     gx = ops.conv_backward_data(gv, w, desc, ctx.store["wkey"], dtype=dt, round_out=ctx.store.get("round", False),
                                 out_dtype=x.dtype) if nx else None
-    if side is not None:
-        hgraphs.join(side, x.device)
-    elif nw:
-        gw = ops.conv_backward_weight(x, gv, desc, dtype=dt)
+    gw = ops.conv_backward_weight(x, gv, desc, dtype=dt) if nw else None
     if gbc is not None:
         gbc = gbc.reshape(ctx.store["bc_shape"])
     return gx, gw, gb, gbc, (gy if nsk else None)

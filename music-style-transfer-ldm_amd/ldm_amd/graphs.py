@@ -20,29 +20,9 @@ import torch
 CAPTURE_MODE = "thread_local"
 
 
-_CAPTURE_STREAM = []   # the origin stream of the capture in progress (capture())
-
-
-@contextlib.contextmanager
 def capture(graph, stream=None, pool=None):
     """Context manager: capture into `graph` (torch.cuda.CUDAGraph) on `stream`, thread-local mode."""
-    with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=CAPTURE_MODE):
-        _CAPTURE_STREAM.append(torch.cuda.current_stream().cuda_stream)
-        try:
-            yield
-        finally:
-            _CAPTURE_STREAM.pop()
-
-
-def wgrad_stream_enabled(device):
-    """Conv backward: the weight gradient on a side stream next to the data gradient, for nodes on the capture's
-    origin stream only (no fork from a branch stream).  LDM_AMD_WGRAD_STREAM=1 (default off: a form with forks
-    from every stream crashed in capture_end)."""
-    if os.environ.get("LDM_AMD_WGRAD_STREAM", "0") == "0" or torch.device(device).type != "cuda":
-        return False
-    if not _CAPTURE_STREAM or not torch.cuda.is_current_stream_capturing():
-        return False
-    return torch.cuda.current_stream(torch.device(device)).cuda_stream == _CAPTURE_STREAM[-1]
+    return torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=CAPTURE_MODE)
 
 
 _BRANCH_STREAMS = {}

@@ -507,31 +507,9 @@ def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=Fa
         return dv, None, None
     ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
     code = L.ACT[act] | st_code(st, x16=ah, dy16=dyh, dx16=dyh and dv is not None)
-    cnt = reduce_counters(C, dy.device) if (need_bias or need_bcast) and dy.is_cuda else None
-    L.call("ldm_act_backward_ex", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)), code, B,
-           C, HW, _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), _p(cnt), stream_handle())
+    L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)), code, B,
+           C, HW, _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), stream_handle())
     return dv, db, dbc
-
-
-_CNT = {}
-
-
-def reduce_counters(C, device):
-    """Per-(device, stream) zeroed int32 arrival counters for the finalize-in-launch reductions (the kernels
-    return them to zero; LDM_AMD_FUSED_FINALIZE=1 turns them on, else None: the two-launch form)."""
-    if os.environ.get("LDM_AMD_FUSED_FINALIZE", "0") == "0":
-        return None
-    key = (str(device), _stream_key(device))
-    buf = _CNT.get(key)
-    if buf is None or buf.numel() < C:
-        if buf is not None:
-            _CNT_OLD.append(buf)   # a captured graph may still hold the old one
-        buf = torch.zeros(max(int(C), 1024), device=device, dtype=torch.int32)
-        _CNT[key] = buf
-    return buf
-
-
-_CNT_OLD = []
 
 
 def reduce_workspace(B, C, HW, device):

@@ -162,25 +162,3 @@ def test_store16_policy():
     assert ops.store16_dtype(1 << 22, 1) == torch.float16
     assert ops.store16_dtype((1 << 22) - 1, 2) == torch.float32
     assert ops.store16_dtype(1 << 24, 0) == torch.float32
-
-
-@pytest.mark.parametrize("shape", [(4, 64, 32, 64), (32, 64, 16, 64), (8, 128, 8, 32), (4, 32, 17, 33)])
-@pytest.mark.parametrize("st", [0, 2])
-def test_act_backward_fused_finalize(cuda, monkeypatch, shape, st):
-    """The bias / broadcast sums finalized inside the activation-backward launch (per-channel arrival
-    counters, ldm_act_backward_ex) == the two-launch form, bitwise; twice in a row (the counters reset)."""
-    from ldm_amd import ops
-    a = torch.relu(_rand(shape, 51))
-    g = _rand(shape, 52)
-    if st:
-        a, g = a.to(T[st]), g.to(T[st])
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("LDM_AMD_FUSED_FINALIZE", mode)
-        outs = [ops.act_backward(g.to(cuda), "relu", act_out=a.to(cuda), need_bias=True, need_bcast=True)
-                for _ in range(2)]
-        torch.cuda.synchronize()
-        res[mode] = outs
-    for i in range(2):
-        for j in range(3):
-            assert torch.equal(res["0"][i][j], res["1"][i][j]), (i, j)
