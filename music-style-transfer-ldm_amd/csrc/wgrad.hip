@@ -676,8 +676,188 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp_kernel(LpArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// The double-rate weight gradient on 16-bit maps (both Dense and Gath stored in the operand type, LDM_DT_X16 +
+// LDM_DT_DY16): the tiles arrive by LDS DMA as they are stored, 16 bits, and the MFMA operands are read from
+// LDS without any conversion.  Same blocks, waves, chunks and k-steps as wgrad_lp_kernel, so the same sums in
+// the same order (bitwise equal to the fp32-storage form on the same values).  Layout in 16-bit elements:
+//   Dense [BM][QC], 16-B pieces of 8 positions, XOR-swizzled per row pair (a fragment is one ds_read_b128);
+//   window [32][pitch16] of rows of wca16 elements from the 8-aligned origin qx0*S - 8 (so e = 7; Wg % 8 == 0:
+//   a piece is wholly inside or outside the image row), channel pitch = 8 mod 128 elements.
+// B fragment of tap (ky, kx) for positions q0 + j: window elements 7 + kx + S j of the lane's channel row run
+// (read as NB16 16-byte loads); stride 2 takes every other 16-bit element (one v_perm per dword), stride 1
+// eight consecutive ones (aligned, or a funnel shift).
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+__host__ __device__ constexpr int lp16_nb(int S, int KK) { return (7 + KK + 7 * S + 7) / 8; }   // b128 per k-step
+__host__ __device__ inline int lp16_buf_bytes(int bm, int qc, int pitch16) {
+    return bm * qc * 2 + (kLC * pitch16 * 2 + 1023) / 1024 * 1024;
+}
+template <int PPR>
+__host__ __device__ constexpr int lp16_swz(int row) { return (row >> 1) & (PPR - 1); }
+
+// 8 consecutive 16-bit elements starting at element `e` (compile-time) of the dword array w, stride S
+template <int S, int E, int N>
+__device__ __forceinline__ u16x8 lp16_frag(const unsigned (&w)[N]) {
+    static_assert((E >> 1) + (S == 2 ? 8 : 5) <= N, "fragment past the loaded run");
+    unsigned d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (S == 2) {
+            // elements E + 4i and E + 4i + 2: the same half of dwords (E + 4i) / 2 and (E + 4i) / 2 + 1
+            constexpr int h = E & 1;
+            const unsigned lo = w[(E >> 1) + 2 * i], hi = w[(E >> 1) + 2 * i + 1];
+            d[i] = h ? ((lo >> 16) | (hi & 0xffff0000u)) : ((lo & 0xffffu) | (hi << 16));
+        } else {
+            if constexpr ((E & 1) == 0) {
+                d[i] = w[(E >> 1) + i];
+            } else {
+                const unsigned lo = w[(E >> 1) + i], hi = w[(E >> 1) + i + 1];
+                d[i] = (lo >> 16) | (hi << 16);
+            }
+        }
+    }
+    return __builtin_bit_cast(u16x8, (uint4){d[0], d[1], d[2], d[3]});
+}
+
+template <int DT>
+__device__ __forceinline__ floatx16 mma16x(const u16x8& a, const u16x8& b, const floatx16& c) {
+    if constexpr (DT == 1)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c, 0,
+                                                      0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                       0, 0, 0);
+}
+
+template <int S, int KK, int BM, int WM, int QC, int DT>
+__global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16_kernel(LpArgs a) {
+    constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp16_nb(S, KK);
+    constexpr int PPR = QC / 8, RPI = 64 / PPR, NKS = QC / 16;
+    static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
+    extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ky = wave % KK, wm = wave / KK;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * BM, c0 = blockIdx.x * kLC;
+    const int HQ = a.Hq * a.Wq;
+    const int bufB = lp16_buf_bytes(BM, QC, a.pitch_c);   // (LpArgs.wca / pitch_c hold the 16-bit geometry here)
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 2), 0x00020000);
+
+    auto issue = [&](int ch, int buf) {
+        const int b = ch / a.cps;
+        const int rr = ch - b * a.cps;
+        int qy0, qx0;
+        if (a.cols == a.Wq) {
+            qy0 = rr * a.rows, qx0 = 0;
+        } else {
+            const int segs = a.Wq / QC;
+            qy0 = rr / segs, qx0 = (rr - qy0 * segs) * QC;
+        }
+        char* base = reinterpret_cast<char*>(smem16) + buf * bufB;
+        for (int gi = wave; gi < BM / RPI; gi += NW) {
+            const int row = gi * RPI + lane / PPR;
+            const int sp = (lane % PPR) ^ lp16_swz<PPR>(row);
+            const int ql = sp * 8;
+            const int qy = qy0 + ql / a.cols, qx = qx0 + ql % a.cols;
+            const int m = m0 + row;
+            const int voff = m < a.M ? (((b * a.M + m) * HQ + qy * a.Wq + qx) * 2) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(base + gi * 1024), 16, voff, 0, 0, 0);
+        }
+        const int wq8 = a.wca >> 3, pq = a.pitch_c >> 3;
+        const int npiece = kLC * pq;
+        const int row0 = qy0 * S - 1, colA = qx0 * S - 8;   // pad 1, e = 7
+        for (int gi = wave; gi * 64 < npiece; gi += NW) {
+            const int pc = gi * 64 + lane;
+            const int cl = pc / pq;
+            const int rem = pc - cl * pq;
+            const int wrow = rem / wq8, wp = rem - wrow * wq8;
+            const int c = c0 + cl, iy = row0 + wrow, ix = colA + wp * 8;
+            const bool ok = pc < npiece && c < a.C && wrow < a.wr && (unsigned)iy < (unsigned)a.Hg &&
+                            (unsigned)ix < (unsigned)a.Wg;
+            const int voff = ok ? ((((b * a.C + c) * a.Hg + iy) * a.Wg + ix) * 2) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(base + BM * QC * 2 + gi * 1024), 16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx16 acc[MF][KK];
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int t = 0; t < KK; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
+
+    // per-lane byte offsets inside a buffer for k-step ks: the A piece of fragment f, the window run start
+    int aoff[NKS][MF], boff[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int q0 = ks * 16 + 8 * h;
+        const int rl = q0 / a.cols, xl0 = q0 - rl * a.cols;
+#pragma unroll
+        for (int f = 0; f < MF; ++f) {
+            const int row = (wm * MF + f) * 32 + r;
+            aoff[ks][f] = row * QC * 2 + (((q0 >> 3) ^ lp16_swz<PPR>(row)) << 4);
+        }
+        boff[ks] = BM * QC * 2 + (r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S) * 2;
+    }
+
+    if (ch_begin < ch_end) issue(ch_begin, 0);
+    for (int ch = ch_begin; ch < ch_end; ++ch) {
+        const int buf = (ch - ch_begin) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // chunk ch landed; every wave is done with the other buffer
+        if (ch + 1 < ch_end) issue(ch + 1, buf ^ 1);
+        const char* sb = reinterpret_cast<const char*>(smem16) + buf * bufB;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            u16x8 fa[MF];
+#pragma unroll
+            for (int f = 0; f < MF; ++f) fa[f] = *reinterpret_cast<const u16x8*>(sb + aoff[ks][f]);
+            unsigned w[4 * NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const uint4 p = *reinterpret_cast<const uint4*>(sb + boff[ks] + 16 * i);
+                w[4 * i + 0] = p.x, w[4 * i + 1] = p.y, w[4 * i + 2] = p.z, w[4 * i + 3] = p.w;
+            }
+            static_for<0, KK>([&](auto kxc) {
+                constexpr int kx = decltype(kxc)::value;
+                const u16x8 fb = lp16_frag<S, 7 + kx, 4 * NB>(w);
+#pragma unroll
+                for (int f = 0; f < MF; ++f) acc[f][kx] = mma16x<DT>(fa[f], fb, acc[f][kx]);
+            });
+        }
+    }
+
+    const int c = c0 + r;
+    if (c < a.C) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * a.C * T + (size_t)c * T + ky * KK;
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int m = m0 + (wm * MF + f) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (m < a.M) {
+                    float* o = out + (size_t)m * a.C * T;
+                    if constexpr (KK == 4) {
+                        *reinterpret_cast<floatx4*>(o) = floatx4{acc[f][0][reg], acc[f][1][reg], acc[f][2][reg], acc[f][3][reg]};
+                    } else {
+#pragma unroll
+                        for (int kx = 0; kx < KK; ++kx) o[kx] = acc[f][kx][reg];
+                    }
+                }
+            }
+    }
+}
+
 struct LpPlan {
     int S, KK, BM, WM, QC, splits, lds_bytes;
+    int lds16;   // 1: a and lds_bytes hold the 16-bit geometry (wgrad_lp16_kernel)
     LpArgs a;
 };
 
@@ -719,6 +899,7 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     p.BM = a.M >= 128 ? 128 : (a.M > 32 ? 64 : 32);
     p.WM = p.BM == 128 ? 2 : 1;
     p.lds_bytes = 2 * lp_buf_floats(p.BM, qc, a.pitch_c) * 4;
+    p.lds16 = 0;
     if (p.lds_bytes > 160 * 1024) return false;
     const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + kLC - 1) / kLC);
     int s = 1;
@@ -727,6 +908,33 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     a.per_split = (a.nchunk + s - 1) / s;
     p.a = a;
     return true;
+}
+
+// the 16-bit geometry of a plan (wgrad_lp16_kernel): window rows of wca16 elements from the 8-aligned origin,
+// channel pitch = 8 mod 128 elements; false when Wg % 8 != 0 or the double buffer exceeds the LDS
+bool lp16_plan(LpPlan& p) {
+    LpArgs& a = p.a;
+    if (a.Wg % 8) return false;
+    a.wca = (7 + (a.cols - 1) * p.S + p.KK + 7) / 8 * 8;
+    int pc = a.wr * a.wca;
+    while (pc % 128 != 8) pc += 8;
+    a.pitch_c = pc;
+    p.lds_bytes = 2 * lp16_buf_bytes(p.BM, p.QC, a.pitch_c) + 64;   // (+ the tail a last run may read past)
+    return p.lds_bytes <= 160 * 1024;
+}
+
+template <int S, int KK, int BM, int WM, int QC, int DT>
+int launch_lp16(const LpPlan& p, hipStream_t st) {
+    auto kfn = wgrad_lp16_kernel<S, KK, BM, WM, QC, DT>;
+    static bool opted = false;
+    if (!opted) {
+        LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        opted = true;
+    }
+    dim3 grid((p.a.C + kLC - 1) / kLC, (p.a.M + BM - 1) / BM, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * KK), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_lp16_kernel");
+    return 0;
 }
 
 template <int S, int KK, int BM, int WM, int QC, int DT, int XS>
@@ -744,6 +952,7 @@ int launch_lp_xs(const LpPlan& p, hipStream_t st) {
 }
 template <int S, int KK, int BM, int WM, int QC, int DT>
 int launch_lp_dt(const LpPlan& p, hipStream_t st) {
+    if (p.a.dense16 && p.a.gath16 && p.lds16) return launch_lp16<S, KK, BM, WM, QC, DT>(p, st);   // both 16-bit
     if (p.a.dense16 || p.a.gath16) return launch_lp_xs<S, KK, BM, WM, QC, DT, DT>(p, st);
     return launch_lp_xs<S, KK, BM, WM, QC, DT, 0>(p, st);
 }
@@ -904,7 +1113,15 @@ int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, fl
     if (!wg::plan(d, p)) return -1;
     if (dtype != LDM_DT_F32 && !wgrad_lp_disabled()) {   // 16-bit operands: the double-rate MFMA form
         wg::LpPlan lp;
-        if (wg::lp_plan(d, lp) && (!st16 || lp_staged_fits(lp))) {
+        bool ok = wg::lp_plan(d, lp);
+        if (ok && st16 == 3) {
+            wg::LpPlan l16 = lp;   // both maps 16-bit: the 16-bit DMA form where its geometry fits
+            if (wg::lp16_plan(l16)) {
+                lp = l16;
+                lp.lds16 = 1;
+            }
+        }
+        if (ok && (!st16 || lp.lds16 || lp_staged_fits(lp))) {
             lp.a.dense = dense;
             lp.a.gath = gath;
             lp.a.partial = partial;
