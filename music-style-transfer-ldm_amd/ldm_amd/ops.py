@@ -646,7 +646,7 @@ def batchnorm_train_(x, weight, bias, running_mean, running_var, momentum, eps, 
 
 
 def activation(x, act, inplace=False):
-    require_device(x)
+    require_device(x, dtype=None)   # (a 16-bit map is read through an fp32 copy)
     x = f32c(x)
     y = x if inplace else torch.empty_like(x)
     L.call("ldm_activation", x.data_ptr(), y.data_ptr(), x.numel(), L.ACT[act], stream_handle())
@@ -654,7 +654,8 @@ def activation(x, act, inplace=False):
 
 
 def batchnorm_eval(x, weight, bias, running_mean, running_var, eps, act="none"):
-    require_device(x, weight, bias, running_mean, running_var)
+    require_device(x, dtype=None)
+    require_device(weight, bias, running_mean, running_var)
     x = f32c(x)
     y = torch.empty_like(x)
     B, C = x.shape[0], x.shape[1]
@@ -669,7 +670,7 @@ _LOSS_WS = {}
 
 def loss_forward(kind, a, b=None):
     """kind 0: mean((a-b)^2); kind 1: mean(0.5*(a^2-1-log(a^2+1e-8))).  Returns a 0-dim device tensor."""
-    require_device(a, b)
+    require_device(a, b, dtype=None)
     a = f32c(a)
     if b is not None:
         b = f32c(b)
@@ -741,7 +742,8 @@ def time_mlp(t, w1, b1, w2, b2):
 
 def attention_core(q, kv, heads):
     """q [B,E,L], kv [B,2E,S] -> [B,E,L] (softmax((q*sqrt(1/d))^T k) v per head)."""
-    require_device(q, kv)
+    require_device(q, kv, dtype=None)
+    q, kv = f32c(q), f32c(kv)
     B, E, Lq = q.shape
     S = kv.shape[2]
     out = torch.empty_like(q)
@@ -759,7 +761,8 @@ def attention_uses_flash(E, heads, Lq, S):
 
 def attention_forward_lse(q, kv, heads):
     """q [B,E,L], kv [B,2E,S] -> (out [B,E,L], lse [B,heads,L]) on the KV-tiled online-softmax kernel."""
-    require_device(q, kv)
+    require_device(q, kv, dtype=None)
+    q, kv = f32c(q), f32c(kv)
     B, E, Lq = q.shape
     S = kv.shape[2]
     out = torch.empty_like(q)
@@ -800,7 +803,8 @@ def alpha_bar_coef_table(alpha_bar, device):
 
 
 def q_sample(x0, eps, coef_table, t):
-    require_device(x0, eps, coef_table)
+    require_device(x0, eps, dtype=None)
+    require_device(coef_table)
     t = t.to(x0.device, torch.int64).contiguous()
     x0 = f32c(x0)
     eps = f32c(eps)
@@ -812,7 +816,8 @@ def q_sample(x0, eps, coef_table, t):
 
 
 def predict_start(zt, eps, coef_table, t):
-    require_device(zt, eps, coef_table)
+    require_device(zt, eps, dtype=None)
+    require_device(coef_table)
     t = t.to(zt.device, torch.int64).contiguous()
     zt = f32c(zt)
     eps = f32c(eps)
@@ -878,7 +883,7 @@ def u8_to_unit(u8):
 # ---- VGGish feature / style loss pieces (features.hip; reference loss.py:52-101) ---------------------------
 def maxpool2x2(x):
     """nn.MaxPool2d(kernel_size=2, stride=2) on NCHW fp32 (floor mode)."""
-    require_device(x, what="maxpool2x2")
+    require_device(x, dtype=None, what="maxpool2x2")
     x = f32c(x)
     B, C, H, W = x.shape
     y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=torch.float32)
