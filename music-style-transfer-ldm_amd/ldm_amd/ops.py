@@ -320,8 +320,8 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     """act(BN_eval(conv(x, w) + bias)) (+ bcast[b, c]) (+ skip).  bn = (gamma, beta, mean, var, eps).
     act_out (preallocated, output-shaped) also receives act(.) before the adds.  x may be a 16-bit map of the
     operand type; out_dtype = that 16-bit type asks for a 16-bit y where the kernel stores one (else fp32)."""
-    require_device(x, dtype=None)
-    require_device(weight, bias, bcast, skip)
+    require_device(x, bcast, skip, dtype=None)   # (bcast / skip: read through fp32 copies when 16-bit)
+    require_device(weight, bias)
     B, Cin, H, W = x.shape
     if transposed:
         cin_w, Cout, kh, kw = weight.shape
