@@ -472,6 +472,13 @@ def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
     LDM_DT_* operand precision."""
     dtype = int(dtype)
     st = wgrad_storage16(desc, dtype)
+    if st == L.DT_X16 | L.DT_DY16 and (T16.get(x.dtype) == dtype) != (T16.get(dy.dtype) == dtype):
+        # one 16-bit map and one fp32 map: the fp32 one rounded to the operand type first (the kernel rounds
+        # it the same way, RNE), so both tiles take the 16-bit DMA form (wgrad_lp16_kernel) — same result
+        if T16.get(x.dtype) == dtype:
+            dy = dy.to(TORCH16[dtype])
+        else:
+            x = x.to(TORCH16[dtype])
     x, xh = in16(x, dtype, st & L.DT_X16)
     dy, dyh = in16(dy, dtype, st & L.DT_DY16)
     if desc.transposed:

@@ -162,3 +162,24 @@ def test_store16_policy():
     assert ops.store16_dtype(1 << 22, 1) == torch.float16
     assert ops.store16_dtype((1 << 22) - 1, 2) == torch.float32
     assert ops.store16_dtype(1 << 24, 0) == torch.float32
+
+
+@pytest.mark.parametrize("which", ["x16", "dy16"])
+def test_wgrad_mixed_maps(cuda, which):
+    """A weight gradient with one 16-bit and one fp32 map (the VAE's third layer: 16-bit input, fp32 output
+    gradient; the decoder's first layer the other way round): the fp32 map is rounded to the operand type
+    first, as the kernel rounds it, so the result equals the all-fp32-storage form."""
+    from ldm_amd import ops
+    dt = 2
+    B, Cin, H, W, Cout = 2, 64, 32, 128, 32
+    desc = ops.make_desc(B, Cin, H, W, Cout, 3, 3, 2, 1)
+    x16, x32 = _q(_rand((B, Cin, H, W), 61), dt)
+    g = _rand((B, Cout, desc.Hout, desc.Wout), 62)
+    g16, g32 = _q(g, dt)
+    ref = ops.conv_backward_weight(x32.to(cuda), g32.to(cuda), desc, dtype=dt)
+    if which == "x16":
+        got = ops.conv_backward_weight(x16.to(cuda), g.to(cuda), desc, dtype=dt)   # dy fp32, rounded inside
+    else:
+        got = ops.conv_backward_weight(_rand((B, Cin, H, W), 61).to(cuda), g16.to(cuda), desc, dtype=dt)   # x fp32
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
