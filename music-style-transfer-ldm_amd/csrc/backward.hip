@@ -467,9 +467,9 @@ using namespace ldm;
 // ---- weight gradient ------------------------------------------------------------------------------
 // ---- weight gradient of a 1x1 conv (the cross-attention projections): dW[m][c] = sum_b sum_n dy[b][m][n] x[b][c][n]
 // over HW % 16 == 0 planes, an NT GEMM whose K (b, n) is contiguous in both NCHW operands.  A block owns a 32 x 32
-// tile of dW; its four waves take interleaved quarters of the 16-position k-steps (the next step's loads issued
-// before this step's MFMAs) and meet in LDS in wave order, so no split-K partials and no reduction launch (the
-// tap-shared form above ran these at 16 x 16 tiles of one wave plus a reduction).  DT 0: fp32 operands on
+// tile of dW; its eight waves take interleaved eighths of the 16-position k-steps (two steps per iteration, the
+// next two steps' loads issued before these MFMAs) and meet in LDS in wave order, so no split-K partials and no
+// reduction launch (the tap-shared form above ran these at 16 x 16 tiles of one wave plus a reduction).  DT 0: fp32 operands on
 // v_mfma_f32_32x32x2f32 (the k-pairs in a fixed permutation); DT 1 / 2: operands rounded to fp16 / bf16 on the
 // double-rate 32x32x16 MFMA (the autocast region's weight gradients).
 typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
@@ -483,9 +483,32 @@ struct W1Args {
     int32_t B, M, C, HW, accumulate;
 };
 
+constexpr int kW1Waves = 8;   // waves per block of wgrad_1x1_kernel (the K quarters... eighths)
+
 template <int DT>
-__global__ __launch_bounds__(256) void wgrad_1x1_kernel(W1Args a) {
-    __shared__ float red[4][16][64];
+__device__ __forceinline__ floatx16 w1_mma(const floatx4 (&ca)[2], const floatx4 (&cb)[2], floatx16 acc) {
+    if constexpr (DT == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[j >> 2][j & 3], cb[j >> 2][j & 3], acc, 0, 0, 0);
+        return acc;
+    } else {
+        const wfloatx8 fa{ca[0][0], ca[0][1], ca[0][2], ca[0][3], ca[1][0], ca[1][1], ca[1][2], ca[1][3]};
+        const wfloatx8 fb{cb[0][0], cb[0][1], cb[0][2], cb[0][3], cb[1][0], cb[1][1], cb[1][2], cb[1][3]};
+        if constexpr (DT == 1)
+            return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_convertvector(fa, whalfx8),
+                                                          __builtin_convertvector(fb, whalfx8), acc, 0, 0, 0);
+        else
+            return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_convertvector(fa, wbf16x8),
+                                                           __builtin_convertvector(fb, wbf16x8), acc, 0, 0, 0);
+    }
+}
+
+// wave w takes k-steps w, w + 8, ...: two steps per iteration, the next two steps' loads issued before these
+// MFMAs (the chain is load latency-bound, not MFMA-bound)
+template <int DT>
+__global__ __launch_bounds__(64 * kW1Waves) void wgrad_1x1_kernel(W1Args a) {
+    __shared__ float red[kW1Waves][16][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
@@ -494,7 +517,9 @@ __global__ __launch_bounds__(256) void wgrad_1x1_kernel(W1Args a) {
     const size_t sa = (size_t)a.M * a.HW, sb = (size_t)a.C * a.HW;
     const float* pa = a.dy + (size_t)(m0 + r) * a.HW + 8 * h;
     const float* pb = a.x + (size_t)(c0 + r) * a.HW + 8 * h;
+    // step st (clamped to the last one: a re-load whose MFMA is skipped)
     auto load = [&](int st, floatx4 (&va)[2], floatx4 (&vb)[2]) {
+        st = st < nsteps ? st : nsteps - 1;
         const int b = st / spp, n0 = (st - b * spp) * 16;
         const float* qa = pa + b * sa + n0;
         const float* qb = pb + b * sb + n0;
@@ -506,36 +531,27 @@ __global__ __launch_bounds__(256) void wgrad_1x1_kernel(W1Args a) {
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    floatx4 ca[2], cb[2], na[2], nb[2];
-    int st = wave;
-    if (st < nsteps) load(st, ca, cb);
-    for (; st < nsteps; st += 4) {
-        const int nx = st + 4 < nsteps ? st + 4 : st;   // (past the end: a harmless re-load)
-        load(nx, na, nb);
-        if constexpr (DT == 0) {
+    constexpr int W = kW1Waves;
+    floatx4 ca0[2], cb0[2], ca1[2], cb1[2], na0[2], nb0[2], na1[2], nb1[2];
+    load(wave, ca0, cb0);
+    load(wave + W, ca1, cb1);
+    for (int st = wave; st < nsteps; st += 2 * W) {
+        load(st + 2 * W, na0, nb0);
+        load(st + 3 * W, na1, nb1);
+        acc = w1_mma<DT>(ca0, cb0, acc);
+        if (st + W < nsteps) acc = w1_mma<DT>(ca1, cb1, acc);
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[j >> 2][j & 3], cb[j >> 2][j & 3], acc, 0, 0, 0);
-        } else {
-            const wfloatx8 fa{ca[0][0], ca[0][1], ca[0][2], ca[0][3], ca[1][0], ca[1][1], ca[1][2], ca[1][3]};
-            const wfloatx8 fb{cb[0][0], cb[0][1], cb[0][2], cb[0][3], cb[1][0], cb[1][1], cb[1][2], cb[1][3]};
-            if constexpr (DT == 1)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_convertvector(fa, whalfx8),
-                                                             __builtin_convertvector(fb, whalfx8), acc, 0, 0, 0);
-            else
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_convertvector(fa, wbf16x8),
-                                                              __builtin_convertvector(fb, wbf16x8), acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) ca[i] = na[i], cb[i] = nb[i];
+        for (int i = 0; i < 2; ++i) ca0[i] = na0[i], cb0[i] = nb0[i], ca1[i] = na1[i], cb1[i] = nb1[i];
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
     __syncthreads();
-    // 1024 outputs, four per thread: the wave partials summed in wave order
-    for (int o = threadIdx.x; o < 16 * 64; o += 256) {
+    // 1024 outputs, two per thread: the wave partials summed in wave order
+    for (int o = threadIdx.x; o < 16 * 64; o += 64 * W) {
         const int reg = o >> 6, l = o & 63;
-        const float v = ((red[0][reg][l] + red[1][reg][l]) + red[2][reg][l]) + red[3][reg][l];
+        float v = red[0][reg][l];
+#pragma unroll
+        for (int w = 1; w < W; ++w) v += red[w][reg][l];
         const int m = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5), c = c0 + (l & 31);
         float* d = a.dw + (size_t)m * a.C + c;
         *d = a.accumulate ? *d + v : v;
@@ -618,9 +634,10 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
         W1Args w{dy, x, dw, d->B, d->Cout, d->Cin, d->Hout * d->Wout, accumulate};
         const dim3 grid(d->Cin / 32, d->Cout / 32);
         hipStream_t s1 = (hipStream_t)stream;
-        if (dtype == LDM_DT_F16) hipLaunchKernelGGL(wgrad_1x1_kernel<1>, grid, dim3(256), 0, s1, w);
-        else if (dtype == LDM_DT_BF16) hipLaunchKernelGGL(wgrad_1x1_kernel<2>, grid, dim3(256), 0, s1, w);
-        else hipLaunchKernelGGL(wgrad_1x1_kernel<0>, grid, dim3(256), 0, s1, w);
+        const dim3 blk(64 * kW1Waves);
+        if (dtype == LDM_DT_F16) hipLaunchKernelGGL(wgrad_1x1_kernel<1>, grid, blk, 0, s1, w);
+        else if (dtype == LDM_DT_BF16) hipLaunchKernelGGL(wgrad_1x1_kernel<2>, grid, blk, 0, s1, w);
+        else hipLaunchKernelGGL(wgrad_1x1_kernel<0>, grid, blk, 0, s1, w);
         LDM_CHECK_LAUNCH("wgrad_1x1_kernel");
         return 0;
     }
