@@ -467,7 +467,7 @@ using namespace ldm;
 // ---- weight gradient ------------------------------------------------------------------------------
 // ---- weight gradient of a 1x1 conv (the cross-attention projections): dW[m][c] = sum_b sum_n dy[b][m][n] x[b][c][n]
 // over HW % 16 == 0 planes, an NT GEMM whose K (b, n) is contiguous in both NCHW operands.  A block owns a 32 x 32
-// tile of dW; its eight waves take interleaved eighths of the 16-position k-steps (two steps per iteration, the
+// tile of dW; its eight waves take interleaved shares of the 16-position k-steps (two steps per iteration, the
 // next two steps' loads issued before these MFMAs) and meet in LDS in wave order, so no split-K partials and no
 // reduction launch (the tap-shared form above ran these at 16 x 16 tiles of one wave plus a reduction).  DT 0: fp32 operands on
 // v_mfma_f32_32x32x2f32 (the k-pairs in a fixed permutation); DT 1 / 2: operands rounded to fp16 / bf16 on the
@@ -483,7 +483,7 @@ struct W1Args {
     int32_t B, M, C, HW, accumulate;
 };
 
-constexpr int kW1Waves = 8;   // waves per block of wgrad_1x1_kernel (the K quarters... eighths)
+constexpr int kW1Waves = 8;   // waves per block of wgrad_1x1_kernel (interleaved k-step shares; 16: 88 vs 79 us per step)
 
 template <int DT>
 __device__ __forceinline__ floatx16 w1_mma(const floatx4 (&ca)[2], const floatx4 (&cb)[2], floatx16 acc) {
