@@ -439,7 +439,8 @@ __global__ __launch_bounds__(64 * kChanWaves) void act_bwd_chan_kernel(const voi
     for (int b = wave; b < B; b += kChanWaves) {
         const size_t base = ((size_t)b * C + c) * HW;
         float sd = 0.f, sg = 0.f;
-        for (int i = lane * 4; i < HW; i += 256) {
+#pragma unroll 4
+        for (int i = lane * 4; i < HW; i += 256) {   // (unrolled: the plane's loads issued together)
             float g[4], d[4];
             ld_st<ST, 4>(dy, base + i, dyh, g);
             if (aval) {

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 4 final: the whole -m gpu suite, smoke(), the headline bench with its rocprofv3 summary, the secondary
-# lines (transfer, train + its kernel summary) and the train-step PMC passes; copies what is judged into
-# profiles/r04.   bash tools/gpu_r4_final.sh <tag>
+# Round-end validation: the whole -m gpu suite, smoke(), the headline bench with its rocprofv3 summary, the
+# secondary lines (transfer, train + its kernel summary) and the train-step PMC passes, all under
+# gpurun_out/<tag>/ (the judged copies go to profiles/rNN/ by hand).   bash tools/gpu_round_end.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-T=${1:-r4final}; O=$PWD/gpurun_out/$T; mkdir -p $O
+T=${1:-round_end}; O=$PWD/gpurun_out/$T; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -3 $O/gpu_tests.log
 if [ $rc -ne 0 ]; then grep -E "^FAILED|^ERROR" $O/gpu_tests.log | head -20; echo "FAILED: pytest -m gpu exited $rc"; exit $rc; fi
