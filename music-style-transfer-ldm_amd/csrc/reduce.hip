@@ -12,7 +12,6 @@
 // slices in order), so results are bitwise reproducible run to run.  BatchNorm statistics are fp64
 // (sum x, sum x^2) so the per-rank sums can be all-reduced for SyncBatchNorm between the two stages
 // (ldm_batchnorm_stats -> all-reduce -> ldm_batchnorm_apply; likewise the backward).
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -420,58 +419,6 @@ __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const void* __
     }
 }
 
-// The planes (HW = 64..1024) with their sums, in ONE launch: a block per channel, its 16 waves taking the B planes
-// of that channel in turn (plane b to wave b % 16), each plane's dv and dy sums a wave shuffle tree (dbcast[b, c]
-// from lane 0), the channel's dv sum the waves' partials in wave order (dbias[c]).  Replaces the per-plane
-// kernel + the finalize launch (two launches per call, ~10 us at the train batch) when sums are asked for.
-constexpr int kChanWaves = 16;
-template <int ST>
-__global__ __launch_bounds__(64 * kChanWaves) void act_bwd_chan_kernel(const void* __restrict__ dy,
-                                                                      const void* __restrict__ aval, int act, int sf,
-                                                                      int B, int C, int HW, void* dv,
-                                                                      float* __restrict__ dbias,
-                                                                      float* __restrict__ dbcast) {
-    __shared__ float wsum[kChanWaves];
-    const bool dyh = sf & LDM_ST_DY16, ah = sf & LDM_ST_X16, dvh = sf & LDM_ST_DX16;
-    const int c = blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float sdw = 0.f;
-    for (int b = wave; b < B; b += kChanWaves) {
-        const size_t base = ((size_t)b * C + c) * HW;
-        float sd = 0.f, sg = 0.f;
-#pragma unroll 4
-        for (int i = lane * 4; i < HW; i += 256) {   // (unrolled: the plane's loads issued together)
-            float g[4], d[4];
-            ld_st<ST, 4>(dy, base + i, dyh, g);
-            if (aval) {
-                float a4[4];
-                ld_st<ST, 4>(aval, base + i, ah, a4);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) d[j] = g[j] * act_grad(act, a4[j]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) d[j] = g[j];
-            }
-            if (dv) st_st<ST, 4>(dv, base + i, dvh, d);
-            sd += ((d[0] + d[1]) + d[2]) + d[3];
-            sg += ((g[0] + g[1]) + g[2]) + g[3];
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            sd += __shfl_xor(sd, o);
-            sg += __shfl_xor(sg, o);
-        }
-        if (lane == 0 && dbcast) dbcast[(size_t)b * C + c] = sg;
-        sdw += sd;
-    }
-    if (lane == 0) wsum[wave] = sdw;
-    __syncthreads();
-    if (threadIdx.x == 0 && dbias) {
-        float t = wsum[0];
-        for (int w = 1; w < kChanWaves; ++w) t += wsum[w];
-        dbias[c] = t;
-    }
-}
-
 // dbias[c] = sum_b sum_k part_dv;  dbcast[b,c] = sum_k part_dy.  One block per channel: a plane's Q slice
 // partials go to QP lanes (QP = Q rounded up to a power of two, at most 64; lane stride past 64), so a wave
 // takes 64 / QP planes per step (wave w the planes from w * 64 / QP on, stepping by 256 / QP) and sums each
@@ -841,19 +788,6 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
     LDM_REQUIRE(!sums || workspace, "act_backward: bias / bcast sums need the workspace");
     // act none: dv = dy, so the write is dropped only when dv IS dy (a separate dv buffer is still written)
     float* dvp = act == LDM_ACT_NONE && dv == dy ? nullptr : dv;
-    static const bool chan = [] {   // LDM_ACT_BWD_CHAN=0: the per-plane kernel + finalize (A/B timing)
-        const char* e = std::getenv("LDM_ACT_BWD_CHAN");
-        return !e || e[0] != '0';
-    }();
-    if (chan && sums && HW >= 64 && HW <= 1024 && (HW & (HW - 1)) == 0 && act != LDM_ACT_GELU &&
-        vec_ok(HW, dy, aval0, nullptr, dvp)) {
-        st_dispatch(sc, [&](auto stc) {
-            hipLaunchKernelGGL((act_bwd_chan_kernel<decltype(stc)::value>), dim3(C), dim3(64 * kChanWaves), 0, st, dy,
-                               aval0, act, sc.sf, B, C, HW, dvp, dbias, dbcast);
-        });
-        LDM_CHECK_LAUNCH("act_bwd_chan_kernel");
-        return 0;
-    }
     if (HW >= 64 && HW <= 1024 && (HW & (HW - 1)) == 0 && act != LDM_ACT_GELU && vec_ok(HW, dy, aval0, nullptr, dvp)) {
         const int nplanes = B * C;
         float* part = sums ? workspace : nullptr;
