@@ -285,7 +285,13 @@ template <int ST, int W>
 __device__ __forceinline__ void ld_st(const void* p, size_t o, bool h, float (&v)[W]) {
     if (ST != 0 && h) {
         const unsigned short* q = reinterpret_cast<const unsigned short*>(p) + o;
-        if constexpr (W == 4) {
+        if constexpr (W == 8) {   // one 16-byte load
+            const uint4 t = *reinterpret_cast<const uint4*>(q);
+            const unsigned u[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                v[2 * j] = from16<ST>((unsigned short)(u[j] & 0xffff)), v[2 * j + 1] = from16<ST>((unsigned short)(u[j] >> 16));
+        } else if constexpr (W == 4) {
             const uint2 t = *reinterpret_cast<const uint2*>(q);
             v[0] = from16<ST>((unsigned short)(t.x & 0xffff)), v[1] = from16<ST>((unsigned short)(t.x >> 16));
             v[2] = from16<ST>((unsigned short)(t.y & 0xffff)), v[3] = from16<ST>((unsigned short)(t.y >> 16));
@@ -295,9 +301,12 @@ __device__ __forceinline__ void ld_st(const void* p, size_t o, bool h, float (&v
         }
     } else {
         const float* q = reinterpret_cast<const float*>(p) + o;
-        if constexpr (W == 4) {
-            const float4 t = *reinterpret_cast<const float4*>(q);
-            v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
+        if constexpr (W % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < W; j += 4) {
+                const float4 t = *reinterpret_cast<const float4*>(q + j);
+                v[j] = t.x, v[j + 1] = t.y, v[j + 2] = t.z, v[j + 3] = t.w;
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < W; ++j) v[j] = q[j];
@@ -308,7 +317,13 @@ template <int ST, int W>
 __device__ __forceinline__ void st_st(void* p, size_t o, bool h, const float (&v)[W]) {
     if (ST != 0 && h) {
         unsigned short* q = reinterpret_cast<unsigned short*>(p) + o;
-        if constexpr (W == 4) {
+        if constexpr (W == 8) {   // one 16-byte store
+            unsigned u[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                u[j] = (unsigned)to16s<ST>(v[2 * j]) | ((unsigned)to16s<ST>(v[2 * j + 1]) << 16);
+            *reinterpret_cast<uint4*>(q) = make_uint4(u[0], u[1], u[2], u[3]);
+        } else if constexpr (W == 4) {
             uint2 t;
             t.x = (unsigned)to16s<ST>(v[0]) | ((unsigned)to16s<ST>(v[1]) << 16);
             t.y = (unsigned)to16s<ST>(v[2]) | ((unsigned)to16s<ST>(v[3]) << 16);
@@ -319,8 +334,10 @@ __device__ __forceinline__ void st_st(void* p, size_t o, bool h, const float (&v
         }
     } else {
         float* q = reinterpret_cast<float*>(p) + o;
-        if constexpr (W == 4) {
-            *reinterpret_cast<float4*>(q) = make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (W % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < W; j += 4)
+                *reinterpret_cast<float4*>(q + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
         } else {
 #pragma unroll
             for (int j = 0; j < W; ++j) q[j] = v[j];

@@ -12,6 +12,7 @@
 // slices in order), so results are bitwise reproducible run to run.  BatchNorm statistics are fp64
 // (sum x, sum x^2) so the per-rank sums can be all-reduced for SyncBatchNorm between the two stages
 // (ldm_batchnorm_stats -> all-reduce -> ldm_batchnorm_apply; likewise the backward).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -21,16 +22,31 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// blocks a BatchNorm pass aims for (LDM_BN_BLOCKS, default 2048: 8 blocks of 256 threads per CU, so 32 waves
+// keep enough 16-byte loads in flight; 1024 left the normalise / backward passes at 2.4-3.5 TB/s)
+inline int64_t bn_blocks() {
+    static const int64_t v = [] {
+        const char* e = getenv("LDM_BN_BLOCKS");
+        const long x = e ? atol(e) : 2048;
+        return (int64_t)(x >= 256 && x <= 16384 ? x : 2048);
+    }();
+    return v;
+}
+
 // slices per channel for a reduction over n = B*HW elements across C channels
 inline int bn_slices(int64_t n, int C) {
-    int64_t p = (1024 + C - 1) / C;                 // >= 1024 blocks in total
+    int64_t p = (bn_blocks() + C - 1) / C;          // >= bn_blocks() blocks in total
     const int64_t by_len = (n + 2047) / 2048;       // but >= ~2048 elements per slice
     if (p > by_len) p = by_len;
     if (p < 1) p = 1;
     if (p > 256) p = 256;
     return (int)p;
 }
-inline int64_t slice_len(int64_t n, int P) { return ((n + P - 1) / P + 3) & ~(int64_t)3; }
+// slice length: a multiple of the access width W (4 or 8 elements; 4 for the scalar form, as before)
+inline int64_t slice_len(int64_t n, int P, int W = 4) {
+    const int64_t a = W > 4 ? W : 4;
+    return ((n + P - 1) / P + a - 1) / a * a;
+}
 
 // slices per (b,c) plane for the activation backward
 inline int act_slices(int B, int C, int HW) {
@@ -67,20 +83,7 @@ __device__ __forceinline__ float act_grad(int act, float a) {
 
 template <int W>
 __device__ __forceinline__ void ld(const float* p, float (&v)[W]) {
-    if constexpr (W == 4) {
-        const float4 t = *reinterpret_cast<const float4*>(p);
-        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-    } else {
-        v[0] = *p;
-    }
-}
-template <int W>
-__device__ __forceinline__ void st(float* p, const float (&v)[W]) {
-    if constexpr (W == 4) {
-        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-        *p = v[0];
-    }
+    ld_st<0, W>(p, 0, false, v);
 }
 
 // Visit channel c's elements with flattened (b, hw) index in [e0, e1): f(offset) for W consecutive
@@ -516,6 +519,25 @@ bool vec_ok(int HW, const void* a, const void* b = nullptr, const void* c = null
     return HW % 4 == 0 && al(a) && al(b) && al(c) && al(d);
 }
 
+// elements per thread access of the sliced kernels: 8 (one 16-byte load of a 16-bit map, two float4 of an fp32
+// one) when HW % 8 == 0 and the pointers are 16-byte aligned, else 4 (float4 / 8-byte), else 1.  The width
+// depends only on HW and alignment, never on the storage type, so a map's sums keep the same order (and bits)
+// in 16-bit and fp32 storage.  LDM_REDUCE_W8=0: 4 at most.
+inline int vec_width(int HW, const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr) {
+    static const bool w8 = [] {
+        const char* e = getenv("LDM_REDUCE_W8");
+        return !(e && e[0] == '0');
+    }();
+    if (!vec_ok(HW, a, b, c, d)) return 1;
+    return w8 && HW % 8 == 0 ? 8 : 4;
+}
+template <class F>
+void w_dispatch(int w, F&& f) {
+    if (w == 8) f(std::integral_constant<int, 8>{});
+    else if (w == 4) f(std::integral_constant<int, 4>{});
+    else f(std::integral_constant<int, 1>{});
+}
+
 // the storage fields of an act code (ldm_capi.h LDM_ST_*): 16-bit type, per-tensor flags, and the act + round
 // bits the kernels read
 struct StCode {
@@ -552,17 +574,14 @@ static int bn_stats_launch(const void* x, const StCode& sc, int32_t B, int32_t C
                            void* stream) {
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
+    const int vw = vec_width(HW, x);
+    const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
-    const bool v4 = vec_ok(HW, x);
     st_dispatch(sc, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (v4)
-            hipLaunchKernelGGL((bn_stats_partial_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, sc.sf,
-                               C, HW, n, S, part);
-        else
-            hipLaunchKernelGGL((bn_stats_partial_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, sc.sf,
-                               C, HW, n, S, part);
+        w_dispatch(vw, [&](auto wc) {
+            hipLaunchKernelGGL((bn_stats_partial_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads),
+                               0, (hipStream_t)stream, x, sc.sf, C, HW, n, S, part);
+        });
     });
     LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
     return 0;
@@ -596,20 +615,16 @@ static int bn_apply_launch(const float* x, float* y, int32_t B, int32_t C, int32
                            float* save_invstd, const double* part, void* stream) {
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
-    const dim3 grid(P, C);
     const StCode sc = st_code(act);
-    const bool v4 = vec_ok(HW, x, y);
+    const int vw = vec_width(HW, x, y);
+    const int64_t S = slice_len(n, P, vw);
+    const dim3 grid(P, C);
     st_dispatch(sc, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (v4)
-            hipLaunchKernelGGL((bn_apply_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, sc.sf, C, HW,
-                               n, S, stats, count, weight, bias, running_mean, running_var, momentum, eps, sc.act,
-                               save_mean, save_invstd, part, part ? P : 0);
-        else
-            hipLaunchKernelGGL((bn_apply_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, x, y, sc.sf, C, HW,
-                               n, S, stats, count, weight, bias, running_mean, running_var, momentum, eps, sc.act,
-                               save_mean, save_invstd, part, part ? P : 0);
+        w_dispatch(vw, [&](auto wc) {
+            hipLaunchKernelGGL((bn_apply_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0,
+                               (hipStream_t)stream, x, y, sc.sf, C, HW, n, S, stats, count, weight, bias, running_mean,
+                               running_var, momentum, eps, sc.act, save_mean, save_invstd, part, part ? P : 0);
+        });
     });
     LDM_CHECK_LAUNCH("bn_apply_kernel");
     return 0;
@@ -667,17 +682,15 @@ static int bn_bwd_partial_launch(const void* dy, const void* y, const void* x, c
                                   int act, int32_t B, int32_t C, int32_t HW, double* part, void* stream) {
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
+    const int vw = vec_width(HW, dy, y, x);
+    const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
-    const bool v4 = vec_ok(HW, dy, y, x);
     st_dispatch(sc, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (v4)
-            hipLaunchKernelGGL((bn_bwd_partial_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
-                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, part);
-        else
-            hipLaunchKernelGGL((bn_bwd_partial_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
-                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, part);
+        w_dispatch(vw, [&](auto wc) {
+            hipLaunchKernelGGL((bn_bwd_partial_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads),
+                               0, (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW,
+                               n, S, part);
+        });
     });
     LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
     return 0;
@@ -713,19 +726,15 @@ static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, con
     if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
-    const int64_t S = slice_len(n, P);
+    const int vw = vec_width(HW, dy, y, x, dx);
+    const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
-    const bool v4 = vec_ok(HW, dy, y, x, dx);
     st_dispatch(sc, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (v4)
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<4, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
-                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part,
-                               part ? P : 0, dweight, dbias);
-        else
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<1, ST>), grid, dim3(kThreads), 0, (hipStream_t)stream, dy, y, x,
-                               sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n, S, sums, count, dx, part,
-                               part ? P : 0, dweight, dbias);
+        w_dispatch(vw, [&](auto wc) {
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0,
+                               (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n,
+                               S, sums, count, dx, part, part ? P : 0, dweight, dbias);
+        });
     });
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
     return 0;
@@ -811,19 +820,16 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         return 0;
     }
     const int Q = act_slices(B, C, HW);
-    const int64_t S = ((HW + Q - 1) / Q + 3) & ~3;
-    const dim3 grid(Q, B * C);
     const float* aval = aval0;
     float* part = sums ? workspace : nullptr;
-    const bool v4 = vec_ok(HW, dy, aval, pre_act, dv);
+    const int vw = vec_width(HW, dy, aval, pre_act, dv);
+    const int64_t S = slice_len(HW, Q, vw);
+    const dim3 grid(Q, B * C);
     st_dispatch(sc, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (v4)
-            hipLaunchKernelGGL((act_bwd_kernel<4, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
-                               HW, S, dv, part);
-        else
-            hipLaunchKernelGGL((act_bwd_kernel<1, ST>), grid, dim3(kThreads), 0, st, dy, aval, pre_act, act, sc.sf, C,
-                               HW, S, dv, part);
+        w_dispatch(vw, [&](auto wc) {
+            hipLaunchKernelGGL((act_bwd_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0, st,
+                               dy, aval, pre_act, act, sc.sf, C, HW, S, dv, part);
+        });
     });
     LDM_CHECK_LAUNCH("act_bwd_kernel");
     if (sums) {
