@@ -144,6 +144,8 @@ struct PackJob {   // one weight of a multi-tensor re-pack (pack.hip); filled by
     int64_t wofs[kMaxPhase];
     int32_t kk[kMaxPhase][kMaxTap];
     FastDiv fd_mpad, fd_cin, fd_ntap[kMaxPhase];
+    FastDiv fd_kr;                 // kinds 1/2 with remap: 8-element runs per packed row (K / 8)
+    int32_t remap;
 };
 int conv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j);    // kinds 1, 2 (conv.hip)
 int tconv_pack_job(const ldm_conv_desc& d, const ldm_conv_plan& p, PackJob& j);   // kind 3 (tconv.hip)
