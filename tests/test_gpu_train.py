@@ -128,11 +128,12 @@ def test_linear_and_gelu_backward(cuda):
         assert rel_err(npy(g.grad), r.grad.numpy()) < TOL
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 8, 8), (3, 8, 36, 36), (5, 4, 30, 30), (32, 16, 16, 64)])
+@pytest.mark.parametrize("shape", [(4, 64, 8, 8), (3, 8, 36, 36), (5, 4, 30, 30), (3, 6, 7, 9), (32, 16, 16, 64)])
 @pytest.mark.parametrize("act", ["none", "relu"])
 def test_batchnorm_train_backward(cuda, act, shape):
     """Train-mode BN forward / backward against fp64 autograd; the shapes force several slices per
-    channel (P > 1), slices crossing plane boundaries, the scalar path (HW % 4 != 0) and the B=32 form."""
+    channel (P > 1), slices crossing plane boundaries, the three access widths (8 elements: HW % 8 == 0,
+    float4: HW = 900, scalar: HW = 63) and the B=32 form."""
     from ldm_amd import nn as hnn
     C = shape[1]
     x = _rand(shape, 21, -2, 2)
@@ -606,12 +607,12 @@ def test_wgrad_tap_shared(cuda, case):
 
 @pytest.mark.parametrize("shape", [(32, 128, 1, 1), (32, 512, 2, 8), (3, 8, 36, 36), (2, 64, 5, 5),
                                    (4, 96, 8, 8), (5, 24, 8, 16), (3, 40, 16, 16), (2, 8, 16, 32), (2, 16, 16, 64),
-                                   (70, 4, 8, 8), (300, 2, 4, 16), (40, 3, 40, 40)])
+                                   (70, 4, 8, 8), (300, 2, 4, 16), (40, 3, 40, 40), (3, 8, 30, 30)])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu"])
 def test_act_backward_sums(cuda, shape, act):
     """ldm_act_backward (dv, dbias, dbcast) against fp64 on the small-plane kernel (HW <= 16), the multi-plane
-    kernel (HW = 64..1024, powers of two: 16-256 threads per plane) and the sliced one (scalar and float4
-    paths)."""
+    kernel (HW = 64..1024, powers of two: 16-256 threads per plane) and the sliced one (scalar: HW = 25, float4:
+    HW % 8 == 4, 8-wide: HW % 8 == 0)."""
     from ldm_amd import ops
     B, C = shape[0], shape[1]
     v = torch.from_numpy(_rand(shape, 31, -2, 2)).double()
