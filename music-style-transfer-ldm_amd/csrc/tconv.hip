@@ -888,7 +888,8 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     // LDM_TCONV_WIN: bit 0 the single-phase window forms, bit 1 the four-phase form of the k3 s2 op1 transposed
     // convs (0 = the per-chunk gather form everywhere).  Default bit 0 only: in the train step (B = 32, bf16)
     // 4.899 ms per step on the gather form, 4.823 with bit 0, 4.874 with both — the four-phase form won only on
-    // style_enc3's data gradient (85 -> 71 us) and lost 5-16 us on the other four (profiles/r04/tconv_window)
+    // style_enc3's data gradient (85 -> 71 us) and lost 5-16 us on the other four (profiles/r04/tconv_window);
+    // re-measured with the maps in 16 bits: 909 vs 724 us for those layers, 3.98-4.00 vs 3.86-3.95 ms per step
     static const int win = [] {
         const char* e = std::getenv("LDM_TCONV_WIN");
         return e ? (int)std::strtol(e, nullptr, 0) : 1;
