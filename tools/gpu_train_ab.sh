@@ -11,7 +11,7 @@
 # A setting is space-free VAR=VALUE pairs joined by commas, e.g.
 #   bash tools/gpu_train_ab.sh st16 tests LDM_AMD_STORE16=1 LDM_AMD_STORE16=0
 # Switches measured this way: LDM_AMD_STORE16, LDM_AMD_STORE16_MIN, LDM_AMD_BRANCH_STREAMS,
-# LDM_WGRAD_1X1, LDM_TCONV_WIN, LDM_AMD_AUTOCAST_OUT.
+# LDM_WGRAD_1X1, LDM_TCONV_WIN, LDM_AMD_AUTOCAST_OUT, LDM_BN_BLOCKS, LDM_REDUCE_W8.
 # Output: gpurun_out/<tag>/train_<round>_<i>.json, prof_<i>/ and one summary line per setting and round.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
