@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2_kernel(ConvArgs a) {
 // order.  At B = 32 the two-rows-per-lane kernel has 65,536 lanes, one 4-wave block per CU walking all 64
 // channels in a chain of dependent loads (119 us per launch); here 4x the waves walk a quarter each.
 template <int LP, int RO, int XS>
-__global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, 4) void convT4_cout1_r2s_kernel(ConvArgs a) {
     __shared__ float part[3][32][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int W4 = a.Win >> 2, H2 = a.Hin >> 1;
@@ -1272,22 +1272,15 @@ __global__ __launch_bounds__(256) void convT4_cout1_r2s_kernel(ConvArgs a) {
                             acc[u][ry][2 * jj + rx] = fmaf(xr[1 + u + dy][1 + jj + dx], w, acc[u][ry][2 * jj + rx]);
                     }
     };
-    // cq even; channel order kept within the quarter; the next channel pair's loads are issued before the
-    // current pair's FMAs (the last pass re-loads the final pair: a harmless L2 hit)
-    float xa[4][6], xb[4][6], na[4][6], nb[4][6];
-    load(xp, xa);
-    load(xp + HW, xb);
-    for (int ci = c0; ci < c0 + cq; ci += 2) {
-        const float* np = ci + 2 < c0 + cq ? xp + 2 * HW : xp;
-        load(np, na);
-        load(np + HW, nb);
+    // cq even; channel order kept within the quarter.  No register prefetch of the next pair: without it the
+    // kernel fits 128 VGPRs, so the 1024 blocks of B = 32 are resident at once (4 waves per SIMD) instead of
+    // 3 + 1 rounds at 164 VGPRs, and the other waves hide the loads
+    float xa[4][6], xb[4][6];
+    for (int ci = c0; ci < c0 + cq; ci += 2, xp += 2 * HW) {
+        load(xp, xa);
+        load(xp + HW, xb);
         mac(xa, a.w + ci * 16);
         mac(xb, a.w + (ci + 1) * 16);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int c = 0; c < 6; ++c) xa[i][c] = na[i][c], xb[i][c] = nb[i][c];
-        xp = np;
     }
     if (g > 0) {
 #pragma unroll
