@@ -7,12 +7,21 @@ One bench "step" = one complete 49-iteration reverse loop over the batch (replay
 including the reference's per-step pred_x0 / noise_pred log copies).  value = denoising iterations
 (UNet forward + DDIM update over a batch-8 latent) per second summed over all ranks.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]       (N > 1: bench.py starts its own N ranks)
     torchrun --nproc-per-node N bench.py --gpus N ...      (weak scaling: 8 latents per GPU)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py is its own launcher: before any GPU call it
+checks that N HIP devices are visible, starts N fresh worker processes of itself (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, the same env:// rendezvous and init_process_group("nccl")
+path torchrun gives them), waits for them and exits with the first failing rank's code.  Under torchrun
+(WORLD_SIZE set) --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -389,13 +398,91 @@ def run_train(args, world, rank, dev, M):
     }
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, cmd, env=None, poll_s=0.2, grace_s=30.0):
+    """Start `cmd` as n worker processes, rank r with RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n,
+    MASTER_ADDR = 127.0.0.1 and one free MASTER_PORT (an inherited MASTER_PORT is kept), every other variable
+    inherited (HSA_ENABLE_IPC_MODE_LEGACY=0 among them).  The workers share this process's stdout / stderr (rank 0
+    prints the JSON line).  Waits for all of them; when one fails, the others get SIGTERM after `grace_s` seconds
+    (they are usually blocked in a collective with the dead rank) and SIGKILL if they ignore it.  Returns 0 or the
+    exit code of the first rank that failed.  The workers stay in this process's process group (a `timeout` or
+    job-control signal to the group reaches them too); this function signals only the PIDs it started, and a
+    SIGTERM to this process is forwarded to them."""
+    base = dict(os.environ if env is None else env)
+    base["MASTER_ADDR"] = "127.0.0.1"
+    base.setdefault("MASTER_PORT", str(_free_port()))
+    base["WORLD_SIZE"] = base["LOCAL_WORLD_SIZE"] = str(n)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen(cmd, env=e))
+    first_bad, t_bad = 0, None
+
+    def _forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        raise SystemExit(128 + signum)
+    old = signal.signal(signal.SIGTERM, _forward)
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            for c in codes:
+                if c not in (None, 0) and first_bad == 0:
+                    first_bad, t_bad = c, time.monotonic()
+            if all(c is not None for c in codes):
+                break
+            if t_bad is not None and time.monotonic() - t_bad > grace_s:
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                t_bad = float("inf")
+                deadline = time.monotonic() + 10.0
+                while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+                    time.sleep(poll_s)
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+            time.sleep(poll_s)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    if first_bad < 0:                       # killed by a signal: report it the way a shell does
+        first_bad = 128 - first_bad
+    return first_bad
+
+
+def self_launch(n):
+    """bench.py --gpus n > 1 without torchrun: n fresh ranks of this script, started before this process makes
+    any GPU call (torch.cuda.device_count() does not initialise the runtime on this image)."""
+    visible = torch.cuda.device_count()
+    if visible < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {visible} HIP device(s) visible; one rank per GPU needs {n}")
+    return launch_ranks(n, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(self_launch(args.gpus))
+        if args.gpus < 1:
+            raise SystemExit(f"--gpus {args.gpus}: need at least one GPU")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU, the two must agree")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
