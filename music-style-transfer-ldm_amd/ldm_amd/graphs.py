@@ -10,7 +10,16 @@ therefore raced the watchdog: when a pass fell inside the capture window the eve
 WorkNCCL rethrew, the watchdog thread died and, with TORCH_NCCL_ASYNC_ERROR_HANDLING=3 (the default), took
 the process down from a thread with no Python frame — after the capture, e.g. during the first replays
 (round 3's intermittent abort).  In thread-local mode only the capturing thread is
-restricted, which is all the capture needs: nothing on this path calls the runtime from another thread.
+restricted.  Note that the backward of a captured train step runs on autograd's device worker thread, not on the
+capturing thread: in thread-local mode that thread is not checked for unsafe calls (a hidden synchronisation or
+legacy-stream call in a backward function would run at capture time and be missing from the replays instead of
+failing the capture).  The guard for that is tests/test_gpu_train.py's capture of the whole train step in the
+global mode (LDM_AMD_CAPTURE_MODE=global; no RCCL watchdog is alive there), which must succeed and replay
+equal to the eager step.
+
+Side streams (branch(), the pool of prepare_streams) are recorded per capture: capture() joins every pool
+stream that took part in the capture back into the origin stream before the capture ends, so no captured work
+is left outside the graph's sink whatever order autograd ran the branches in.
 """
 import contextlib
 import os
@@ -20,9 +29,36 @@ import torch
 CAPTURE_MODE = "thread_local"
 
 
+def capture_mode():
+    """The capture mode of capture(): thread_local, or LDM_AMD_CAPTURE_MODE (global / relaxed / thread_local)."""
+    return os.environ.get("LDM_AMD_CAPTURE_MODE", CAPTURE_MODE)
+
+
+_CAPTURES = []   # per capture in progress: (origin stream, set of pool streams that joined it)
+
+
+@contextlib.contextmanager
 def capture(graph, stream=None, pool=None):
-    """Context manager: capture into `graph` (torch.cuda.CUDAGraph) on `stream`, thread-local mode."""
-    return torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=CAPTURE_MODE)
+    """Context manager: capture into `graph` (torch.cuda.CUDAGraph) on `stream` (capture_mode()).  Before the
+    capture ends, the origin stream waits on every branch stream that forked from it during the capture."""
+    with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=capture_mode()):
+        origin = torch.cuda.current_stream()
+        rec = (origin, {})
+        _CAPTURES.append(rec)
+        ok = False
+        try:
+            yield
+            ok = True
+        finally:
+            _CAPTURES.pop()
+            if ok:
+                for side in rec[1].values():
+                    origin.wait_stream(side)
+
+
+def captured_side_streams():
+    """The branch streams recorded by the innermost capture in progress (for tests / assertions)."""
+    return list(_CAPTURES[-1][1].values()) if _CAPTURES else []
 
 
 _BRANCH_STREAMS = {}
@@ -89,6 +125,8 @@ def branch(device, name):
         yield None
         return
     side.wait_stream(main)
+    if _CAPTURES and torch.cuda.is_current_stream_capturing():
+        _CAPTURES[-1][1][side.cuda_stream] = side
     with torch.cuda.stream(side):
         yield side
 

@@ -341,6 +341,13 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
     plan = plan or get_plan(desc)
     wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
     st = conv_storage16(desc, plan, dt)
+    if st and plan.kind == 0 and (bcast is not None or skip is not None or
+                                  (out is not None and out.data_ptr() % 16) or
+                                  (act_out is not None and act_out.data_ptr() % 16)):
+        # the VALU convs that take 16-bit maps (Cin = 1 stride 2: y; 64 -> 1 k4 s2 convT: x) run only with a
+        # simple epilogue and 16-byte aligned y / act_out (conv.hip conv_forward_ex); any other call of those
+        # shapes takes the general direct kernel with fp32 maps
+        st = 0
     x, xh = in16(x, dt, st & L.DT_X16)
     y16 = out is None and act_out is None and T16.get(out_dtype) == dt and bool(st & L.DT_Y16)
     y = out if out is not None else torch.empty((B, Cout, desc.Hout, desc.Wout), device=x.device,

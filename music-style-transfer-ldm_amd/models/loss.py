@@ -35,18 +35,12 @@ _PERCEPTUAL_BACKEND = None
 _WARNED = set()
 
 
-_ZEROS = {}
-
-
 def _const_zero(device):
-    """The 0-d zero an absent offline term returns: one cached tensor per device, marked so that the sums
+    """The 0-d zero an absent offline term returns: a new tensor on every call, as the reference's
+    torch.zeros, so a caller's in-place update of it reaches no later call; it is marked so that the sums
     below skip adding it (x + w * 0 == x for every finite x: the same value, two fewer launches per use)."""
-    key = str(device)
-    z = _ZEROS.get(key)
-    if z is None:
-        z = torch.zeros((), device=device, dtype=torch.float32)
-        z._ldm_const_zero = True
-        _ZEROS[key] = z
+    z = torch.zeros((), device=device, dtype=torch.float32)
+    z._ldm_const_zero = True
     return z
 
 

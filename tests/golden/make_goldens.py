@@ -6,6 +6,7 @@
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --amp8   # ref_goldens_amp8.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --vggish # ref_goldens_vggish.npz
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --r3     # ref_goldens_r3.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py --fp16train   # ref_goldens_fp16.npz
 
 Imports /root/reference/models/model.py and loss.py with two absent, unused-on-this-path imports
 stubbed (``pytorch_lightning`` at model.py:4 and ``lpips`` at loss.py:3) and with
@@ -517,6 +518,88 @@ def round3():
     print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
 
 
+def fp16train():
+    """(13) The reference's DEFAULT train-step precision -> ref_goldens_fp16.npz: LDMTrainer.train_step
+    (train.py:163-208) with its own torch.autocast region (device default: float16 on a GPU, train.py:174) and
+    its GradScaler (train.py:157, :189-201; init scale 2^16, growth 2, backoff 0.5, interval 2000), Adam(lr=1e-4)
+    (LDMTrainer default), at config 3's shape and inputs (r3_inputs: batch 32, 1x128x512, recipe seed 700,
+    every module in train mode, q_sample noise injected).  On the CPU the region is torch.autocast("cpu",
+    float16) and the scaler torch.amp.GradScaler("cpu") (same defaults and the same unscale / inf-check / update
+    arithmetic as 'cuda').  Loss = compression (MSE + 0.01 KL; LPIPS left out, remote weights) + diffusion +
+    0.1 x style (VGGish stubbed to 0), as the reference adds them.
+
+    Two steps: (A) at the default scale 2^16 -- loss terms, reconstructed samples 0 / 31, the unscaled
+    TRAIN_GRAD_KEYS gradients, whether the scaler found an inf, the scale after update(); (B) the scale set
+    to 2^40 with update(new_scale=...) first, so the fp16 backward overflows: found-inf, the step skipped
+    (parameters and Adam state untouched), the scale backed off to 2^39."""
+    torch.set_num_threads(8)
+    M, L = import_reference()
+    G = {}
+    content, style, t, noise = r3_inputs()
+    ldm = M.LDM(32, pretrained_path="")
+    recipe.fill_module(ldm, seed=700)
+    ldm.train()
+    trainable = [p for p in ldm.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(trainable, lr=1e-4)
+    scaler = torch.amp.GradScaler("cpu")
+    named = dict(ldm.named_parameters())
+
+    def train_step():
+        opt.zero_grad()
+        real_randn_like = torch.randn_like
+        torch.randn_like = lambda x, *a, **k: noise.clone()
+        try:
+            with torch.autocast("cpu", dtype=torch.float16):
+                out = ldm(content.float(), style.float(), t)
+            # the loss terms with CUDA autocast's semantics: mse_loss, pow and log are on its fp32 list (their
+            # 16-bit inputs cast to fp32), so on a GPU the reference computes every term below in fp32.  CPU
+            # autocast keeps pow / log in fp16, where KL's + 1e-8 underflows to 0 and log(0) makes the loss inf,
+            # which the reference on a GPU never sees: the terms are taken on the fp32 casts instead.
+            dl = L.diffusion_loss(out["noise_pred"].float(), out["noise"].float())
+            mse = torch.nn.MSELoss()(out["reconstructed"].float(), content)
+            kl = L.kl_regularization_loss(out["z_0"].float())
+            comp = mse + 0.01 * kl
+            style_l = torch.zeros(())
+            total = comp + dl + 0.1 * style_l
+        finally:
+            torch.randn_like = real_randn_like
+        scaler.scale(total).backward()
+        scaler.step(opt)
+        found = float(sum(v.item() for v in scaler._found_inf_per_device(opt).values()))
+        scaler.update()
+        return out, comp, dl, total, found
+
+    before = {k: named[k].detach().clone() for k in TRAIN_GRAD_KEYS}
+    out, comp, dl, total, found = train_step()
+    G["fp16_a_found_inf"] = np.float32(found)
+    G["fp16_a_scale_after"] = np.float32(scaler.get_scale())
+    G["fp16_compression"] = np32(comp.float())
+    G["fp16_diffusion"] = np32(dl.float())
+    G["fp16_total"] = np32(total.float())
+    G["fp16_recon_0_31"] = np32(out["reconstructed"].float()[[0, R3_B - 1]])
+    for k in TRAIN_GRAD_KEYS:
+        g = named[k].grad
+        G["fp16_grad_" + k] = np32(g[:256] if g.dim() == 2 and g.shape[0] > 256 else g)
+    G["fp16_a_param_moved"] = np.array([float((named[k].detach() - before[k]).abs().max()) for k in TRAIN_GRAD_KEYS],
+                                       dtype=np.float32)
+    print("step A: compression", float(comp), "diffusion", float(dl), "total", float(total), "found_inf", found, "scale after", scaler.get_scale(), flush=True)
+    snap = {k: named[k].detach().clone() for k in TRAIN_GRAD_KEYS}
+    steps = [opt.state[named[k]]["step"].clone() if named[k] in opt.state else None for k in TRAIN_GRAD_KEYS]
+    scaler.update(new_scale=2.0 ** 40)
+    out, comp, dl, total, found = train_step()
+    G["fp16_b_found_inf"] = np.float32(found)
+    G["fp16_b_scale_after"] = np.float32(scaler.get_scale())
+    G["fp16_b_total"] = np32(total.float())
+    G["fp16_b_params_unchanged"] = np.float32(all(torch.equal(named[k], snap[k]) for k in TRAIN_GRAD_KEYS))
+    G["fp16_b_adam_step_unchanged"] = np.float32(all(
+        s is None or torch.equal(opt.state[named[k]]["step"], s) for k, s in zip(TRAIN_GRAD_KEYS, steps)))
+    print("step B: total", float(total), "found_inf", found, "scale after", scaler.get_scale(),
+          "params unchanged", bool(G["fp16_b_params_unchanged"]), flush=True)
+    path = os.path.join(HERE, "ref_goldens_fp16.npz")
+    np.savez_compressed(path, **G)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(G), "arrays")
+
+
 TRAIN_GRAD_KEYS = ("unet.time_mlp.1.weight", "unet.dec1.weight", "unet.dec1.bias", "unet.enc1.weight",
                    "unet.cross_attention1.multihead_attn.in_proj_weight", "unet.bottleneck.bias",
                    "decoder.decoder.6.weight", "decoder.decoder.1.weight", "style_encoder.enc6.bias",
@@ -528,7 +611,9 @@ AE_KEYS = ("encoder.encoder.0.weight", "encoder.encoder.1.weight", "encoder.enco
 
 
 if __name__ == "__main__":
-    if "--r2" in sys.argv:
+    if "--fp16train" in sys.argv:
+        fp16train()
+    elif "--r2" in sys.argv:
         round2()
     elif "--r3" in sys.argv:
         round3()

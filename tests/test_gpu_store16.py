@@ -105,6 +105,33 @@ def test_cin1_and_cout1_store16(cuda, k):
                        ops.conv_backward_weight(h32.to(cuda), r, d2, dtype=dt))
 
 
+def test_cin1_cout1_with_skip_fall_back_to_fp32_maps(cuda):
+    """The 16-bit VALU convs run only with a simple epilogue: a Cin = 1 stride-2 conv asked for a 16-bit output
+    with a skip / broadcast add, and the 64 -> 1 convT handed a 16-bit input with a skip, take the general kernel
+    on fp32 maps (an fp32 y) instead of failing, with the same values as the all-fp32 call."""
+    from ldm_amd import ops
+    dt = 2
+    x = _rand((4, 1, 64, 256), 51).to(cuda)
+    w1 = _rand((64, 1, 3, 3), 52, -0.3, 0.3).to(cuda)
+    b1 = _rand((64,), 53, -0.1, 0.1).to(cuda)
+    sk = _rand((4, 64, 32, 128), 54).to(cuda)
+    bc = _rand((4, 64), 55).to(cuda)
+    kw = dict(stride=2, padding=1, act="relu", dtype=dt)
+    for extra in (dict(skip=sk), dict(bcast=bc)):
+        ref = ops.conv_forward(x, w1, b1, **kw, **extra)
+        got = ops.conv_forward(x, w1, b1, out_dtype=T[dt], **kw, **extra)
+        torch.cuda.synchronize()
+        assert got.dtype == torch.float32 and torch.equal(got, ref)
+    h16, h32 = _q(_rand((4, 64, 32, 128), 56, 0.0, 1.0), dt)
+    w2 = _rand((64, 1, 4, 4), 57, -0.2, 0.2).to(cuda)
+    sk2 = _rand((4, 1, 64, 256), 58).to(cuda)
+    kt = dict(stride=2, padding=1, transposed=True, act="tanh", dtype=dt, skip=sk2)
+    ref = ops.conv_forward(h32.to(cuda), w2, None, **kt)
+    got = ops.conv_forward(h16.to(cuda), w2, None, **kt)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 class _StubGroup:
     """A world-1 stand-in for a SyncBatchNorm group: the two-stage kernels with an identity all-reduce."""
 

@@ -324,14 +324,20 @@ def test_second_step_uses_updated_weights(cuda):
         assert abs(l2[k] - l1b[k]) <= 1e-5 * abs(l1b[k]), (k, l2[k], l1b[k])
 
 
-@pytest.mark.parametrize("autocast", [False, True])
-def test_graphed_train_step_equals_eager(cuda, autocast):
+@pytest.mark.parametrize("autocast,mode", [(False, "thread_local"), (True, "thread_local"), (True, "global")])
+def test_graphed_train_step_equals_eager(cuda, autocast, mode, monkeypatch):
     """LDMTrainer.graph_step: 2 eager warm-up steps, then the step captured into a hipGraph and replayed.
     With injected t / noise the eight steps' losses and the final parameters and BN buffers equal an eager
     trainer's bitwise (same kernels; the capturable Adam forms its scalars from the device step count
-    exactly as the host form does); under autocast too; a learning-rate change after step 5 re-captures."""
+    exactly as the host form does); under autocast too; a learning-rate change after step 5 re-captures.
+    mode "global": the capture in the global capture mode, in which an unsafe runtime call from ANY thread --
+    the backward runs on autograd's device thread -- fails the capture instead of running at capture time and
+    missing from the replays (the product captures in the thread-local mode, ldm_amd/graphs.py)."""
     import models.model as M
     import models.train as TR
+    from ldm_amd import graphs as hgraphs
+    monkeypatch.setenv("LDM_AMD_CAPTURE_MODE", mode)
+    assert hgraphs.capture_mode() == mode
     content = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 860)).to(cuda)
     style = torch.from_numpy(recipe.uniform01((2, 1, 128, 128), 861)).to(cuda)
     t = torch.tensor([10, 150], device=cuda)
