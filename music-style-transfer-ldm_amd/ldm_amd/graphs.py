@@ -20,6 +20,13 @@ equal to the eager step.
 Side streams (branch(), the pool of prepare_streams) are recorded per capture: capture() joins every pool
 stream that took part in the capture back into the origin stream before the capture ends, so no captured work
 is left outside the graph's sink whatever order autograd ran the branches in.
+
+Only the capture's ORIGIN stream forks.  A fork from a stream that is itself a forked capture stream (origin M
+forks S, S forks W; W joins S, S joins M) segfaults the HIP runtime in hipStreamEndCapture on ROCm 7.2, from the
+capturing thread alone, without autograd (tools/capture_nest_repro.py; the same pattern inside a backward,
+tools/capture_wgrad_repro.py): that was round 4's crash of the per-conv weight-gradient side stream, whose
+backward nodes of the style-encoder branch forked from the branch stream.  branch() therefore runs its block in
+place when the current stream is a capture stream other than the origin.
 """
 import contextlib
 import os
@@ -120,12 +127,16 @@ def branch(device, name):
         yield None
         return
     main = torch.cuda.current_stream(torch.device(device))
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing and _CAPTURES and main.cuda_stream != _CAPTURES[-1][0].cuda_stream:
+        yield None          # never fork from a forked capture stream (the runtime crashes at capture end)
+        return
     side = branch_stream(device, name)
     if side is None or side.cuda_stream == main.cuda_stream:
         yield None
         return
     side.wait_stream(main)
-    if _CAPTURES and torch.cuda.is_current_stream_capturing():
+    if _CAPTURES and capturing:
         _CAPTURES[-1][1][side.cuda_stream] = side
     with torch.cuda.stream(side):
         yield side

@@ -76,6 +76,12 @@ def test_config3_graphed_step_matches_reference(g3, cuda, dtype, monkeypatch):
     if dtype == "fp32":
         monkeypatch.setenv("LDM_AMD_DTYPE", "fp32")
     m, tr = _bench_trainer(cuda, dtype)
+    check_graphed_step(g3, cuda, dtype, m, tr)
+
+
+def check_graphed_step(g3, cuda, dtype, m, tr):
+    """Two warm-up steps at lr = 0, then the captured step replayed at lr = 1e-4, checked against the
+    reference's config-3 step (ref_goldens_r3.npz) and float64 Adam (see the module docstring)."""
     content, style, t, noise = _inputs(cuda)
     assert np.array_equal(t.cpu().numpy(), g3["r3_t"])
     lr = 1e-4

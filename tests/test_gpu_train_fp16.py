@@ -9,8 +9,9 @@ lr = 0, so the weights stay the recipe's, then the captured step replayed).
 
 Step A (scale 2^16): the reference finds no inf; ours must not either, the scale stays 2^16, and the loss
 terms, reconstructed samples 0 / 31 and the ten TRAIN_GRAD_KEYS gradients (unscaled) agree with the reference's
-fp16 step by the rule of test_gpu_amp.py: per quantity within 2 e + 1e-3 of both the fp16 and the fp32
-reference (e = the reference's own fp16-vs-fp32 distance, ref_goldens_r3.npz r3_fp32_*); the Adam update is
+fp16 step by the rule of test_gpu_train_config3.py's bf16 case: per quantity within 1.5 e + 1e-4 of the fp16
+reference and 2 e + 1e-4 of the fp32 one (e = the reference's own fp16-vs-fp32 distance, ref_goldens_r3.npz
+r3_fp32_*; measured on MI355X: every quantity within 1.48 e of the fp16 reference); the Adam update is
 checked against float64 Adam on our own gradients from the moments before the step.
 Step B (the scale set to 2^40 first, update(new_scale=...) as on torch's scaler): the fp16 backward overflows
 in the reference; ours must find the inf too, skip the step (parameters and Adam moments / step count bitwise
@@ -108,7 +109,7 @@ def test_default_fp16_gradscaler_step_matches_reference(gf, g3, cuda, graph):
         e = rel_err(f16, f32)
         to32, to16 = rel_err(ours, f32), rel_err(ours, f16)
         rows.append(f"{name}: ref fp16-vs-fp32 {e:.2e}, ours-vs-fp32 {to32:.2e}, ours-vs-fp16 {to16:.2e}")
-        if to32 > 2 * e + 1e-3 or to16 > 2 * e + 1e-3:
+        if to32 > 2 * e + 1e-4 or to16 > 1.5 * e + 1e-4:
             bad.append(name)
     print("\n".join(rows))
     assert not bad, (bad, rows)
