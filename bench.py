@@ -134,7 +134,25 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
     shape = engine.shape(B, 32, H, W)
     w = engine.weights(shape)
     out = {}
+    # the bottleneck on CA1's folded values (bfold.hip) replaces CA1's P V and the uconv bottleneck in the loop
+    bfold = int(w.use_step) != 0 and bool(lib.ldm_bneck_fold_supported(B, H, W))
     for layer, (name, cin, cout, mode, div) in enumerate(STEP_LAYERS):
+        if bfold and name == "bottleneck":
+            u = torch.randn(B, 512, 576, device=dev)
+            pr = torch.softmax(torch.randn(B, 4, 16, 16, device=dev), -1).contiguous()
+            pbias = torch.randn(16, 512, device=dev)
+            yb = torch.empty(B, 16, 512, device=dev)
+            dt = int(w.step_dtype)
+            fn = lambda: lib.ldm_bneck_pv(u.data_ptr(), pr.data_ptr(), pbias.data_ptr(), yb.data_ptr(), B, dt,  # noqa: E731
+                                          torch.cuda.current_stream().cuda_stream)
+            L.check(fn(), name)
+            us = _graph_time_us(fn, reps)
+            fl = 2.0 * B * 16 * 512 * 576
+            by = 4.0 * (B * 512 * 576 + B * 4 * 256 + 16 * 512 + B * 16 * 512)
+            out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
+                         "flops": fl, "bytes": by, "bound": "hbm",
+                         "kernel": "bneck_pv_kernel (CA1 values folded into the bottleneck, K = 576 per sample)"}
+            continue
         hin, win = H // div, W // div
         hout, wout = (hin, win) if mode == 0 else ((hin // 2, win // 2) if mode == 1 else (2 * hin, 2 * win))
         x = torch.randn(B, hin, win, cin, device=dev)
@@ -164,20 +182,29 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
                      "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else
                                                           ("uconv_kernel (K split)" if layer in KS_LAYERS else "uconv_kernel"))
                      + ("" if dt == 0 else (" fp16 operands" if dt == 1 else " bf16 operands"))}
-    # the folded cross-attentions of the loop
+    # the folded cross-attentions of the loop (CA1: its probabilities only when the bottleneck takes the values)
     for name, E, Lt in (("attn2_folded", 256, H * W // 16), ("attn1_folded", 512, H * W // 64)):
         z = torch.randn(B, Lt, E, device=dev)
         kv = torch.randn(B, 2 * E, Lt, device=dev)
         kf = torch.randn(B, 4, Lt, E, device=dev)
         bf = torch.randn(B, 4, Lt, device=dev)
         o = torch.empty(B, Lt, E, device=dev)
-        us = _graph_time_us(lambda: lib.ldm_attention_folded(z.data_ptr(), kv.data_ptr(), kf.data_ptr(), bf.data_ptr(),
-                                                             o.data_ptr(), B, E, 4, Lt, Lt,
-                                                             torch.cuda.current_stream().cuda_stream), reps)
-        fl = 2.0 * B * 4 * Lt * Lt * E + 2.0 * B * E * Lt * Lt
-        by = 4.0 * B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
+        probs = bfold and name == "attn1_folded"
+        if probs:
+            us = _graph_time_us(lambda: lib.ldm_attention_folded_probs(z.data_ptr(), kf.data_ptr(), bf.data_ptr(),
+                                                                       o.data_ptr(), B, E, 4, Lt, Lt,
+                                                                       torch.cuda.current_stream().cuda_stream), reps)
+            fl = 2.0 * B * 4 * Lt * Lt * E
+            by = 4.0 * B * (Lt * E + 4 * E * Lt + 4 * Lt * Lt)
+        else:
+            us = _graph_time_us(lambda: lib.ldm_attention_folded(z.data_ptr(), kv.data_ptr(), kf.data_ptr(),
+                                                                 bf.data_ptr(), o.data_ptr(), B, E, 4, Lt, Lt,
+                                                                 torch.cuda.current_stream().cuda_stream), reps)
+            fl = 2.0 * B * 4 * Lt * Lt * E + 2.0 * B * E * Lt * Lt
+            by = 4.0 * B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "kernel": "attention_mfma_kernel (folded)"}
+                     "flops": fl, "bytes": by, "bound": "hbm",
+                     "kernel": "attention_mfma_kernel (folded" + (", probabilities only)" if probs else ")")}
     return out
 
 
@@ -594,7 +621,7 @@ def main():
     if rank == 0 and not args.no_kernel_timing:
         with torch.no_grad():
             kt = time_step_layers(eng, B, 16, 64, dev)
-        dom = max(kt, key=lambda k: kt[k]["us"])      # the longest launch of the step (the bottleneck conv)
+        dom = max(kt, key=lambda k: kt[k]["us"])      # the longest launch of the step
         dk = kt[dom]
         traffic = None
         if os.path.exists(args.pmc):
@@ -607,10 +634,16 @@ def main():
         peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
         if args.dtype != "fp32":
             traffic = None     # profiles/r04/pmc_traffic_step.json holds the fp32 kernels' counters
-        result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
-                              "achieved": dk["tflops"], "peak": peak, "unit": "TFLOP/s",
-                              "frac": round(dk["tflops"] / peak, 4), "traffic": traffic,
-                              "flops_per_launch": dk["flops"], "avg_launch_us": dk["us"]}
+        if dk.get("bound") == "hbm":   # a byte-bound launch (the folded-value bottleneck, the attentions)
+            result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "hbm",
+                                  "achieved": dk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(dk["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                  "bytes_per_launch": dk["bytes"], "avg_launch_us": dk["us"]}
+        else:
+            result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "mfma",
+                                  "achieved": dk["tflops"], "peak": peak, "unit": "TFLOP/s",
+                                  "frac": round(dk["tflops"] / peak, 4), "traffic": traffic,
+                                  "flops_per_launch": dk["flops"], "avg_launch_us": dk["us"]}
         result["kernels"] = {k: {kk: vv for kk, vv in v.items() if kk not in ("flops", "bytes")} for k, v in kt.items()}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

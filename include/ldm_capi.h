@@ -194,6 +194,22 @@ int ldm_attention_fold_keys(const float* kv, const float* wq, const float* bq, i
                             int32_t S, float scale, float* kf, float* bf, void* stream);
 int ldm_attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out, int32_t B,
                          int32_t E, int32_t heads, int32_t L, int32_t S, void* stream);
+/* The folded attention's probabilities only: p [B,heads,L,S] = softmax(z^T kf_h + bf_h) (CA1's instance: E 512,
+ * 4 heads, L, S <= 16).  The reverse loop's bottleneck then contracts them with its folded values (below). */
+int ldm_attention_folded_probs(const float* z, const float* kf, const float* bf, float* p, int32_t B, int32_t E,
+                               int32_t heads, int32_t L, int32_t S, void* stream);
+/* The bottleneck after CA1 with the attention's values folded into its weights (bfold.hip; model.py:214-217):
+ * u [B,512,576] = W' (x) V once per loop, u[b][co][(t*4 + h)*16 + s] = sum_d w_fold[co][h*128 + d][t] *
+ * kv[b][512 + h*128 + d][s] (w_fold = the bottleneck o out-projection fold of ldm_fold_conv_proj, torch layout
+ * [512,512,3,3]; kv the CA1 K/V projection [B,1024,16]); then per step y [B,2,8,512] (NHWC) = relu(sum over
+ * (t, h, s) of u * p[b][h][l_t][s] + pos_bias[l][co]) with pos_bias [16][512] (position-major) and p from
+ * ldm_attention_folded_probs.  dtype LDM_DT_F16 / _BF16 rounds the output to that type (operands stay fp32).
+ * Used by ldm_ddim_sample when ldm_bneck_fold_supported(B, H, W): the canonical 16 x 64 latent, B <= 8
+ * (LDM_BNECK_FOLD=0 turns it off). */
+int32_t ldm_bneck_fold_supported(int32_t B, int32_t H, int32_t W);
+int ldm_bneck_fold_values(const float* w_fold, const float* kv, float* u, int32_t B, void* stream);
+int ldm_bneck_pv(const float* u, const float* p, const float* pos_bias, float* y, int32_t B, int32_t dtype,
+                 void* stream);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that
@@ -282,6 +298,10 @@ typedef struct ldm_unet_weights {
     const float* step_pb[2];
     int32_t use_step;
     int32_t step_dtype;   /* LDM_DT_*: operand precision of the step kernels (not F32: uconv.hip only) */
+    /* The bottleneck o CA1 out-projection fold in the torch layout [512,512,3,3] (ldm_fold_conv_proj's w_out,
+     * unpacked): the source of the folded values U when the loop runs the bottleneck on them
+     * (ldm_bneck_fold_supported; ldm_bneck_fold_values).  NULL: the uconv bottleneck. */
+    const float* step_bneck_w;
 } ldm_unet_weights;
 
 typedef struct ldm_unet_shape {

@@ -206,6 +206,12 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
                      int32_t E, int32_t heads, int32_t L, int32_t S, hipStream_t st);
 int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
                         int32_t S, float scale, float* kf, float* bf, hipStream_t st);
+int attention_folded_probs(const float* z, const float* kf, const float* bf, float* p, int32_t B, int32_t E,
+                           int32_t heads, int32_t L, int32_t S, hipStream_t st);
+// bfold.hip: the reverse loop's bottleneck with CA1's values folded into its weights (U, once per loop)
+bool bneck_fold_supported(int B, int H, int W);
+int bneck_fold_values(const float* wf, const float* kv, float* u, int B, hipStream_t st);
+int bneck_pv(const float* u, const float* p, const float* pb, float* y, int B, int dtype, hipStream_t st);
 
 // uconv.hip: the step kernels of the reverse loop (NHWC activations, see ldm_capi.h)
 struct StepConv {

@@ -156,7 +156,9 @@ struct AMfma<2> {
 // the scores are z^T kf[b,h] + bf[b,h] with kf [B,heads,S,E] = scale*Wq_h^T K_h and bf [B,heads,S] =
 // scale*bq_h^T K_h (ldm_attention_fold_keys) — the same scores as ((Wq z + bq)*scale)^T K re-associated,
 // so the Q in-projection needs no launch of its own.
-template <int KIND, int LP, int SP, int D, int LT, bool TOK, int EQ = 0, int NW = 4>
+// PONLY (folded instances): stop after the softmax and write the probabilities P [B, heads, L, S] (S fastest) to
+// `out` instead of P V — the bottleneck after CA1 contracts P with values folded into its weights (bfold.hip).
+template <int KIND, int LP, int SP, int D, int LT, bool TOK, int EQ = 0, int NW = 4, bool PONLY = false>
 __global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                              float* __restrict__ out, int E, int heads, int L, int S,
                                                              float scale, const float* __restrict__ kf = nullptr,
@@ -189,7 +191,8 @@ __global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __
     const float* vb = kv + ((size_t)b * 2 * E + E + (size_t)h * D) * S;
 
     // stage V [D][S] -> LDS [D][SP+1]: every load of this thread issues before any LDS store
-    if (S == SP && (D * SP) % (256 * NW) == 0 && D * SP >= 256 * NW) {   // full rows: 16-byte loads
+    if constexpr (PONLY) {
+    } else if (S == SP && (D * SP) % (256 * NW) == 0 && D * SP >= 256 * NW) {   // full rows: 16-byte loads
         constexpr int NV4 = D * SP >= 256 * NW ? D * SP / (256 * NW) : 1;
         float4 v[NV4];
 #pragma unroll
@@ -339,6 +342,14 @@ __global__ __launch_bounds__(64 * NW) void attention_mfma_kernel(const float* __
         }
     }
     __syncthreads();
+    if constexpr (PONLY) {
+        float* pb = out + ((size_t)(b * heads + h) * L + l0) * S;
+        for (int e = threadIdx.x; e < LT * SP; e += 64 * NW) {
+            const int r = e / SP, s = e % SP;
+            if (l0 + r < L && s < S) pb[(size_t)r * S + s] = Ps[r * LDP + s];
+        }
+        return;
+    }
     // O[c][l] = sum_s V[c][s] P[l][s]
     constexpr int NTC = D / TILE;
     float* ob = TOK ? out + (size_t)b * L * E + (size_t)h * D : out + ((size_t)b * E + (size_t)h * D) * L;
@@ -737,6 +748,20 @@ int attention_folded(const float* z, const float* kv, const float* kf, const flo
     return fail(3, "attention (folded): no instance for this shape");
 }
 
+// The probabilities of the folded cross-attention only (P [B, heads, L, S]): the CA1 instance of
+// attention_folded without its P V product.
+int attention_folded_probs(const float* z, const float* kf, const float* bf, float* p, int32_t B, int32_t E,
+                           int32_t heads, int32_t L, int32_t S, hipStream_t st) {
+    LDM_REQUIRE(z && kf && bf && p, "attention probs (folded): null argument");
+    LDM_REQUIRE(B > 0 && heads == 4 && E == 512 && L > 0 && L <= 16 && S > 0 && S <= 16,
+                "attention probs (folded): instances for CA1's 2 x 8 plane only (E 512, L, S <= 16)");
+    auto kfn = attention_mfma_kernel<2, 16, 16, 128, 16, true, 512, 8, true>;
+    const size_t lds = ((size_t)8 * 16 * 17 + (size_t)128 * 17) * sizeof(float);
+    hipLaunchKernelGGL(kfn, dim3(B * heads), dim3(64 * 8), lds, st, z, kf, p, E, heads, L, S, 1.0f, kf, bf);   // (kv unread)
+    LDM_CHECK_LAUNCH("attention_mfma_kernel (folded, probabilities)");
+    return 0;
+}
+
 int attention_fold_keys(const float* kv, const float* wq, const float* bq, int32_t B, int32_t E, int32_t heads,
                         int32_t S, float scale, float* kf, float* bf, hipStream_t st) {
     LDM_REQUIRE(kv && wq && bq && kf && bf && B > 0 && heads > 0 && E % heads == 0 && S > 0, "fold keys: bad argument");
@@ -905,6 +930,11 @@ extern "C" int ldm_attention_fold_keys(const float* kv, const float* wq, const f
 extern "C" int ldm_attention_folded(const float* z, const float* kv, const float* kf, const float* bf, float* out,
                                     int32_t B, int32_t E, int32_t heads, int32_t L, int32_t S, void* stream) {
     return ldm::attention_folded(z, kv, kf, bf, out, B, E, heads, L, S, (hipStream_t)stream);
+}
+
+extern "C" int ldm_attention_folded_probs(const float* z, const float* kf, const float* bf, float* p, int32_t B,
+                                          int32_t E, int32_t heads, int32_t L, int32_t S, void* stream) {
+    return ldm::attention_folded_probs(z, kf, bf, p, B, E, heads, L, S, (hipStream_t)stream);
 }
 
 extern "C" int ldm_fold_conv_proj(const ldm_conv_desc* d, const float* w_conv, const float* b_conv, const float* w_proj,

@@ -98,6 +98,7 @@ struct UNetWs {
     float* xs;                      // the sampler state in NHWC (reverse loop with the step kernels)
     float* ustep;                   // split-K counters + slabs of the LDS-staged step kernels (zero-filled)
     float* uks;                     // split-K counters + slabs of the K-split step kernels (uconv.hip)
+    float *ubn, *p1;                // the bottleneck's folded values U and CA1's probabilities (bfold.hip)
     int64_t total;
 };
 
@@ -159,6 +160,12 @@ static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* 
     return m;
 }
 
+// The reverse loop's bottleneck on CA1's folded values (bfold.hip) at the canonical plane, B <= 8.
+static bool use_bneck_fold(const ldm_unet_shape& s, const ldm_unet_weights* w) {
+    return w && w->use_fold && w->use_step && w->step_bneck_w && s.C == 32 && s.nf == 64 &&
+           bneck_fold_supported(s.B, s.H, s.W);
+}
+
 static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float* base) {
     const int64_t B = s.B, nf = s.nf, HW = (int64_t)s.H * s.W;
     const int64_t HW2 = HW / 4, L2 = HW / 16, L1 = HW / 64;
@@ -195,6 +202,9 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.xs = take(B * (int64_t)s.C * HW);
     w.ustep = take(ustep_ws_floats(s, wts));
     w.uks = take(wts && wts->use_step ? step_ws_floats(s.B, s.H, s.W) : 0);
+    const bool bfold = use_bneck_fold(s, wts);
+    w.ubn = take(bfold ? B * 512 * 576 : 0);
+    w.p1 = take(bfold ? B * 4 * L1 * L1 : 0);
     w.total = off;
     return w;
 }
@@ -356,6 +366,12 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     LDM_TRY(run(0, 2));
     LDM_TRY(attention_folded(ws.z3, ws.kv2, ws.kf2, ws.bf2, ws.a2, s.B, 256, 4, L2, L2, st));
     LDM_TRY(run(3, 3));
+    if (use_bneck_fold(s, &w)) {
+        // CA1's probabilities, then the bottleneck on its folded values U (formed before the loop)
+        LDM_TRY(attention_folded_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, 512, 4, L1, L1, st));
+        LDM_TRY(bneck_pv(ws.ubn, ws.p1, w.step_pb[1], ws.zb, s.B, w.step_dtype, st));
+        return run(5, 8);
+    }
     LDM_TRY(attention_folded(ws.z4, ws.kv1, ws.kf1, ws.bf1, ws.a1, s.B, 512, 4, L1, L1, st));
     return run(4, 8);
 }
@@ -443,6 +459,7 @@ extern "C" int ldm_ddim_sample(const ldm_unet_shape* s, const ldm_unet_weights* 
             for (int l = 0; l < 9; ++l) LDM_REQUIRE(w->step_w[l], "ddim_sample: use_step needs the step weights");
             LDM_REQUIRE(w->step_pb[0] && w->step_pb[1], "ddim_sample: use_step needs the folded biases");
             LDM_REQUIRE(w->step_dtype >= LDM_DT_F32 && w->step_dtype <= LDM_DT_BF16, "ddim_sample: step_dtype");
+            if (use_bneck_fold(*s, w)) LDM_TRY(bneck_fold_values(w->step_bneck_w, ws.kv1, ws.ubn, s->B, st));
             LDM_TRY(step_layout(x, ws.xs, s->B, s->C, HW, true, st));
             for (int i = 0; i < nsteps; ++i) {
                 DdimFuse fuse{coef_table + 4 * (size_t)i, eta, ws.xs, x0_logs ? x0_logs + (size_t)i * n : nullptr,

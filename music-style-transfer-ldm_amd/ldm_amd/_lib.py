@@ -57,7 +57,7 @@ class UNetWeights(ctypes.Structure):
                 ("t_freqs", c_fp), ("t_w1", c_fp), ("t_b1", c_fp), ("t_w2", c_fp), ("t_b2", c_fp),
                 ("ca_wq_raw", c_fp * 2), ("fold_w", c_fp * 2), ("fold_pb", c_fp * 2), ("use_fold", c_int32),
                 ("step_w", c_fp * 9), ("step_pb", c_fp * 2), ("use_step", c_int32),
-                ("step_dtype", c_int32)]
+                ("step_dtype", c_int32), ("step_bneck_w", c_fp)]
 
 
 ACT = {"none": 0, "relu": 1, "tanh": 2, "tanh_half": 3, "gelu": 4}
@@ -142,6 +142,11 @@ SIGNATURES = {
     "ldm_attention_folded": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_vp]),
     "ldm_fold_conv_proj": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_fp, c_int32, c_fp, c_fp, c_vp]),
+    "ldm_attention_folded_probs": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                             c_vp]),
+    "ldm_bneck_fold_supported": (c_int32, [c_int32, c_int32, c_int32]),
+    "ldm_bneck_fold_values": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp]),
+    "ldm_bneck_pv": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_vp]),
     "ldm_q_sample": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_predict_start": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_sched_backward": (c_int32, [c_int32, c_fp, c_fp, c_int32, c_vp, c_fp, c_fp, c_int32, c_int64, c_vp]),

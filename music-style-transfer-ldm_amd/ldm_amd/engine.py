@@ -182,6 +182,8 @@ class UNetEngine:
                     w.step_pb[j] = pbt.data_ptr()
                 w.use_step = self.step
                 w.step_dtype = sdt
+                # the bottleneck's fold unpacked: U (CA1's values folded into it) is formed from it once per loop
+                w.step_bneck_w = folded[4][0].data_ptr()
         tm = u.time_mlp
         freqs = ops.sinusoid_freqs(tm[1].weight.shape[0], tm[1].weight.device)
         keep.append(freqs)

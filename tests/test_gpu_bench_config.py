@@ -241,3 +241,36 @@ def test_bench_config_every_layer_instance(bench_objects, cuda):
         got = _from_layout(y, (d.B, d.Cout, d.Hout, d.Wout), True)
         assert rel_err(npy(got), ref.clamp_min(0).numpy()) < 1e-5, ("fold", layer)
     assert len(seen) >= 8
+
+
+def test_bench_config_bottleneck_on_folded_values(bench_objects, cuda):
+    """The instance the loop runs for CA1 -> bottleneck at the bench shape (bfold.hip): U formed from the engine's
+    unpacked fold (step_bneck_w) and a CA1 K/V projection, contracted with CA1's probabilities plus the engine's
+    folded position bias (step_pb[1]) == relu(bottleneck(out_proj(concat_h P_h V_h))) in float64 (1e-5)."""
+    from ldm_amd import _lib as L
+    eng, ldm = bench_objects["eng"], bench_objects["ldm"]
+    B, H, W = 8, 16, 64
+    lib = L.load()
+    if not lib.ldm_bneck_fold_supported(B, H, W):
+        pytest.skip("LDM_BNECK_FOLD=0: the loop runs CA1 + the uconv bottleneck (covered above)")
+    w = eng.weights(eng.shape(B, 32, H, W))
+    assert w.step_bneck_w
+    u = ldm.unet
+    g = torch.Generator().manual_seed(91)
+    kv = torch.randn(B, 1024, 16, generator=g)
+    p = torch.softmax(torch.randn(B, 4, 16, 16, generator=g) * 2.0, dim=-1)
+    kvd, pd = kv.to(cuda), p.contiguous().to(cuda)
+    ub = torch.empty(B, 512, 576, device=cuda)
+    y = torch.empty(B, 16, 512, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    L.call("ldm_bneck_fold_values", w.step_bneck_w, kvd.data_ptr(), ub.data_ptr(), B, st)
+    L.call("ldm_bneck_pv", ub.data_ptr(), pd.data_ptr(), w.step_pb[1], y.data_ptr(), B, 0, st)
+    torch.cuda.synchronize()
+    v = kv.double()[:, 512:, :].reshape(B, 4, 128, 16)
+    a = torch.einsum("bhls,bhds->bhdl", p.double(), v).reshape(B, 512, 2, 8)
+    mha = u.cross_attention1.multihead_attn
+    x64 = torch.einsum("oc,bchw->bohw", mha.out_proj.weight.detach().double().cpu(), a) + \
+        mha.out_proj.bias.detach().double().cpu()[None, :, None, None]
+    ref = F.conv2d(x64, u.bottleneck.weight.detach().double().cpu(), u.bottleneck.bias.detach().double().cpu(),
+                   padding=1).clamp_min(0)
+    assert rel_err(npy(y.view(B, 2, 8, 512).permute(0, 3, 1, 2)), ref.numpy()) < 1e-5

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=$PWD/gpurun_out/${1:-workloads}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
-timeout -k 10 240 python -u bench.py --workload transfer --steps 10 --warmup 2 --no-cpu-baseline > $O/transfer.json 2> $O/transfer.err || { echo "transfer failed"; tail -20 $O/transfer.err; exit 1; }
+timeout -k 10 240 python -u bench.py --workload transfer --steps 10 --warmup 2 > $O/transfer.json 2> $O/transfer.err || { echo "transfer failed"; tail -20 $O/transfer.err; exit 1; }
 cat $O/transfer.json
 timeout -k 10 240 python -u bench.py --workload train --steps 10 --warmup 3 > $O/train.json 2> $O/train.err || { echo "train failed"; tail -20 $O/train.err; exit 1; }
 cat $O/train.json
