@@ -16,6 +16,7 @@
 // instead of the K-split uconv form's 147 KB of W' plus partial slabs, and the CA1 launch writes P only (no
 // P V product).  U is formed once per loop (bneck_fold_values_kernel), like the folded keys.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -52,16 +53,17 @@ __global__ __launch_bounds__(288) void bneck_fold_values_kernel(const float* __r
 }
 
 // y[b][l][co] (NHWC on the 2 x 8 plane) = relu(sum_k U[b][co][k] B[k][l] + pb[l][co]), B[(t,h,s)][l] = P[b][h][l_t][s]
-// (0 where tap t of l falls outside the plane).  Block = (16-row co tile, sample b); its 4 waves split the 36 chunks
-// of 16 k (one (tap, head) pair each) 9 / 9 / 9 / 9, all their operand loads in flight before the MFMAs
+// (0 where tap t of l falls outside the plane).  Block = (16-row co tile, sample b); its NWV waves (9 by default) split
+// the 36 chunks of 16 k (one (tap, head) pair each), all their operand loads in flight before the MFMAs
 // (v_mfma_f32_16x16x4_f32: lane (row = l & 15, lg = l >> 4) holds A[row][4 lg + j] and B[4 lg + j][col = l & 15]
 // for step j — one 16-byte load each per chunk), and meet in LDS in wave order.  DT != 0: the output is rounded to
 // the 16-bit type, as the reference's autocast conv returns it (the operands stay fp32).
-template <int DT>
-__global__ __launch_bounds__(256) void bneck_pv_kernel(const float* __restrict__ u, const float* __restrict__ p,
-                                                       const float* __restrict__ pb, float* __restrict__ y) {
-    constexpr int NCH = K / 16, PER = NCH / 4;   // 36 chunks, 9 per wave
-    __shared__ floatx4 red[4][64];
+template <int DT, int NWV>
+__global__ __launch_bounds__(64 * NWV) void bneck_pv_kernel(const float* __restrict__ u, const float* __restrict__ p,
+                                                            const float* __restrict__ pb, float* __restrict__ y) {
+    constexpr int NCH = K / 16, PER = NCH / NWV;   // 36 chunks, PER per wave
+    static_assert(NCH % NWV == 0, "chunks per wave");
+    __shared__ floatx4 red[NWV][64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int row = lane & 15, lg = lane >> 4;
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void bneck_pv_kernel(const float* __restrict__
     if (wave != 0) return;
     floatx4 v = red[0][lane];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) v = v + red[w][lane];
+    for (int w = 1; w < NWV; ++w) v = v + red[w][lane];
     const int co = co0 + 4 * lg;   // D rows 4 lg + r, column l
     const floatx4 bias = *reinterpret_cast<const floatx4*>(pb + (size_t)l * E + co);
     floatx4 o;
@@ -125,13 +127,31 @@ int bneck_pv(const float* u, const float* p, const float* pb, float* y, int B, i
     LDM_REQUIRE(u && p && pb && y && B > 0, "bottleneck (folded values): bad argument");
     LDM_REQUIRE((((uintptr_t)u | (uintptr_t)p | (uintptr_t)pb | (uintptr_t)y) & 15) == 0,
                 "bottleneck (folded values): operands must be 16-byte aligned");
+    LDM_REQUIRE(dtype >= LDM_DT_F32 && dtype <= LDM_DT_BF16, "bottleneck (folded values): unknown operand precision");
+    // waves per block splitting the 36 chunks (LDM_BNECK_WAVES: 4, 6, 9 or 12).  Measured in the loop
+    // (gpurun_out/ab1, two rounds): 4 waves 75.30 / 75.34 us per iteration, 6: 74.08 / 73.84, 9: 73.48 / 73.22,
+    // 12: 73.48 / 73.55 — more loads in flight per CU; 9 (four chunks per wave) kept
+    static const int nwv = [] {
+        const char* e = std::getenv("LDM_BNECK_WAVES");
+        const int v = e ? std::atoi(e) : 9;
+        return (v == 4 || v == 6 || v == 12) ? v : 9;
+    }();
     const dim3 grid(bf::E / 16, B);
-    switch (dtype) {
-        case LDM_DT_F32: hipLaunchKernelGGL(bf::bneck_pv_kernel<0>, grid, dim3(256), 0, st, u, p, pb, y); break;
-        case LDM_DT_F16: hipLaunchKernelGGL(bf::bneck_pv_kernel<LDM_DT_F16>, grid, dim3(256), 0, st, u, p, pb, y); break;
-        case LDM_DT_BF16: hipLaunchKernelGGL(bf::bneck_pv_kernel<LDM_DT_BF16>, grid, dim3(256), 0, st, u, p, pb, y); break;
-        default: return fail(2, "bottleneck (folded values): unknown operand precision");
-    }
+    auto go = [&](auto dtc, auto nwc) {
+        constexpr int DT = decltype(dtc)::value, NW = decltype(nwc)::value;
+        hipLaunchKernelGGL((bf::bneck_pv_kernel<DT, NW>), grid, dim3(64 * NW), 0, st, u, p, pb, y);
+    };
+    auto by_waves = [&](auto dtc) {
+        switch (nwv) {
+            case 6: go(dtc, std::integral_constant<int, 6>{}); break;
+            case 9: go(dtc, std::integral_constant<int, 9>{}); break;
+            case 12: go(dtc, std::integral_constant<int, 12>{}); break;
+            default: go(dtc, std::integral_constant<int, 4>{}); break;
+        }
+    };
+    if (dtype == LDM_DT_F16) by_waves(std::integral_constant<int, LDM_DT_F16>{});
+    else if (dtype == LDM_DT_BF16) by_waves(std::integral_constant<int, LDM_DT_BF16>{});
+    else by_waves(std::integral_constant<int, 0>{});
     LDM_CHECK_LAUNCH("bneck_pv_kernel");
     return 0;
 }

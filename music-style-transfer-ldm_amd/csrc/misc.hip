@@ -755,9 +755,20 @@ int attention_folded_probs(const float* z, const float* kf, const float* bf, flo
     LDM_REQUIRE(z && kf && bf && p, "attention probs (folded): null argument");
     LDM_REQUIRE(B > 0 && heads == 4 && E == 512 && L > 0 && L <= 16 && S > 0 && S <= 16,
                 "attention probs (folded): instances for CA1's 2 x 8 plane only (E 512, L, S <= 16)");
-    auto kfn = attention_mfma_kernel<2, 16, 16, 128, 16, true, 512, 8, true>;
-    const size_t lds = ((size_t)8 * 16 * 17 + (size_t)128 * 17) * sizeof(float);
-    hipLaunchKernelGGL(kfn, dim3(B * heads), dim3(64 * 8), lds, st, z, kf, p, E, heads, L, S, 1.0f, kf, bf);   // (kv unread)
+    // waves splitting the E-long score contraction (LDM_CA1P_WAVES: 8 or 16; A/B timing)
+    static const int nw = [] {
+        const char* e = std::getenv("LDM_CA1P_WAVES");
+        return e && std::atoi(e) == 16 ? 16 : 8;
+    }();
+    if (nw == 16) {
+        auto kfn = attention_mfma_kernel<2, 16, 16, 128, 16, true, 512, 16, true>;
+        const size_t lds = ((size_t)16 * 16 * 17 + (size_t)128 * 17) * sizeof(float);
+        hipLaunchKernelGGL(kfn, dim3(B * heads), dim3(64 * 16), lds, st, z, kf, p, E, heads, L, S, 1.0f, kf, bf);
+    } else {
+        auto kfn = attention_mfma_kernel<2, 16, 16, 128, 16, true, 512, 8, true>;
+        const size_t lds = ((size_t)8 * 16 * 17 + (size_t)128 * 17) * sizeof(float);
+        hipLaunchKernelGGL(kfn, dim3(B * heads), dim3(64 * 8), lds, st, z, kf, p, E, heads, L, S, 1.0f, kf, bf);   // (kv unread)
+    }
     LDM_CHECK_LAUNCH("attention_mfma_kernel (folded, probabilities)");
     return 0;
 }
