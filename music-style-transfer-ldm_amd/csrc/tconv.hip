@@ -492,19 +492,11 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     const EpiArgs& e = a.ep;
     const bool ro = e.round_out != 0;   // a select per value: DT is known here, the mode test is not per value
     auto rnd = [ro](float v) { return ro ? round16(v, DT) : v; };
-    auto epi = [&](float v, int co) {
-        if (e.bias) v = v + e.bias[co];
-        v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
-        if (e.bn_w) {   // as epi_finish (conv.hip)
-            const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
-            const float alpha = invstd * e.bn_w[co];
-            const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-            v = rnd(v * alpha + beta);
-        }
-        return rnd(apply_act(v, e.act));
-    };
     if constexpr (NT == 4) {
-        // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values
+        // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values.
+        // Per channel (i, q) the bias / BN constants are read once for the lane's two positions, and the
+        // activation, the BN flag and the storage type are compile-time forms dispatched once (see below).
+        size_t obase[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int nn = n0 + wn * 64 + 32 * j + r;
@@ -513,18 +505,55 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
             const int qy = a.fd_w.div(rr);
             const int qx = rr - qy * a.pt.Wq;
             const int oy = qy * a.pt.osy + a.pt.ry[ph], ox = qx * a.pt.osy + a.pt.rx[ph];
-            const size_t obase = (size_t)bb * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+            obase[j] = (size_t)bb * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+        }
+        const size_t HWo = (size_t)a.Hout * a.Wout;
+        auto store_lane = [&](auto actc, auto bnc, auto y16c) {
+            constexpr int ACT = decltype(actc)::value;   // LDM_ACT_NONE, LDM_ACT_RELU, or -1: e.act at run time
+            constexpr bool BNF = decltype(bnc)::value, Y16 = decltype(y16c)::value;
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const int co = mbase + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
                     if (co >= a.Cout) continue;
-                    const float v = epi(acc[0][i][j][q], co);
-                    const size_t o = obase + (size_t)co * a.Hout * a.Wout;
-                    if (e.act_out) st1_st<DT>(e.act_out, o, e.y16, v);
-                    st1_st<DT>(a.y, o, e.y16, v);
+                    const float bias = e.bias ? e.bias[co] : 0.f;
+                    float alpha = 0.f, beta = 0.f;
+                    if constexpr (BNF) {   // as epi_finish (conv.hip)
+                        const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
+                        alpha = invstd * e.bn_w[co];
+                        beta = e.bn_b[co] - e.bn_m[co] * alpha;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        float v = acc[0][i][j][q];
+                        if (e.bias) v = v + bias;
+                        v = rnd(v);
+                        if constexpr (BNF) v = rnd(v * alpha + beta);
+                        if constexpr (ACT == LDM_ACT_RELU) v = v < 0.f ? 0.f : v;
+                        else if constexpr (ACT < 0) v = apply_act(v, e.act);
+                        v = rnd(v);
+                        const size_t o = obase[j] + (size_t)co * HWo;
+                        if (e.act_out) st1_st<DT>(e.act_out, o, Y16, v);
+                        st1_st<DT>(a.y, o, Y16, v);
+                    }
                 }
+        };
+        auto by_store = [&](auto actc, auto bnc) {
+            if (e.y16) store_lane(actc, bnc, std::true_type{});
+            else store_lane(actc, bnc, std::false_type{});
+        };
+        using A0 = std::integral_constant<int, LDM_ACT_NONE>;
+        using A1 = std::integral_constant<int, LDM_ACT_RELU>;
+        using AG = std::integral_constant<int, -1>;
+        if (e.bn_w) {
+            if (e.act == LDM_ACT_NONE) by_store(A0{}, std::true_type{});
+            else if (e.act == LDM_ACT_RELU) by_store(A1{}, std::true_type{});
+            else by_store(AG{}, std::true_type{});
+        } else {
+            if (e.act == LDM_ACT_NONE) by_store(A0{}, std::false_type{});
+            else if (e.act == LDM_ACT_RELU) by_store(A1{}, std::false_type{});
+            else by_store(AG{}, std::false_type{});
         }
     } else {
         // Staged through LDS (the image buffers are free now) as [channel][output row segment], then written
@@ -532,13 +561,21 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         // direct stores are 4-byte scalars (64-128 per lane), and the store issue, not the bytes, bounded the
         // large-plane layers.  One pass for a single phase (the tile's R rows x Cq columns); PK 1: one pass per
         // output row parity ry, holding phases (ry, 0) and (ry, 1) interleaved into whole output rows.
+        // The raw accumulators are staged; the epilogue runs in the store pass, on a 16-byte piece of one output
+        // channel at a time (its bias / BN constants loaded once per piece, not once per value), with the
+        // activation and the BN flag as compile-time forms (dispatched once: per-value runtime switches and the
+        // inlined tanh / erf paths of every value made the epilogue the kernel's largest VALU stream).
         constexpr int NPASS = PK ? 2 : 1;
-        const int cq = 1 << a.cq_log2, R = BN >> a.cq_log2;
-        const int rowlen = PK ? 2 * cq : cq;            // floats per staged output row
-        const int seg = R * rowlen;                     // floats per channel in one pass
-        const int pitch = seg + 4;                      // (+16 B: consecutive channels start on different banks)
+        constexpr int SEG = BN * (PK ? 2 : 1);          // floats per channel in one pass (R rows x rowlen)
+        const int cq = 1 << a.cq_log2;
+        const int rl_log2 = a.cq_log2 + (PK ? 1 : 0);   // rowlen = floats per staged output row
+        const int rowlen = 1 << rl_log2;
+        constexpr int pitch = SEG + 4;                  // (+16 B: consecutive channels start on different banks)
         float* stg = reinterpret_cast<float*>(img);
         const int HWo = a.Hout * a.Wout;
+        const int b = a.fd_hw.div(n0);
+        const int rem0 = n0 - b * HWq;
+        const int qy0 = a.fd_w.div(rem0), qx0 = rem0 - qy0 * a.pt.Wq;
         static_for<0, NPASS>([&](auto passc) {
             constexpr int pass = decltype(passc)::value;
             __syncthreads();   // every wave is done with the image (pass 0) / the previous pass's reads
@@ -555,34 +592,66 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
 #pragma unroll
                         for (int q = 0; q < 16; ++q) {
                             const int cl = wm * (BM / 2) + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
-                            const int co = mt * BM + cl;
-                            stg[cl * pitch + col] = epi(acc[u][i][j][q], co < a.Cout ? co : 0);
+                            stg[cl * pitch + col] = acc[u][i][j][q];
                         }
                 }
             });
             __syncthreads();
-            const int nv = BM * seg / 4;               // 16-byte pieces of the staged tile
-            const int b = a.fd_hw.div(n0);
-            const int rem0 = n0 - b * HWq;
-            const int qy0 = a.fd_w.div(rem0), qx0 = rem0 - qy0 * a.pt.Wq;
-            for (int k = tid; k < nv; k += 256) {
-                const int cl = k / (seg / 4);
-                const int rest4 = (k - cl * (seg / 4)) * 4;
-                const int co = mt * BM + cl;
-                if (co >= a.Cout) continue;
-                const int rr = rest4 / rowlen, c0 = rest4 - rr * rowlen;
-                const int oy = PK ? 2 * (qy0 + rr) + pass : qy0 + rr;
-                const int ox = PK ? 2 * qx0 + c0 : qx0 + c0;
-                const floatx4 v = *reinterpret_cast<const floatx4*>(stg + cl * pitch + rest4);
-                const size_t o = ((size_t)b * a.Cout + co) * HWo + (size_t)oy * a.Wout + ox;
-                if (e.y16) {   // 16-bit storage: 8-byte stores of the four values
-                    const float vv[4] = {v[0], v[1], v[2], v[3]};
-                    if (e.act_out) st_st<DT, 4>(e.act_out, o, true, vv);
-                    st_st<DT, 4>(a.y, o, true, vv);
-                } else {
-                    if (e.act_out) *reinterpret_cast<floatx4*>(e.act_out + o) = v;
-                    *reinterpret_cast<floatx4*>(a.y + o) = v;
+            constexpr int nv = BM * SEG / 4;           // 16-byte pieces of the staged tile
+            auto store_pass = [&](auto actc, auto bnc) {
+                constexpr int ACT = decltype(actc)::value;   // LDM_ACT_NONE, LDM_ACT_RELU, or -1: e.act at run time
+                constexpr bool BNF = decltype(bnc)::value;
+                for (int k = tid; k < nv; k += 256) {
+                    const int cl = k / (SEG / 4);
+                    const int rest4 = (k - cl * (SEG / 4)) * 4;
+                    const int co = mt * BM + cl;
+                    if (co >= a.Cout) continue;
+                    const int rr = rest4 >> rl_log2, c0 = rest4 - (rr << rl_log2);
+                    const int oy = PK ? 2 * (qy0 + rr) + pass : qy0 + rr;
+                    const int ox = PK ? 2 * qx0 + c0 : qx0 + c0;
+                    const floatx4 raw = *reinterpret_cast<const floatx4*>(stg + cl * pitch + rest4);
+                    const float bias = e.bias ? e.bias[co] : 0.f;
+                    float alpha = 0.f, beta = 0.f;
+                    if constexpr (BNF) {   // as epi_finish (conv.hip)
+                        const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
+                        alpha = invstd * e.bn_w[co];
+                        beta = e.bn_b[co] - e.bn_m[co] * alpha;
+                    }
+                    float vv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float v = raw[q];
+                        if (e.bias) v = v + bias;
+                        v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
+                        if constexpr (BNF) v = rnd(v * alpha + beta);
+                        if constexpr (ACT == LDM_ACT_RELU) v = v < 0.f ? 0.f : v;
+                        else if constexpr (ACT < 0) v = apply_act(v, e.act);
+                        vv[q] = rnd(v);
+                    }
+                    const size_t o = ((size_t)b * a.Cout + co) * HWo + (size_t)oy * a.Wout + ox;
+                    if (e.y16) {   // 16-bit storage: 8-byte stores of the four values
+                        if (e.act_out) st_st<DT, 4>(e.act_out, o, true, vv);
+                        st_st<DT, 4>(a.y, o, true, vv);
+                    } else {
+                        const floatx4 v4{vv[0], vv[1], vv[2], vv[3]};
+                        if (e.act_out) *reinterpret_cast<floatx4*>(e.act_out + o) = v4;
+                        *reinterpret_cast<floatx4*>(a.y + o) = v4;
+                    }
                 }
+            };
+            using A0 = std::integral_constant<int, LDM_ACT_NONE>;
+            using A1 = std::integral_constant<int, LDM_ACT_RELU>;
+            using AG = std::integral_constant<int, -1>;
+            using BT = std::true_type;
+            using BF = std::false_type;
+            if (e.bn_w) {
+                if (e.act == LDM_ACT_NONE) store_pass(A0{}, BT{});
+                else if (e.act == LDM_ACT_RELU) store_pass(A1{}, BT{});
+                else store_pass(AG{}, BT{});
+            } else {
+                if (e.act == LDM_ACT_NONE) store_pass(A0{}, BF{});
+                else if (e.act == LDM_ACT_RELU) store_pass(A1{}, BF{});
+                else store_pass(AG{}, BF{});
             }
         });
     }
@@ -725,7 +794,7 @@ static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* 
 
 // The window form of one kind-3 conv: one launch per group of phases with equal tap counts.  Returns 1 (and
 // launches nothing) when some group's geometry does not fit an instance.
-static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st) {
+static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st, bool any_density) {
     const PhaseTable& pt = t.pt;
     auto fill = [&](WArgs& a) {
         a.x = t.x, a.w = t.w, a.y = t.y;
@@ -759,7 +828,7 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         // measured (profiles/r04/tconv_window): the window form wins for 3x3 convs (5-25 %) and where a window
         // feeds >= 16 MFMAs per wave with one M tile (the decoder's 32 -> 128 convT and its data gradient); with
         // fewer taps x rows per window, or a window re-loaded by two M tiles, the per-chunk form is faster
-        const bool dense = nt * (bm / 64) >= 8 && t.nM == 1;
+        const bool dense = (nt * (bm / 64) >= 8 || any_density) && t.nM == 1;
         const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && bm == 64 && ns <= 5 && dense) ||
                         (nt == 4 && sy == 1 && ns <= 2 && dense);
         if (!ok) return 1;
@@ -890,9 +959,13 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     // 4.899 ms per step on the gather form, 4.823 with bit 0, 4.874 with both — the four-phase form won only on
     // style_enc3's data gradient (85 -> 71 us) and lost 5-16 us on the other four (profiles/r04/tconv_window);
     // re-measured with the maps in 16 bits: 909 vs 724 us for those layers, 3.98-4.00 vs 3.86-3.95 ms per step
+    // Round 5: with the epilogue's per-value branches and loads gone (tconvw_kernel's store pass) the four-phase
+    // form wins on every k3 s2 data gradient of the step (tools/one_conv.py, B = 32 bf16: 64 -> 128 104.9 -> 66.7
+    // us, 128 -> 256 91.3 -> 53.1, 256 -> 256 52.5 -> 32.7, 128 -> 32 46.1 -> 22.7): default 3.  Bit 2: the
+    // single-phase window form for the 4-tap phases whatever their density (A/B timing).
     static const int win = [] {
         const char* e = std::getenv("LDM_TCONV_WIN");
-        return e ? (int)std::strtol(e, nullptr, 0) : 1;
+        return e ? (int)std::strtol(e, nullptr, 0) : 3;
     }();
     if (win) {
         const bool k16 = a.pt.nphase == 1 && a.pt.ntap[0] == 16;
@@ -900,7 +973,7 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
         if ((k3t && (win & 2)) || (!k3t && (win & 1))) {
             tc::TArgs t = a;
             if ((k16 || k3t) && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
-            const int rc = tc::forward_window(d, t, (k16 || k3t) ? 64 : 64 * p.tm, p.tn, s);
+            const int rc = tc::forward_window(d, t, (k16 || k3t) ? 64 : 64 * p.tm, p.tn, s, (win & 4) != 0);
             if (rc != 1) return rc;
         }
     }
