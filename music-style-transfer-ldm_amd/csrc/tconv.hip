@@ -236,41 +236,74 @@ __global__ __launch_bounds__(256) void tconv_kernel(TArgs a) {
         if (c + 6 >= nch) break;
     }
 
-    // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store
+    // ---- epilogue: bias -> eval-BN -> act (-> act_out), NCHW store.  Per channel (i, q) the bias / BN constants
+    // are read once for the lane's two positions; the activation, the BN flag and the storage type are
+    // compile-time forms dispatched once (per-value runtime switches and loads were the epilogue's cost).
     const EpiArgs& e = a.ep;
     const bool ro = e.round_out != 0;   // a select per value: DT is known here, the mode test is not per value
     auto rnd = [ro](float v) { return ro ? round16(v, DT) : v; };
+    size_t obase[2];
+    bool nok[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int64_t n = n0 + wn * 64 + 32 * j + r;
-        if (n >= a.N) continue;
-        const int nn = (int)n;
+        nok[j] = n < a.N;
+        const int nn = nok[j] ? (int)n : 0;
         const int b = a.fd_hw.div(nn);
         const int rr = nn - b * (a.pt.Hq * a.pt.Wq);
         const int qy = a.fd_w.div(rr);
         const int qx = rr - qy * a.pt.Wq;
         const int oy = qy * a.pt.osy + a.pt.ry[ph], ox = qx * a.pt.osy + a.pt.rx[ph];
-        const size_t obase = (size_t)b * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+        obase[j] = (size_t)b * a.Cout * a.Hout * a.Wout + (size_t)oy * a.Wout + ox;
+    }
+    const size_t HWo = (size_t)a.Hout * a.Wout;
+    auto store_lane = [&](auto actc, auto bnc, auto y16c) {
+        constexpr int ACT = decltype(actc)::value;   // LDM_ACT_NONE, LDM_ACT_RELU, or -1: e.act at run time
+        constexpr bool BNF = decltype(bnc)::value, Y16 = decltype(y16c)::value;
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int co = mbase + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (co >= a.Cout) continue;
-                float v = acc[i][j][q];
-                if (e.bias) v = v + e.bias[co];
-                v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
-                if (e.bn_w) {   // as epi_finish (conv.hip)
+                const float bias = e.bias ? e.bias[co] : 0.f;
+                float alpha = 0.f, beta = 0.f;
+                if constexpr (BNF) {   // as epi_finish (conv.hip)
                     const float invstd = 1.0f / sqrtf(e.bn_v[co] + e.bn_eps);
-                    const float alpha = invstd * e.bn_w[co];
-                    const float beta = e.bn_b[co] - e.bn_m[co] * alpha;
-                    v = rnd(v * alpha + beta);
+                    alpha = invstd * e.bn_w[co];
+                    beta = e.bn_b[co] - e.bn_m[co] * alpha;
                 }
-                v = rnd(apply_act(v, e.act));
-                const size_t o = obase + (size_t)co * a.Hout * a.Wout;
-                if (e.act_out) st1_st<DT>(e.act_out, o, e.y16, v);
-                st1_st<DT>(a.y, o, e.y16, v);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (!nok[j]) continue;
+                    float v = acc[i][j][q];
+                    if (e.bias) v = v + bias;
+                    v = rnd(v);   // (autocast output semantics: round_out is 0 or DT)
+                    if constexpr (BNF) v = rnd(v * alpha + beta);
+                    if constexpr (ACT == LDM_ACT_RELU) v = v < 0.f ? 0.f : v;
+                    else if constexpr (ACT < 0) v = apply_act(v, e.act);
+                    v = rnd(v);
+                    const size_t o = obase[j] + (size_t)co * HWo;
+                    if (e.act_out) st1_st<DT>(e.act_out, o, Y16, v);
+                    st1_st<DT>(a.y, o, Y16, v);
+                }
             }
+    };
+    auto by_store = [&](auto actc, auto bnc) {
+        if (e.y16) store_lane(actc, bnc, std::true_type{});
+        else store_lane(actc, bnc, std::false_type{});
+    };
+    using A0 = std::integral_constant<int, LDM_ACT_NONE>;
+    using A1 = std::integral_constant<int, LDM_ACT_RELU>;
+    using AG = std::integral_constant<int, -1>;
+    if (e.bn_w) {
+        if (e.act == LDM_ACT_NONE) by_store(A0{}, std::true_type{});
+        else if (e.act == LDM_ACT_RELU) by_store(A1{}, std::true_type{});
+        else by_store(AG{}, std::true_type{});
+    } else {
+        if (e.act == LDM_ACT_NONE) by_store(A0{}, std::false_type{});
+        else if (e.act == LDM_ACT_RELU) by_store(A1{}, std::false_type{});
+        else by_store(AG{}, std::false_type{});
     }
 }
 
@@ -328,15 +361,25 @@ struct WArgs {
 // conv) in ONE block over one shared window — phases (0,0), (0,1), (1,0), (1,1) have 1, 2, 2, 4 taps, all reading
 // input offsets {0, 1} x {0, 1}, so the block runs nine (phase, tap) pairs per window into four accumulator sets,
 // the compute density of a 3x3 conv (a launch per phase reloads the window for one to four taps).
-__host__ __device__ constexpr int pk1_phase(int i) { return i < 1 ? 0 : (i < 3 ? 1 : (i < 5 ? 2 : 3)); }
-__host__ __device__ constexpr int pk1_tap(int i) { return i < 1 ? i : (i < 3 ? i - 1 : (i < 5 ? i - 3 : i - 5)); }
-__host__ __device__ constexpr int pk1_ntap(int p) { return p == 0 ? 1 : (p == 3 ? 4 : 2); }
+// PK = 2 (round 5): the same for the four phases of a k4 s2 p1 transposed conv (the decoder's 128 -> 64 layer): four
+// taps each, all reading input offsets {-1, 0, 1} x {-1, 0, 1}: sixteen (phase, tap) pairs per shared window.
+template <int PK>
+__host__ __device__ constexpr int pk_phase(int i) {
+    return PK == 2 ? i / 4 : (i < 1 ? 0 : (i < 3 ? 1 : (i < 5 ? 2 : 3)));
+}
+template <int PK>
+__host__ __device__ constexpr int pk_tap(int i) {
+    return PK == 2 ? i % 4 : (i < 1 ? i : (i < 3 ? i - 1 : (i < 5 ? i - 3 : i - 5)));
+}
+template <int PK>
+__host__ __device__ constexpr int pk_ntap(int p) { return PK == 2 ? 4 : (p == 0 ? 1 : (p == 3 ? 4 : 2)); }
 
 template <int BM, int NT, int SY, int DT, int NS, int PK = 0, int XS = 0>
 __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     constexpr int MT = BM / 64;
     constexpr int NACC = PK ? 4 : 1;
-    static_assert(!PK || (NT == 9 && SY == 1), "PK 1: the nine (phase, tap) pairs of a k3 op1 transposed conv");
+    static_assert(!PK || (NT == (PK == 2 ? 16 : 9) && SY == 1),
+                  "PK 1 / 2: the nine / sixteen (phase, tap) pairs of a k3 op1 / k4 p1 transposed conv");
     extern __shared__ __attribute__((aligned(16))) unsigned short img[];   // [2][image]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -432,11 +475,11 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     const int mbase = mt * BM + wm * (BM / 2);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, 0x7ffffff0, 0x00020000);
     u16x8 af[NT][MT];
-    // pair tp: phase PK ? pk1_phase(tp) : ph, tap in that phase PK ? pk1_tap(tp) : tp
+    // pair tp: phase PK ? pk_phase(tp) : ph, tap in that phase PK ? pk_tap(tp) : tp
     auto loadA = [&](int w, auto tpc, u16x8 (&dst)[MT]) {
         constexpr int tp = decltype(tpc)::value;
-        const int pp = PK ? pk1_phase(tp) : ph;
-        const int c = (w >> 1) * (PK ? pk1_ntap(pk1_phase(tp)) : NT) + (PK ? pk1_tap(tp) : tp);
+        const int pp = PK ? pk_phase<PK>(tp) : ph;
+        const int c = (w >> 1) * (PK ? pk_ntap<PK>(pk_phase<PK>(tp)) : NT) + (PK ? pk_tap<PK>(tp) : tp);
         const int wph = (int)a.pt.wofs[pp];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
@@ -472,8 +515,8 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         const unsigned short* bimg = img + buf * (imgsz + WP);
         static_for<0, NT>([&](auto tpc) {
             constexpr int tp = decltype(tpc)::value;
-            constexpr int u = PK ? pk1_phase(tp) : 0;
-            const int to = (PK ? a.toff[u][pk1_tap(tp)] : a.toff[ph][tp]) * WP;
+            constexpr int u = PK ? pk_phase<PK>(tp) : 0;
+            const int to = (PK ? a.toff[u][pk_tap<PK>(tp)] : a.toff[ph][tp]) * WP;
             u16x8 bf[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const u16x8*>(bimg + lb[j] + to);
@@ -794,7 +837,8 @@ static bool w_geometry(const ldm_conv_desc& d, const PhaseTable& pt, const int* 
 
 // The window form of one kind-3 conv: one launch per group of phases with equal tap counts.  Returns 1 (and
 // launches nothing) when some group's geometry does not fit an instance.
-static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st, bool any_density) {
+static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt, hipStream_t st, bool any_density,
+                          bool four_phase_k4) {
     const PhaseTable& pt = t.pt;
     auto fill = [&](WArgs& a) {
         a.x = t.x, a.w = t.w, a.y = t.y;
@@ -811,6 +855,16 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         fill(a);
         a.nph = 1;
         return dt == LDM_DT_F16 ? launch_w<64, 9, 1, 1, 2, 1>(a, st) : launch_w<64, 9, 1, 2, 2, 1>(a, st);
+    }
+    // a k4 s2 p1 transposed conv (the decoder's upsampling layers: four phases of four taps): likewise
+    if (four_phase_k4 && pt.nphase == 4 && pt.sy == 1 && pt.ntap[0] == 4 && pt.ntap[1] == 4 && pt.ntap[2] == 4 &&
+        pt.ntap[3] == 4) {
+        WArgs a{};
+        const int all[4] = {0, 1, 2, 3};
+        if (bm != 64 || !w_geometry(d, pt, all, 4, a, true) || a.nsu > 2 * 256) return 1;
+        fill(a);
+        a.nph = 1;
+        return dt == LDM_DT_F16 ? launch_w<64, 16, 1, 1, 2, 2>(a, st) : launch_w<64, 16, 1, 2, 2, 2>(a, st);
     }
     int groups[kMaxPhase][kMaxPhase], gn[kMaxPhase], gt[kMaxPhase], ng = 0;
     for (int p = 0; p < pt.nphase; ++p) {
@@ -955,25 +1009,29 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     // the window form where the geometry allows (LDM_TCONV_WIN=0: the per-chunk gather form, A/B timing).
     // 16-tap (4x4 stride-2) convs run it on 64-row tiles: their image needs five register slots per thread.
     // LDM_TCONV_WIN: bit 0 the single-phase window forms, bit 1 the four-phase form of the k3 s2 op1 transposed
-    // convs (0 = the per-chunk gather form everywhere).  Default bit 0 only: in the train step (B = 32, bf16)
+    // convs (0 = the per-chunk gather form everywhere); bit 3 (with bit 1): the four-phase form of the k4 s2 p1
+    // transposed convs too.  Default before round 5: bit 0 only: in the train step (B = 32, bf16)
     // 4.899 ms per step on the gather form, 4.823 with bit 0, 4.874 with both — the four-phase form won only on
     // style_enc3's data gradient (85 -> 71 us) and lost 5-16 us on the other four (profiles/r04/tconv_window);
     // re-measured with the maps in 16 bits: 909 vs 724 us for those layers, 3.98-4.00 vs 3.86-3.95 ms per step
     // Round 5: with the epilogue's per-value branches and loads gone (tconvw_kernel's store pass) the four-phase
     // form wins on every k3 s2 data gradient of the step (tools/one_conv.py, B = 32 bf16: 64 -> 128 104.9 -> 66.7
-    // us, 128 -> 256 91.3 -> 53.1, 256 -> 256 52.5 -> 32.7, 128 -> 32 46.1 -> 22.7): default 3.  Bit 2: the
-    // single-phase window form for the 4-tap phases whatever their density (A/B timing).
+    // us, 128 -> 256 91.3 -> 53.1, 256 -> 256 52.5 -> 32.7, 128 -> 32 46.1 -> 22.7), and its k4 s2 p1 form (bit 3)
+    // on the decoder's convT forwards (128 -> 64 113.2 -> 90.1 us, 32 -> 128 34.6 -> 26.0; train step 3.48-3.49 ->
+    // 3.40-3.44 ms): default 11.  Bit 2: the single-phase window form for the 4-tap phases whatever their density.
     static const int win = [] {
         const char* e = std::getenv("LDM_TCONV_WIN");
-        return e ? (int)std::strtol(e, nullptr, 0) : 3;
+        return e ? (int)std::strtol(e, nullptr, 0) : 11;
     }();
     if (win) {
         const bool k16 = a.pt.nphase == 1 && a.pt.ntap[0] == 16;
         const bool k3t = a.pt.nphase == 4 && a.pt.ntap[0] == 1 && a.pt.ntap[3] == 4;   // k3 s2 op1 transposed
-        if ((k3t && (win & 2)) || (!k3t && (win & 1))) {
+        const bool k4t = a.pt.nphase == 4 && a.pt.ntap[0] == 4 && a.pt.ntap[3] == 4 && (win & 8);   // k4 s2 p1
+        if (((k3t || k4t) && (win & 2)) || (!k3t && (win & 1))) {
             tc::TArgs t = a;
-            if ((k16 || k3t) && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
-            const int rc = tc::forward_window(d, t, (k16 || k3t) ? 64 : 64 * p.tm, p.tn, s, (win & 4) != 0);
+            const bool r64 = k16 || k3t || k4t;   // the 64-row tilings (their image needs 5 slots / 4 acc sets)
+            if (r64 && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
+            const int rc = tc::forward_window(d, t, r64 ? 64 : 64 * p.tm, p.tn, s, (win & 4) != 0, k4t);
             if (rc != 1) return rc;
         }
     }
