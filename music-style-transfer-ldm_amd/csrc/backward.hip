@@ -653,9 +653,11 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     // 16-bit storage (LDM_DT_X16 / LDM_DT_DY16) as Dense / Gath flags: Dense = dy (conv) or x (convT)
     const int d16 = (st16 & (d->transposed ? LDM_DT_X16 : LDM_DT_DY16)) ? 1 : 0;
     const int g16 = (st16 & (d->transposed ? LDM_DT_DY16 : LDM_DT_X16)) ? 1 : 0;
-    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st, d16 | (g16 << 1));   // (wgrad.hip) where it applies
+    rc = wgrad2_run(*d, a.dense, a.gath, workspace, S2, dtype, st, d16 | (g16 << 1),   // (wgrad.hip) where it applies
+                    accumulate ? nullptr : dw);
     if (rc > 0) return rc;
     LDM_REQUIRE(rc == 0 || !st16, "wgrad: 16-bit storage on a layer without the tap-shared form (ldm_conv_wgrad_storage16)");
+    if (rc == 0 && S2 == 0) return 0;   // one K range, written to dw by the kernel
     if (rc == 0) {
         wgrad_reduce((const float*)workspace, S2, MN, dw, accumulate, st);
         LDM_CHECK_LAUNCH("wgrad_reduce_kernel");

@@ -251,7 +251,7 @@ int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 // wgrad.hip: the tap-shared weight-gradient kernel (ldm_conv_backward_weight where it applies)
 bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats);
 int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
-               hipStream_t st, int st16 = 0);
+               hipStream_t st, int st16 = 0, float* dw_direct = nullptr);   // splits = 0: written to dw_direct
 int wgrad2_storage16(const ldm_conv_desc& d);
 
 // One DDIM step for one element, one fp32 rounding per reference op (no contraction: callers compile

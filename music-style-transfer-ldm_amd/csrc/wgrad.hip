@@ -855,9 +855,206 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16_kernel(LpArgs a) {
     }
 }
 
+// The same sums on an NBUF-deep ring of chunk buffers (round 5): the double-buffered form keeps one chunk's
+// DMAs (~25 KB per CU) in flight, which at the grid's one block per CU leaves the HBM pipe latency-bound
+// (tools/pmc_one_conv.sh: 64 -> 128 s2 weight gradient, 172 MB fetched in ~60 us, waves mostly waiting).  Here
+// chunks ch + 1 .. ch + NBUF - 2 are in flight while chunk ch computes.  Every wave issues exactly ND + NG DMAs
+// per chunk (slots past the tile's pieces load nothing into a trash KB), so "chunk ch landed" is one
+// vmcnt immediate; the per-slot offsets are chunk-invariant and computed once (the chunk loop walks the
+// chunk coordinates without divisions).  Same blocks, chunks, k-steps and fragments as wgrad_lp16_kernel: the
+// sums are bitwise those of the double-buffered form.
+__host__ __device__ constexpr int lp16_pitch(int S, int KK, int rows, int cols) {
+    const int wr = (rows - 1) * S + KK, wca = (7 + (cols - 1) * S + KK + 7) / 8 * 8;
+    int pc = wr * wca;
+    while (pc % 128 != 8) pc += 8;
+    return pc;
+}
+// the window's 1-KB DMA groups per wave: the larger of the two geometries a QC allows (rows 1 / 2)
+__host__ __device__ constexpr int lp16_ng(int S, int KK, int QC, int NW) {
+    const int p1 = lp16_pitch(S, KK, 1, QC), p2 = lp16_pitch(S, KK, 2, QC / 2);
+    const int pmax = p1 > p2 ? p1 : p2;
+    const int groups = (kLC * pmax / 8 + 63) / 64;
+    return (groups + NW - 1) / NW;
+}
+
+template <int N>
+__device__ __forceinline__ void lp_wait_vm() {
+    static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int S, int KK, int BM, int WM, int QC, int DT, int NBUF>
+__global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16p_kernel(LpArgs a) {
+    constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp16_nb(S, KK);
+    constexpr int PPR = QC / 8, RPI = 64 / PPR, NKS = QC / 16;
+    constexpr int NDG = BM / RPI, ND = (NDG + NW - 1) / NW, NG = lp16_ng(S, KK, QC, NW), NL = ND + NG;
+    static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
+    static_assert(NBUF >= 3 && (NBUF - 2) * NL <= 63, "ring depth");
+    extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ky = wave % KK, wm = wave / KK;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * BM, c0 = blockIdx.x * kLC;
+    const int HQ = a.Hq * a.Wq;
+    const int bufB = lp16_buf_bytes(BM, QC, a.pitch_c);
+    char* const trash = reinterpret_cast<char*>(smem16) + NBUF * bufB;
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 2), 0x00020000);
+
+    // chunk-invariant slot offsets (elements): Dense row m's position run, window piece (channel, row, column)
+    int doff[ND], goff[NG], grow[NG], gcol[NG];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const int gi = wave + j * NW;
+        const int row = gi * RPI + lane / PPR;
+        const int ql = (((lane % PPR) ^ lp16_swz<PPR>(row))) * 8;
+        const int m = m0 + row;
+        doff[j] = (gi < NDG && m < a.M) ? m * HQ + (ql / a.cols) * a.Wq + ql % a.cols : -1;
+    }
+    const int wq8 = a.wca >> 3, pq = a.pitch_c >> 3, npiece = kLC * pq;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int pc = (wave + j * NW) * 64 + lane;
+        const int cl = pc / pq, rem = pc - (pc / pq) * pq;
+        const int wrow = rem / wq8, wx = (rem - wrow * wq8) * 8;
+        const bool ok = pc < npiece && c0 + cl < a.C && wrow < a.wr;
+        goff[j] = ((c0 + cl) * a.Hg + wrow) * a.Wg + wx;
+        grow[j] = ok ? wrow : -(1 << 20);   // (an invalid piece fails the row test of every chunk)
+        gcol[j] = wx;
+    }
+
+    auto issue = [&](int buf, int b, int qy0, int qx0) {
+        char* base = reinterpret_cast<char*>(smem16) + buf * bufB;
+        const int dbase = b * a.M * HQ + qy0 * a.Wq + qx0;
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const int gi = wave + j * NW;
+            const int voff = doff[j] >= 0 ? (dbase + doff[j]) * 2 : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(gi < NDG ? base + gi * 1024 : trash), 16, voff, 0, 0, 0);
+        }
+        const int row0 = qy0 * S - 1, colA = qx0 * S - 8;   // pad 1, e = 7
+        const int gbase = (b * a.C * a.Hg + row0) * a.Wg + colA;
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            const int gi = wave + j * NW;
+            const bool ok = (unsigned)(row0 + grow[j]) < (unsigned)a.Hg && (unsigned)(colA + gcol[j]) < (unsigned)a.Wg;
+            const int voff = ok ? (gbase + goff[j]) * 2 : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(gi * 64 < npiece ? base + BM * QC * 2 + gi * 1024 : trash),
+                                                     16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx16 acc[MF][KK];
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int t = 0; t < KK; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
+
+    int aoff[NKS][MF], boff[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int q0 = ks * 16 + 8 * h;
+        const int rl = q0 / a.cols, xl0 = q0 - rl * a.cols;
+#pragma unroll
+        for (int f = 0; f < MF; ++f) {
+            const int row = (wm * MF + f) * 32 + r;
+            aoff[ks][f] = row * QC * 2 + (((q0 >> 3) ^ lp16_swz<PPR>(row)) << 4);
+        }
+        boff[ks] = BM * QC * 2 + (r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S) * 2;
+    }
+
+    // the issue cursor (chunk ch_begin + k, walked without divisions): sample, chunk row / column origin
+    int ib = ch_begin / a.cps, iqy, iqx;
+    {
+        const int rr = ch_begin - ib * a.cps;
+        if (a.cols == a.Wq) {
+            iqy = rr * a.rows, iqx = 0;
+        } else {
+            const int segs = a.Wq / QC;
+            iqy = rr / segs, iqx = (rr - iqy * segs) * QC;
+        }
+    }
+    auto advance = [&]() {
+        iqx += a.cols;
+        if (iqx >= a.Wq) {
+            iqx = 0, iqy += a.rows;
+            if (iqy >= a.Hq) iqy = 0, ++ib;
+        }
+    };
+    const int n = ch_end - ch_begin;
+#pragma unroll
+    for (int k = 0; k < NBUF - 2; ++k)
+        if (k < n) issue(k, ib, iqy, iqx), advance();
+    int buf = 0, ibuf = NBUF - 2;
+    for (int k = 0; k < n; ++k) {
+        // chunks k + 1 .. min(n - 1, k + NBUF - 2) may stay in flight
+        const int ahead = min(n - 1 - k, NBUF - 2);
+        if constexpr (NBUF == 3) {
+            if (ahead >= 1) lp_wait_vm<NL>(); else lp_wait_vm<0>();
+        } else {
+            static_assert(NBUF == 4, "ring depth 3 or 4");
+            if (ahead >= 2) lp_wait_vm<2 * NL>(); else if (ahead == 1) lp_wait_vm<NL>(); else lp_wait_vm<0>();
+        }
+        __syncthreads();   // chunk k landed for every wave; every wave is done with chunk k - 1's buffer
+        if (k + NBUF - 2 < n) {
+            issue(ibuf, ib, iqy, iqx);
+            advance();
+        }
+        ibuf = ibuf + 1 == NBUF ? 0 : ibuf + 1;
+        const char* sb = reinterpret_cast<const char*>(smem16) + buf * bufB;
+        buf = buf + 1 == NBUF ? 0 : buf + 1;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            u16x8 fa[MF];
+#pragma unroll
+            for (int f = 0; f < MF; ++f) fa[f] = *reinterpret_cast<const u16x8*>(sb + aoff[ks][f]);
+            unsigned w[4 * NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const uint4 p = *reinterpret_cast<const uint4*>(sb + boff[ks] + 16 * i);
+                w[4 * i + 0] = p.x, w[4 * i + 1] = p.y, w[4 * i + 2] = p.z, w[4 * i + 3] = p.w;
+            }
+            static_for<0, KK>([&](auto kxc) {
+                constexpr int kx = decltype(kxc)::value;
+                const u16x8 fb = lp16_frag<S, 7 + kx, 4 * NB>(w);
+#pragma unroll
+                for (int f = 0; f < MF; ++f) acc[f][kx] = mma16x<DT>(fa[f], fb, acc[f][kx]);
+            });
+        }
+    }
+
+    const int c = c0 + r;
+    if (c < a.C) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * a.C * T + (size_t)c * T + ky * KK;
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int m = m0 + (wm * MF + f) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (m < a.M) {
+                    float* o = out + (size_t)m * a.C * T;
+                    if constexpr (KK == 4) {
+                        *reinterpret_cast<floatx4*>(o) = floatx4{acc[f][0][reg], acc[f][1][reg], acc[f][2][reg], acc[f][3][reg]};
+                    } else {
+#pragma unroll
+                        for (int kx = 0; kx < KK; ++kx) o[kx] = acc[f][kx][reg];
+                    }
+                }
+            }
+    }
+}
+
 struct LpPlan {
     int S, KK, BM, WM, QC, splits, lds_bytes;
     int lds16;   // 1: a and lds_bytes hold the 16-bit geometry (wgrad_lp16_kernel)
+    int nbuf;    // the 16-bit form's chunk ring depth: 2 (wgrad_lp16_kernel) or 3 / 4 (wgrad_lp16p_kernel)
     LpArgs a;
 };
 
@@ -900,10 +1097,16 @@ bool lp_plan(const ldm_conv_desc& d, LpPlan& p) {
     p.WM = p.BM == 128 ? 2 : 1;
     p.lds_bytes = 2 * lp_buf_floats(p.BM, qc, a.pitch_c) * 4;
     p.lds16 = 0;
+    p.nbuf = 2;
     if (p.lds_bytes > 160 * 1024) return false;
     const int tiles = ((a.M + p.BM - 1) / p.BM) * ((a.C + kLC - 1) / kLC);
+    static const int smax = [] {   // LDM_WGRAD_SPLITS: the largest K split (A/B timing; default 256)
+        const char* e = std::getenv("LDM_WGRAD_SPLITS");
+        const int v = e ? (int)std::strtol(e, nullptr, 0) : 256;
+        return v < 1 ? 1 : (v > 256 ? 256 : v);
+    }();
     int s = 1;
-    while (s < 256 && tiles * s < 256 && a.nchunk / (s * 2) >= 4) s *= 2;
+    while (s < smax && tiles * s < 256 && a.nchunk / (s * 2) >= 4) s *= 2;
     p.splits = s;
     a.per_split = (a.nchunk + s - 1) / s;
     p.a = a;
@@ -920,7 +1123,23 @@ bool lp16_plan(LpPlan& p) {
     while (pc % 128 != 8) pc += 8;
     a.pitch_c = pc;
     p.lds_bytes = 2 * lp16_buf_bytes(p.BM, p.QC, a.pitch_c) + 64;   // (+ the tail a last run may read past)
-    return p.lds_bytes <= 160 * 1024;
+    if (p.lds_bytes > 160 * 1024) return false;
+    // the ring (wgrad_lp16p_kernel): LDM_WGRAD_RING = 2 / 3 / 4 (default 4), shallower where the LDS is short
+    static const int ring = [] {
+        const char* e = std::getenv("LDM_WGRAD_RING");
+        const int v = e ? (int)std::strtol(e, nullptr, 0) : 4;
+        return v < 2 ? 2 : (v > 4 ? 4 : v);
+    }();
+    p.nbuf = 2;
+    for (int nb = ring; nb >= 3; --nb) {
+        const int bytes = nb * lp16_buf_bytes(p.BM, p.QC, a.pitch_c) + 1024 + 64;   // (+ the trash KB)
+        if (bytes <= 160 * 1024) {
+            p.nbuf = nb;
+            p.lds_bytes = bytes;
+            break;
+        }
+    }
+    return true;
 }
 
 template <int S, int KK, int BM, int WM, int QC, int DT>
@@ -934,6 +1153,24 @@ int launch_lp16(const LpPlan& p, hipStream_t st) {
     dim3 grid((p.a.C + kLC - 1) / kLC, (p.a.M + BM - 1) / BM, p.splits);
     hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * KK), p.lds_bytes, st, p.a);
     LDM_CHECK_LAUNCH("wgrad_lp16_kernel");
+    return 0;
+}
+
+template <int S, int KK, int BM, int WM, int QC, int DT, int NBUF>
+int launch_lp16p(const LpPlan& p, hipStream_t st) {
+    constexpr int NW = WM * KK;
+    // the slot counts the kernel assumes cover this plan's pieces (its window groups fit NG slots per wave)
+    LDM_REQUIRE((kLC * (p.a.pitch_c / 8) + 63) / 64 <= lp16_ng(S, KK, QC, NW) * NW, "wgrad ring: window slots");
+    LDM_REQUIRE(p.a.cols * p.a.rows == QC, "wgrad ring: chunk geometry");
+    auto kfn = wgrad_lp16p_kernel<S, KK, BM, WM, QC, DT, NBUF>;
+    static bool opted = false;
+    if (!opted) {
+        LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        opted = true;
+    }
+    dim3 grid((p.a.C + kLC - 1) / kLC, (p.a.M + BM - 1) / BM, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_lp16p_kernel");
     return 0;
 }
 
@@ -952,7 +1189,11 @@ int launch_lp_xs(const LpPlan& p, hipStream_t st) {
 }
 template <int S, int KK, int BM, int WM, int QC, int DT>
 int launch_lp_dt(const LpPlan& p, hipStream_t st) {
-    if (p.a.dense16 && p.a.gath16 && p.lds16) return launch_lp16<S, KK, BM, WM, QC, DT>(p, st);   // both 16-bit
+    if (p.a.dense16 && p.a.gath16 && p.lds16) {   // both 16-bit
+        if (p.nbuf == 4) return launch_lp16p<S, KK, BM, WM, QC, DT, 4>(p, st);
+        if (p.nbuf == 3) return launch_lp16p<S, KK, BM, WM, QC, DT, 3>(p, st);
+        return launch_lp16<S, KK, BM, WM, QC, DT>(p, st);
+    }
     if (p.a.dense16 || p.a.gath16) return launch_lp_xs<S, KK, BM, WM, QC, DT, DT>(p, st);
     return launch_lp_xs<S, KK, BM, WM, QC, DT, 0>(p, st);
 }
@@ -1108,7 +1349,7 @@ int wgrad2_storage16(const ldm_conv_desc& d) {
 
 // st16: bit 0 Dense, bit 1 Gath stored in 16 bits (-2: not on this layer's forms)
 int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, float* partial, int& splits, int dtype,
-               hipStream_t st, int st16) {
+               hipStream_t st, int st16, float* dw_direct) {
     wg::Plan p;
     if (!wg::plan(d, p)) return -1;
     if (dtype != LDM_DT_F32 && !wgrad_lp_disabled()) {   // 16-bit operands: the double-rate MFMA form
@@ -1128,6 +1369,10 @@ int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, fl
             lp.a.dense16 = st16 & 1;
             lp.a.gath16 = (st16 >> 1) & 1;
             splits = lp.splits;
+            if (lp.splits == 1 && dw_direct) {   // one K range: its partial is the gradient (no reduce launch)
+                lp.a.partial = dw_direct;
+                splits = 0;
+            }
             return dtype == LDM_DT_F16 ? wg::launch_lp<1>(lp, st) : wg::launch_lp<2>(lp, st);
         }
     }

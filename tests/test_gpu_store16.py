@@ -70,6 +70,37 @@ def test_kind3_conv_store16(cuda, case, dt):
     assert torch.equal(dw16, dw32)
 
 
+# weight gradients whose splits run several chunks each, so the chunk ring (wgrad_lp16p_kernel, LDM_WGRAD_RING)
+# cycles through all its buffers and the issue cursor crosses rows and samples: every chunk geometry of the form
+# (rows of 32 positions; 16 x 2; 16 x 1; 8 x 2) and the k3 / k4, stride 1 / 2, transposed layers of the step
+RING = {   # (B, Cin, H, W, Cout, k, stride, pad, out_pad, transposed)
+    "k3s2_64_128": (16, 64, 64, 256, 128, 3, 2, 1, 0, False),
+    "k3s2_128_256": (16, 128, 32, 128, 256, 3, 2, 1, 0, False),
+    "k3s1_32_64": (16, 32, 16, 64, 64, 3, 1, 1, 0, False),
+    "k3s2_rows16x2": (16, 64, 8, 32, 64, 3, 2, 1, 0, False),
+    "k3s1_rows16x2": (16, 64, 4, 16, 64, 3, 1, 1, 0, False),
+    "k3s1_rows16x1": (16, 32, 5, 16, 32, 3, 1, 1, 0, False),
+    "k3s1_rows8x2": (16, 64, 2, 8, 64, 3, 1, 1, 0, False),
+    "k4s2T_128_64": (16, 128, 32, 64, 64, 4, 2, 1, 0, True),
+    "k3s2T_256_128": (16, 256, 8, 32, 128, 3, 2, 1, 1, True),
+}
+
+
+@pytest.mark.parametrize("dt", [2, 1])
+@pytest.mark.parametrize("case", sorted(RING))
+def test_wgrad_ring_equals_fp32_storage(cuda, case, dt):
+    from ldm_amd import ops
+    B, Cin, H, W, Cout, k, s, p, op, tr = RING[case]
+    desc = ops.make_desc(B, Cin, H, W, Cout, k, k, s, p, op, tr)
+    x16, x32 = _q(_rand((B, Cin, H, W), 21), dt)
+    g16, g32 = _q(_rand((B, Cout, desc.Hout, desc.Wout), 22), dt)
+    assert ops.wgrad_storage16(desc, dt), case
+    dw32 = ops.conv_backward_weight(x32.to(cuda), g32.to(cuda), desc, dtype=dt)
+    dw16 = ops.conv_backward_weight(x16.to(cuda), g16.to(cuda), desc, dtype=dt)
+    torch.cuda.synchronize()
+    assert torch.equal(dw16, dw32), float((dw16 - dw32).abs().max())
+
+
 @pytest.mark.parametrize("k", [3, 4])
 def test_cin1_and_cout1_store16(cuda, k):
     """The Cin = 1 first layers (16-bit output), the 64 -> 1 output convT (16-bit input), the data gradient of

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("t", nargs="?", default="")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--maps32", action="store_true", help="fp32 storage of the maps (the UNet's small layers)")
     a = ap.parse_args()
     from ldm_amd import ops
     dev = torch.device("cuda:0")
@@ -34,14 +35,15 @@ def main():
     p, op = 1, 0
     desc = ops.make_desc(B, a.cin, a.h, a.w, a.cout, k, k, s, p, op, tr)
     dt = 2
-    x = (torch.rand(B, a.cin, a.h, a.w, device=dev) - 0.5).to(torch.bfloat16)
+    mt = torch.float32 if a.maps32 else torch.bfloat16
+    x = (torch.rand(B, a.cin, a.h, a.w, device=dev) - 0.5).to(mt)
     w = torch.randn((a.cin, a.cout, k, k) if tr else (a.cout, a.cin, k, k), device=dev) * 0.05
-    dy = (torch.rand(B, a.cout, desc.Hout, desc.Wout, device=dev) - 0.5).to(torch.bfloat16)
+    dy = (torch.rand(B, a.cout, desc.Hout, desc.Wout, device=dev) - 0.5).to(mt)
     if a.kind == "fwd":
         fn = lambda: ops.conv_forward(x, w, None, stride=s, padding=p, transposed=tr, output_padding=op, dtype=dt,  # noqa
-                                      out_dtype=torch.bfloat16)
+                                      out_dtype=mt)
     elif a.kind == "dgrad":
-        fn = lambda: ops.conv_backward_data(dy, w, desc, dtype=dt, out_dtype=torch.bfloat16)  # noqa
+        fn = lambda: ops.conv_backward_data(dy, w, desc, dtype=dt, out_dtype=mt)  # noqa
     else:
         fn = lambda: ops.conv_backward_weight(x, dy, desc, dtype=dt)  # noqa
     for _ in range(3):
