@@ -393,7 +393,7 @@ def run_train(args, world, rank, dev, M):
     # WRITE_SIZE summed over the step's dispatches), bf16 only (the passes profile the default line)
     traffic = None
     if args.dtype == "bf16" and world == 1:
-        for rnd in ("r04", "r03"):
+        for rnd in ("r05", "r04", "r03"):
             pth = os.path.join(ROOT, "profiles", rnd, "train_pmc.json")
             if os.path.exists(pth):
                 try:

@@ -374,16 +374,22 @@ __host__ __device__ constexpr int pk_tap(int i) {
 template <int PK>
 __host__ __device__ constexpr int pk_ntap(int p) { return PK == 2 ? 4 : (p == 0 ? 1 : (p == 3 ? 4 : 2)); }
 
-template <int BM, int NT, int SY, int DT, int NS, int PK = 0, int XS = 0>
+// WNW: waves along the positions.  2: a 2 x 2 wave grid (BM / 2 rows x 64 positions per wave); 1 (round 5,
+// BM = 128): four waves of 32 rows x all 128 positions, so no two waves load the same weight fragments — the
+// weights were 3x the window's bytes per block (four waves x 9 taps x 2 row tiles x 1 KB per window)
+template <int BM, int NT, int SY, int DT, int NS, int PK = 0, int XS = 0, int WNW = 2>
 __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
-    constexpr int MT = BM / 64;
+    constexpr int WMW = 4 / WNW;              // waves along the rows
+    constexpr int MT = BM / (32 * WMW);       // 32-row tiles per wave
+    constexpr int NJ = 4 / WNW;               // 32-position tiles per wave
+    static_assert(MT >= 1 && MT * 32 * WMW == BM, "wave grid");
     constexpr int NACC = PK ? 4 : 1;
     static_assert(!PK || (NT == (PK == 2 ? 16 : 9) && SY == 1),
                   "PK 1 / 2: the nine / sixteen (phase, tap) pairs of a k3 op1 / k4 p1 transposed conv");
     extern __shared__ __attribute__((aligned(16))) unsigned short img[];   // [2][image]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WNW, wn = wave % WNW;
     const int r = lane & 31, h = lane >> 5;
 
     int t = blockIdx.x;
@@ -463,16 +469,16 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
     };
 
     // ---- B fragments: this lane's two 32-column tiles, image position of tap 0's origin
-    int lb[2];
+    int lb[NJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int nl = wn * 64 + 32 * j + r;
+    for (int j = 0; j < NJ; ++j) {
+        const int nl = wn * 32 * NJ + 32 * j + r;
         const int rrow = nl >> a.cq_log2, cx = nl & ((1 << a.cq_log2) - 1);
         lb[j] = (rrow * SY * a.rowp + cx) * WP + 8 * h;
     }
 
     // ---- A fragments: rows mbase + 32 i + r, k = 16 (w & 1) + 8 h of chunk (w / 2) * NT + tap
-    const int mbase = mt * BM + wm * (BM / 2);
+    const int mbase = mt * BM + wm * 32 * MT;
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, 0x7ffffff0, 0x00020000);
     u16x8 af[NT][MT];
     // pair tp: phase PK ? pk_phase(tp) : ph, tap in that phase PK ? pk_tap(tp) : tp
@@ -488,13 +494,13 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         }
     };
 
-    floatx16 acc[NACC][MT][2];
+    floatx16 acc[NACC][MT][NJ];
 #pragma unroll
     for (int u = 0; u < NACC; ++u)
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) acc[u][i][j][q] = 0.f;
 
@@ -517,13 +523,13 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
             constexpr int tp = decltype(tpc)::value;
             constexpr int u = PK ? pk_phase<PK>(tp) : 0;
             const int to = (PK ? a.toff[u][pk_tap<PK>(tp)] : a.toff[ph][tp]) * WP;
-            u16x8 bf[2];
+            u16x8 bf[NJ];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const u16x8*>(bimg + lb[j] + to);
+            for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const u16x8*>(bimg + lb[j] + to);
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[u][i][j] = mma<DT>(af[tp][i], bf[j], acc[u][i][j]);
+                for (int j = 0; j < NJ; ++j) acc[u][i][j] = mma<DT>(af[tp][i], bf[j], acc[u][i][j]);
             loadA(wn1, tpc, af[tp]);   // this tap's set is free: the next window's weights for it
             __builtin_amdgcn_sched_barrier(0);
         });
@@ -539,10 +545,10 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
         // a single transposed-conv phase: its outputs sit two columns apart, so each lane stores its own values.
         // Per channel (i, q) the bias / BN constants are read once for the lane's two positions, and the
         // activation, the BN flag and the storage type are compile-time forms dispatched once (see below).
-        size_t obase[2];
+        size_t obase[NJ];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int nn = n0 + wn * 64 + 32 * j + r;
+        for (int j = 0; j < NJ; ++j) {
+            const int nn = n0 + wn * 32 * NJ + 32 * j + r;
             const int bb = a.fd_hw.div(nn);
             const int rr = nn - bb * HWq;
             const int qy = a.fd_w.div(rr);
@@ -568,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
                         beta = e.bn_b[co] - e.bn_m[co] * alpha;
                     }
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
+                    for (int j = 0; j < NJ; ++j) {
                         float v = acc[0][i][j][q];
                         if (e.bias) v = v + bias;
                         v = rnd(v);
@@ -626,15 +632,15 @@ __global__ __launch_bounds__(256, 2) void tconvw_kernel(WArgs a) {
                 constexpr int u = decltype(uc)::value;
                 if constexpr (PK && (u >> 1) != pass) return;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int nl = wn * 64 + 32 * j + r;
+                for (int j = 0; j < NJ; ++j) {
+                    const int nl = wn * 32 * NJ + 32 * j + r;
                     const int rr = nl >> a.cq_log2, cx = nl & (cq - 1);
                     const int col = rr * rowlen + (PK ? 2 * cx + (u & 1) : cx);
 #pragma unroll
                     for (int i = 0; i < MT; ++i)
 #pragma unroll
                         for (int q = 0; q < 16; ++q) {
-                            const int cl = wm * (BM / 2) + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                            const int cl = wm * 32 * MT + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
                             stg[cl * pitch + col] = acc[u][i][j][q];
                         }
                 }
@@ -745,6 +751,15 @@ static int layout(const ldm_conv_desc& d, int bm, PhaseTable& pt, int& Mpad, int
 // ---- the window form's geometry and launch ------------------------------------------------------------
 // Tap count and stride of one launch of the window form (template NT, SY); its image sizes (NS super-unit
 // slots per thread, LDS bytes) are checked here against the instance.
+// LDM_TCONVW_WNW: the 128-row instances' wave grid (1: four waves along the rows, default; 2: the 2 x 2 grid)
+static int tconvw_wnw() {
+    static const int v = [] {
+        const char* e = std::getenv("LDM_TCONVW_WNW");
+        return (e && e[0] == '2') ? 2 : 1;
+    }();
+    return v;
+}
+
 template <int BM, int NT, int SY, int DT, int NS, int PK, int XS>
 static int launch_wx(WArgs& a, hipStream_t st) {
     LDM_REQUIRE(a.nsu <= NS * 256, "tconvw: window larger than the instance's register slots");
@@ -754,11 +769,14 @@ static int launch_wx(WArgs& a, hipStream_t st) {
     const size_t lds = std::max((size_t)2 * (a.imgsz + WP) * 2, stage);
     (void)cq;
     auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS>;
+    if constexpr (BM == 128)
+        if (tconvw_wnw() == 1) kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS, 1>;
     if (lds > 64 * 1024) {
-        static bool opted = false;
-        if (!opted) {
+        static bool opted[2] = {false, false};
+        const int k = BM == 128 ? tconvw_wnw() - 1 : 1;
+        if (!opted[k]) {
             LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            opted = true;
+            opted[k] = true;
         }
     }
     const int64_t blocks = (int64_t)a.nph * a.nM * a.nN;
