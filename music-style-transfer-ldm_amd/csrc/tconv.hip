@@ -768,8 +768,10 @@ static int launch_wx(WArgs& a, hipStream_t st) {
     const size_t stage = NT == 4 ? 0 : (size_t)BM * ((PK ? 2 * BN : BN) + 4) * 4;
     const size_t lds = std::max((size_t)2 * (a.imgsz + WP) * 2, stage);
     (void)cq;
-    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS>;
-    if constexpr (BM == 128)
+    // (a 16-tap 128-row tile only on the four-waves-along-rows grid: two row tiles x 16 taps of fragments spill)
+    constexpr int WNW0 = (BM == 128 && NT == 16) ? 1 : 2;
+    auto kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS, WNW0>;
+    if constexpr (BM == 128 && WNW0 == 2)
         if (tconvw_wnw() == 1) kfn = tconvw_kernel<BM, NT, SY, DT, NS, PK, XS, 1>;
     if (lds > 64 * 1024) {
         static bool opted[2] = {false, false};
@@ -901,7 +903,7 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         // feeds >= 16 MFMAs per wave with one M tile (the decoder's 32 -> 128 convT and its data gradient); with
         // fewer taps x rows per window, or a window re-loaded by two M tiles, the per-chunk form is faster
         const bool dense = (nt * (bm / 64) >= 8 || any_density) && t.nM == 1;
-        const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && bm == 64 && ns <= 5 && dense) ||
+        const bool ok = (nt == 9 && ns <= (sy == 2 ? 4 : 2)) || (nt == 16 && sy == 2 && ns <= 5 && dense) ||
                         (nt == 4 && sy == 1 && ns <= 2 && dense);
         if (!ok) return 1;
     }
@@ -912,7 +914,7 @@ static int forward_window(const ldm_conv_desc& d, const TArgs& t, int bm, int dt
         int rc;
 #define TCW(BM_, NT_, SY_, NS_)                                                                          \
     (dt == LDM_DT_F16 ? launch_w<BM_, NT_, SY_, 1, NS_>(a, st) : launch_w<BM_, NT_, SY_, 2, NS_>(a, st))
-        if (nt == 16) rc = TCW(64, 16, 2, 5);
+        if (nt == 16) rc = bm == 128 ? TCW(128, 16, 2, 5) : TCW(64, 16, 2, 5);
         else if (nt == 9 && sy == 2) rc = bm == 128 ? TCW(128, 9, 2, 4) : TCW(64, 9, 2, 4);
         else if (nt == 9) rc = bm == 128 ? TCW(128, 9, 1, 2) : TCW(64, 9, 1, 2);
         else rc = bm == 128 ? TCW(128, 4, 1, 2) : TCW(64, 4, 1, 2);
@@ -1037,9 +1039,12 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
     // us, 128 -> 256 91.3 -> 53.1, 256 -> 256 52.5 -> 32.7, 128 -> 32 46.1 -> 22.7), and its k4 s2 p1 form (bit 3)
     // on the decoder's convT forwards (128 -> 64 113.2 -> 90.1 us, 32 -> 128 34.6 -> 26.0; train step 3.48-3.49 ->
     // 3.40-3.44 ms): default 11.  Bit 2: the single-phase window form for the 4-tap phases whatever their density.
+    // Bit 4 (round 5): the 16-tap convs with a 128-row pack on 128-row window tiles (four waves along the rows):
+    // the decoder convT 128 -> 64's data gradient 134.2 -> 100.8 us, train step 3.33-3.34 -> 3.28-3.31 ms
+    // (gpurun_out/k16): default 27.
     static const int win = [] {
         const char* e = std::getenv("LDM_TCONV_WIN");
-        return e ? (int)std::strtol(e, nullptr, 0) : 11;
+        return e ? (int)std::strtol(e, nullptr, 0) : 27;
     }();
     if (win) {
         const bool k16 = a.pt.nphase == 1 && a.pt.ntap[0] == 16;
@@ -1047,7 +1052,10 @@ int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x
         const bool k4t = a.pt.nphase == 4 && a.pt.ntap[0] == 4 && a.pt.ntap[3] == 4 && (win & 8);   // k4 s2 p1
         if (((k3t || k4t) && (win & 2)) || (!k3t && (win & 1))) {
             tc::TArgs t = a;
-            const bool r64 = k16 || k3t || k4t;   // the 64-row tilings (their image needs 5 slots / 4 acc sets)
+            // bit 4: a 16-tap conv with a 128-row pack keeps it (four waves along the rows, WNW 1: 16 taps x one
+            // row tile of weight fragments per wave fit the registers the 2 x 2 grid's two row tiles did not)
+            const bool k16w = k16 && p.tm == 2 && (win & 16);
+            const bool r64 = (k16 && !k16w) || k3t || k4t;   // the 64-row tilings (their image needs 5 slots / 4 acc sets)
             if (r64 && p.tm == 2) t.nM = a.Mpad / 64;   // the 128-row pack is also a valid 64-row tiling
             const int rc = tc::forward_window(d, t, r64 ? 64 : 64 * p.tm, p.tn, s, (win & 4) != 0, k4t);
             if (rc != 1) return rc;

@@ -4,6 +4,8 @@ Every function here computes on the HIP path.  When autograd needs a graph (grad
 requires grad) the call is wrapped in a torch.autograd.Function whose backward runs the matching HIP
 backward kernels (ldm_amd.backward); a missing backward raises instead of silently detaching.
 """
+import contextlib
+
 import torch
 
 from . import _lib as L
@@ -218,6 +220,24 @@ def sync_group_for(m):
     return getattr(m, "ldm_sync_group", False)
 
 
+_BN_COUNT_DEFER = []   # stack of lists collecting num_batches_tracked counters (bn_counts_deferred)
+
+
+@contextlib.contextmanager
+def bn_counts_deferred():
+    """Within the block, training-mode BatchNorms with a momentum collect their num_batches_tracked counters
+    instead of bumping each with its own one-element add kernel; on exit they are all bumped by one
+    torch._foreach_add_ (the train step's five BN layers: 5 launches -> 1).  The counters are read only by the
+    cumulative-average form (momentum None), which keeps the immediate add."""
+    _BN_COUNT_DEFER.append([])
+    try:
+        yield
+    finally:
+        counters = _BN_COUNT_DEFER.pop()
+        if counters:
+            torch._foreach_add_(counters, 1)
+
+
 def batchnorm(x, bn_module, act="none"):
     """nn.BatchNorm2d semantics (train: batch stats + running update; eval: running stats) + act."""
     m = bn_module
@@ -232,9 +252,13 @@ def batchnorm(x, bn_module, act="none"):
 
     momentum = m.momentum
     if m.training and m.track_running_stats:
-        m.num_batches_tracked.add_(1)
         if momentum is None:
+            m.num_batches_tracked.add_(1)
             momentum = 1.0 / float(m.num_batches_tracked.item())
+        elif _BN_COUNT_DEFER:
+            _BN_COUNT_DEFER[-1].append(m.num_batches_tracked)   # bumped by the enclosing bn_counts_deferred()
+        else:
+            m.num_batches_tracked.add_(1)
     rm = m.running_mean if (m.training and m.track_running_stats) else None
     rv = m.running_var if (m.training and m.track_running_stats) else None
 

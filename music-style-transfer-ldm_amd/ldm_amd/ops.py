@@ -448,7 +448,12 @@ def _stream_key(device):
 
 def scratch(name, nfloats, device):
     """Per-(device, stream) scratch buffer reused across stream-ordered calls (grown on demand): the train
-    step runs independent branches on their own streams (graphs.branch), each with its own buffers."""
+    step runs independent branches on their own streams (graphs.branch), each with its own buffers.
+
+    Memory: one buffer per (name, device, stream) at the largest size asked for, kept until release_workspaces()
+    — at config 3 (B = 32) the weight-gradient scratch is the largest (the split-K partials of the biggest layer,
+    ~38 MB) and exists once per stream that ran a backward (the origin stream and graphs.branch's pool, three
+    streams: ~0.1 GB); a program that creates streams of its own should call release_workspaces() when done."""
     key = (name, str(device), _stream_key(device))
     buf = _WS.get(key)
     if buf is None or buf.numel() < nfloats:
@@ -458,6 +463,13 @@ def scratch(name, nfloats, device):
 
 
 _SPLIT_WS = {}
+
+
+def release_workspaces():
+    """Drop every cached scratch / split-K workspace (all devices and streams); the next call re-allocates.
+    Not while a captured graph that uses them may still replay: the graph keeps the addresses it recorded."""
+    _WS.clear()
+    _SPLIT_WS.clear()
 
 
 def split_workspace(plan, device):

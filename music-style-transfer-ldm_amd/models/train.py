@@ -36,6 +36,7 @@ except ImportError:   # reference-style flat imports (models/ on sys.path)
     from loss import VGGishFeatureLoss, compression_loss, diffusion_loss, is_const_zero, style_loss
 
 from ldm_amd import dist as hdist
+from ldm_amd import functional as hF
 from ldm_amd import graphs as hgraphs
 from ldm_amd import ops
 from ldm_amd import optim as hoptim
@@ -210,7 +211,8 @@ class LDMTrainer:
 
     def _step_body(self, content_spec, style_spec, t, noise, ac, rec):
         with torch.autocast(device_type=self.device.type, enabled=self.autocast_enabled, **ac):
-            outputs = self.model(content_spec, style_spec, t, noise=noise)
+            with hF.bn_counts_deferred():   # the BN layers' num_batches_tracked: one add launch, not five
+                outputs = self.model(content_spec, style_spec, t, noise=noise)
             noise_pred = outputs["noise_pred"]
             noise = outputs["noise"]
             z_0 = outputs["z_0"]
