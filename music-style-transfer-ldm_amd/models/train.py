@@ -293,8 +293,8 @@ class LDMTrainer:
             self._graph, self._graph_in, self._graph_out, self._graph_sig = g, static, outs, sig
             self._graph_tables = tables
         for dst, src in zip(self._graph_in, args):
-            if dst is not None:
-                dst.copy_(src)
+            if dst is not None and (src.data_ptr() != dst.data_ptr() or src.shape != dst.shape):
+                dst.copy_(src)      # (a caller that fills graph_inputs() in place passes them back: no copy)
         if self._packset is not None and not self._packset.current():
             self._packset.repack()     # the weights changed outside the graph since its last re-pack
         self._graph.replay()
@@ -306,6 +306,12 @@ class LDMTrainer:
         if self._packset is not None:
             self._packset.rekey()      # the replay ended by re-packing them from the updated weights
         return self._losses(self._graph_out)
+
+    def graph_inputs(self):
+        """The captured step's static input buffers (content, style, t, noise; None until the graph exists or
+        for an input drawn inside it).  A caller may fill them in place and pass them to train_step, which
+        then skips the copy into them."""
+        return None if self._graph is None else tuple(self._graph_in)
 
     def train_epoch(self, epoch):
         self.model.train()
