@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic_step.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "pmc_traffic_step.json"),
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
     a = ap.parse_args()
     if a.batch is None:
@@ -640,7 +640,7 @@ def main():
                 traffic = None
         peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
         if args.dtype != "fp32":
-            traffic = None     # profiles/r04/pmc_traffic_step.json holds the fp32 kernels' counters
+            traffic = None     # profiles/r05/pmc_traffic_step.json holds the fp32 kernels' counters
         if dk.get("bound") == "hbm":   # a byte-bound launch (the folded-value bottleneck, the attentions)
             result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "hbm",
                                   "achieved": dk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
