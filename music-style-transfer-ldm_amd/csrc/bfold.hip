@@ -105,6 +105,54 @@ __global__ __launch_bounds__(64 * NWV) void bneck_pv_kernel(const float* __restr
     *reinterpret_cast<floatx4*>(y + ((size_t)b * L + l) * E + co) = o;
 }
 
+// CA1's probabilities alone, one block of eight waves per (sample, head) (round 5): ca1_bneck_kernel's producer
+// as a kernel of its own — the scores' E = 512 contraction split over the eight waves (v_mfma_f32_16x16x4_f32,
+// two 16-byte loads per lane per 16 e), the partial score tiles summed in wave order in LDS, the bias and the
+// softmax over the 16 keys by wave 0, P stored with plain stores (the next launch reads it).  The generic
+// attention kernel's PONLY instance runs the same contraction through its query / key staging.
+__global__ __launch_bounds__(512) void ca1_probs_kernel(const float* __restrict__ z, const float* __restrict__ kf,
+                                                         const float* __restrict__ bfv, float* __restrict__ p) {
+    __shared__ floatx4 red[8][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane & 15, lg = lane >> 4;
+    const int b = blockIdx.x / HEADS, h = blockIdx.x % HEADS;
+    const int e0 = wave * (E / 8);
+    const float* za = z + ((size_t)b * L + col) * E + e0 + 4 * lg;
+    const float* ka = kf + (((size_t)b * HEADS + h) * S + col) * E + e0 + 4 * lg;
+    floatx4 zz[4], kk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        zz[i] = *reinterpret_cast<const floatx4*>(za + 16 * i);
+        kk[i] = *reinterpret_cast<const floatx4*>(ka + 16 * i);
+    }
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zz[i][j], kk[i][j], acc, 0, 0, 0);
+    red[wave][lane] = acc;
+    __syncthreads();
+    if (wave != 0) return;
+    floatx4 v = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) v = v + red[w][lane];
+    const float bias = bfv[((size_t)b * HEADS + h) * S + col];
+    float* pb = p + ((size_t)(b * HEADS + h) * L) * S;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float x = v[r] + bias;
+        float mx = x;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        const float ex = expf(x - mx);
+        float sum = ex;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        pb[(size_t)(4 * lg + r) * S + col] = ex / sum;
+    }
+}
+
 // CA1's probabilities and the bottleneck in ONE launch (round 5): blocks [0, 4B) are producers, one per (sample,
 // head), each forming P_h = softmax(z4 . kf_h + bf_h) for its sample (eight waves split the E = 512 contraction,
 // v_mfma_f32_16x16x4_f32, meeting in LDS in wave order); blocks [4B, 4B + 32B) are bneck_pv_kernel's consumers,
@@ -286,6 +334,23 @@ int bneck_pv(const float* u, const float* p, const float* pb, float* y, int B, i
     return 0;
 }
 
+// CA1's probabilities on ca1_probs_kernel (LDM_CA1P_FORM=0: the generic attention kernel's PONLY instance)
+bool ca1_probs_own() {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_CA1P_FORM");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+int ca1_probs(const float* z, const float* kf, const float* bfv, float* p, int B, hipStream_t st) {
+    LDM_REQUIRE(z && kf && bfv && p && B > 0, "CA1 probabilities: bad argument");
+    LDM_REQUIRE((((uintptr_t)z | (uintptr_t)kf) & 15) == 0, "CA1 probabilities: operands must be 16-byte aligned");
+    hipLaunchKernelGGL(bf::ca1_probs_kernel, dim3(B * bf::HEADS), dim3(512), 0, st, z, kf, bfv, p);
+    LDM_CHECK_LAUNCH("ca1_probs_kernel");
+    return 0;
+}
+
 // CA1's probabilities + the bottleneck in one launch (ca1_bneck_kernel).  cnt: (2B + 1) x 64 zero-filled int32 (zero
 // again after every launch).  Measured in the loop (config 2, gpurun_out/ca1f, ca1f2; per iteration, two rounds):
 // counters on one line 80.83 / 81.21 us (256 blocks polling and adding on one line serialise), one counter per
@@ -334,4 +399,8 @@ extern "C" int ldm_bneck_pv(const float* u, const float* p, const float* pos_bia
 extern "C" int ldm_ca1_bneck(const float* z4, const float* kf, const float* bf, const float* u, const float* pos_bias,
                              float* p, float* y, int32_t* cnt, int32_t B, int32_t dtype, void* stream) {
     return ldm::ca1_bneck(z4, kf, bf, u, pos_bias, p, y, cnt, B, dtype, (hipStream_t)stream);
+}
+
+extern "C" int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, int32_t B, void* stream) {
+    return ldm::ca1_probs(z4, kf, bf, p, B, (hipStream_t)stream);
 }

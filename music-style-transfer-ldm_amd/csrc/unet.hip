@@ -162,6 +162,9 @@ static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* 
 }
 
 // The reverse loop's bottleneck on CA1's folded values (bfold.hip) at the canonical plane, B <= 8.
+bool ca1_probs_own();   // (bfold.hip)
+int ca1_probs(const float* z, const float* kf, const float* bfv, float* p, int B, hipStream_t st);
+
 static bool use_bneck_fold(const ldm_unet_shape& s, const ldm_unet_weights* w) {
     return w && w->use_fold && w->use_step && w->step_bneck_w && s.C == 32 && s.nf == 64 &&
            bneck_fold_supported(s.B, s.H, s.W);
@@ -373,7 +376,8 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
         if (ca1_bneck_fused()) {
             LDM_TRY(ca1_bneck(ws.z4, ws.kf1, ws.bf1, ws.ubn, w.step_pb[1], ws.p1, ws.zb, ws.cnt1, s.B, w.step_dtype, st));
         } else {
-            LDM_TRY(attention_folded_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, 512, 4, L1, L1, st));
+            if (ca1_probs_own()) LDM_TRY(ca1_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, st));
+            else LDM_TRY(attention_folded_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, 512, 4, L1, L1, st));
             LDM_TRY(bneck_pv(ws.ubn, ws.p1, w.step_pb[1], ws.zb, s.B, w.step_dtype, st));
         }
         return run(5, 8);

@@ -158,3 +158,21 @@ def test_ca1_bneck_one_launch_rounds_output_to_16_bits(cuda, dt, t16):
     assert int(cnt.abs().sum()) == 0
     assert torch.equal(y16, y16.to(t16).float())
     assert rel_err(y16.cpu().numpy(), y32.cpu().numpy()) < (1e-3 if dt == 1 else 8e-3)
+
+
+@pytest.mark.parametrize("B", [1, 8])
+def test_ca1_probs_kernel_matches_float64(cuda, B):
+    """The reverse loop's CA1 probabilities kernel (ca1_probs_kernel) against float64 and against the generic
+    attention kernel's probabilities-only instance."""
+    from ldm_amd import _lib as L
+    ops = _operands(B, 300 + B)
+    p64, _ = _reference64(*ops)
+    z4, kf, bf, kv, wf, pb = (t.to(cuda).contiguous() for t in ops)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = torch.empty(B, 4, 16, 16, device=cuda)
+    p2 = torch.empty(B, 4, 16, 16, device=cuda)
+    L.call("ldm_ca1_probs", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(p), B, st)
+    L.call("ldm_attention_folded_probs", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(p2), B, 512, 4, 16, 16, st)
+    torch.cuda.synchronize()
+    assert rel_err(p.cpu().numpy(), p64.numpy()) < 1e-5
+    assert rel_err(p.cpu().numpy(), p2.cpu().numpy()) < 1e-6
