@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--maps32", action="store_true", help="fp32 storage of the maps (the UNet's small layers)")
+    ap.add_argument("--x32", action="store_true", help="fp32 input map, 16-bit output (the encoders' first layers)")
     a = ap.parse_args()
     from ldm_amd import ops
     dev = torch.device("cuda:0")
@@ -36,7 +37,7 @@ def main():
     desc = ops.make_desc(B, a.cin, a.h, a.w, a.cout, k, k, s, p, op, tr)
     dt = 2
     mt = torch.float32 if a.maps32 else torch.bfloat16
-    x = (torch.rand(B, a.cin, a.h, a.w, device=dev) - 0.5).to(mt)
+    x = (torch.rand(B, a.cin, a.h, a.w, device=dev) - 0.5).to(torch.float32 if a.x32 else mt)
     w = torch.randn((a.cin, a.cout, k, k) if tr else (a.cout, a.cin, k, k), device=dev) * 0.05
     dy = (torch.rand(B, a.cout, desc.Hout, desc.Wout, device=dev) - 0.5).to(mt)
     if a.kind == "fwd":
