@@ -1124,10 +1124,10 @@ bool lp16_plan(LpPlan& p) {
     a.pitch_c = pc;
     p.lds_bytes = 2 * lp16_buf_bytes(p.BM, p.QC, a.pitch_c) + 64;   // (+ the tail a last run may read past)
     if (p.lds_bytes > 160 * 1024) return false;
-    // the ring (wgrad_lp16p_kernel): LDM_WGRAD_RING = 2 / 3 / 4 (default 4), shallower where the LDS is short
+    // the ring (wgrad_lp16p_kernel): LDM_WGRAD_RING = 2 / 3 / 4 (default 3: train step 3.279-3.282 ms against 3.288-3.304 with 4, gpurun_out/trab7), shallower where the LDS is short
     static const int ring = [] {
         const char* e = std::getenv("LDM_WGRAD_RING");
-        const int v = e ? (int)std::strtol(e, nullptr, 0) : 4;
+        const int v = e ? (int)std::strtol(e, nullptr, 0) : 3;
         return v < 2 ? 2 : (v > 4 ? 4 : v);
     }();
     p.nbuf = 2;
