@@ -855,14 +855,22 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16_kernel(LpArgs a) {
     }
 }
 
-// The same sums on an NBUF-deep ring of chunk buffers (round 5): the double-buffered form keeps one chunk's
-// DMAs (~25 KB per CU) in flight, which at the grid's one block per CU leaves the HBM pipe latency-bound
-// (tools/pmc_one_conv.sh: 64 -> 128 s2 weight gradient, 172 MB fetched in ~60 us, waves mostly waiting).  Here
-// chunks ch + 1 .. ch + NBUF - 2 are in flight while chunk ch computes.  Every wave issues exactly ND + NG DMAs
-// per chunk (slots past the tile's pieces load nothing into a trash KB), so "chunk ch landed" is one
-// vmcnt immediate; the per-slot offsets are chunk-invariant and computed once (the chunk loop walks the
-// chunk coordinates without divisions).  Same blocks, chunks, k-steps and fragments as wgrad_lp16_kernel: the
-// sums are bitwise those of the double-buffered form.
+// The same sums on an NBUF-deep ring of chunk buffers: the double-buffered form keeps one chunk's DMAs (~25 KB
+// per CU) in flight, which at the grid's one block per CU leaves the HBM pipe latency-bound (tools/pmc_one_conv.sh:
+// 64 -> 128 s2 weight gradient, 172 MB fetched in ~60 us, waves mostly waiting).  Here chunks ch + 1 .. ch + NBUF - 1
+// are in flight while chunk ch computes.  Every wave issues exactly NL = ND + NG DMAs per chunk (slots past the
+// tile's pieces load nothing into a trash KB), so "chunk ch landed" is one vmcnt immediate; the per-slot offsets
+// are chunk-invariant and computed once (the chunk loop walks the chunk coordinates without divisions).  Same
+// blocks, chunks, k-steps and fragments as wgrad_lp16_kernel: the sums are bitwise those of the double-buffered
+// form.
+// Synchronisation (round 6; the round-5 form waited one chunk short and was rescued by hipcc): at iteration k the
+// chunks k .. min(n - 1, k + NBUF - 2) are outstanding, so "chunk k landed" is vmcnt(ahead * NL) with ahead the
+// chunks issued after k; then a RAW s_barrier (every wave's share of chunk k landed, every wave done reading chunk
+// k - 1), then chunk k + NBUF - 1 is issued into chunk k - 1's buffer.  hipcc would drain the ring twice per
+// chunk: __syncthreads()'s workgroup fence waits vmcnt(0) (an LDS DMA is a pending LDS write), and an ordinary
+// ds_read after any LDS DMA waits for all of them (it may alias).  So the wait + barrier is one asm statement
+// and the fragment reads are asm ds_read_b128 that end in their own lgkmcnt(0) (cdna_hip_programming.md §5,
+// "Pipelining across barriers"): the emitted loop holds no vmcnt but the counted one.
 __host__ __device__ constexpr int lp16_pitch(int S, int KK, int rows, int cols) {
     const int wr = (rows - 1) * S + KK, wca = (7 + (cols - 1) * S + KK + 7) / 8 * 8;
     int pc = wr * wca;
@@ -877,10 +885,19 @@ __host__ __device__ constexpr int lp16_ng(int S, int KK, int QC, int NW) {
     return (groups + NW - 1) / NW;
 }
 
+// this wave's DMAs but the N youngest have landed, then the block's raw barrier (no fence: see above)
 template <int N>
-__device__ __forceinline__ void lp_wait_vm() {
+__device__ __forceinline__ void lp_wait_vm_barrier() {
     static_assert(N >= 0 && N <= 63, "vmcnt immediate");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// a ds_read_b128 the compiler's waitcnt pass does not see (the caller waits lgkmcnt(0) before the use)
+__device__ __forceinline__ u32x4 lp_lds_read(const char* p) {
+    u32x4 v;
+    const unsigned addr = (unsigned)(uintptr_t)(lds_ptr_t)p;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
 }
 
 template <int S, int KK, int BM, int WM, int QC, int DT, int NBUF>
@@ -889,7 +906,7 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16p_kernel(LpArgs a) {
     constexpr int PPR = QC / 8, RPI = 64 / PPR, NKS = QC / 16;
     constexpr int NDG = BM / RPI, ND = (NDG + NW - 1) / NW, NG = lp16_ng(S, KK, QC, NW), NL = ND + NG;
     static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
-    static_assert(NBUF >= 3 && (NBUF - 2) * NL <= 63, "ring depth");
+    static_assert(NBUF >= 3 && (NBUF - 2) * NL <= 63, "ring depth (vmcnt immediate)");
     extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -990,20 +1007,20 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16p_kernel(LpArgs a) {
     };
     const int n = ch_end - ch_begin;
 #pragma unroll
-    for (int k = 0; k < NBUF - 2; ++k)
+    for (int k = 0; k < NBUF - 1; ++k)
         if (k < n) issue(k, ib, iqy, iqx), advance();
-    int buf = 0, ibuf = NBUF - 2;
+    int buf = 0, ibuf = NBUF - 1;   // ibuf = (k + NBUF - 1) % NBUF: chunk k - 1's buffer
     for (int k = 0; k < n; ++k) {
-        // chunks k + 1 .. min(n - 1, k + NBUF - 2) may stay in flight
+        // outstanding: chunks k .. k + ahead; chunk k must land, the ahead younger ones may stay in flight
         const int ahead = min(n - 1 - k, NBUF - 2);
         if constexpr (NBUF == 3) {
-            if (ahead >= 1) lp_wait_vm<NL>(); else lp_wait_vm<0>();
+            if (ahead >= 1) lp_wait_vm_barrier<NL>(); else lp_wait_vm_barrier<0>();
         } else {
             static_assert(NBUF == 4, "ring depth 3 or 4");
-            if (ahead >= 2) lp_wait_vm<2 * NL>(); else if (ahead == 1) lp_wait_vm<NL>(); else lp_wait_vm<0>();
+            if (ahead >= 2) lp_wait_vm_barrier<2 * NL>(); else if (ahead == 1) lp_wait_vm_barrier<NL>(); else lp_wait_vm_barrier<0>();
         }
-        __syncthreads();   // chunk k landed for every wave; every wave is done with chunk k - 1's buffer
-        if (k + NBUF - 2 < n) {
+        // chunk k landed for every wave; every wave is done with chunk k - 1's buffer: refill it
+        if (k + NBUF - 1 < n) {
             issue(ibuf, ib, iqy, iqx);
             advance();
         }
@@ -1012,15 +1029,22 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16p_kernel(LpArgs a) {
         buf = buf + 1 == NBUF ? 0 : buf + 1;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
+            u32x4 ra[MF], rb[NB];
+#pragma unroll
+            for (int f = 0; f < MF; ++f) ra[f] = lp_lds_read(sb + aoff[ks][f]);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) rb[i] = lp_lds_read(sb + boff[ks] + 16 * i);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int f = 0; f < MF; ++f) asm volatile("" : "+v"(ra[f]));
+#pragma unroll
+            for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(rb[i]));
             u16x8 fa[MF];
 #pragma unroll
-            for (int f = 0; f < MF; ++f) fa[f] = *reinterpret_cast<const u16x8*>(sb + aoff[ks][f]);
+            for (int f = 0; f < MF; ++f) fa[f] = __builtin_bit_cast(u16x8, ra[f]);
             unsigned w[4 * NB];
 #pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const uint4 p = *reinterpret_cast<const uint4*>(sb + boff[ks] + 16 * i);
-                w[4 * i + 0] = p.x, w[4 * i + 1] = p.y, w[4 * i + 2] = p.z, w[4 * i + 3] = p.w;
-            }
+            for (int i = 0; i < NB; ++i) w[4 * i + 0] = rb[i][0], w[4 * i + 1] = rb[i][1], w[4 * i + 2] = rb[i][2], w[4 * i + 3] = rb[i][3];
             static_for<0, KK>([&](auto kxc) {
                 constexpr int kx = decltype(kxc)::value;
                 const u16x8 fb = lp16_frag<S, 7 + kx, 4 * NB>(w);

@@ -58,9 +58,14 @@ def capture(graph, stream=None, pool=None):
             ok = True
         finally:
             _CAPTURES.pop()
-            if ok:
-                for side in rec[1].values():
+            # joined whether or not the body succeeded: an unjoined fork would make the capture's end raise
+            # hipErrorStreamCaptureUnjoined and hide the body's own exception
+            for side in rec[1].values():
+                try:
                     origin.wait_stream(side)
+                except Exception:
+                    if ok:
+                        raise
 
 
 def captured_side_streams():
