@@ -210,16 +210,9 @@ int32_t ldm_bneck_fold_supported(int32_t B, int32_t H, int32_t W);
 int ldm_bneck_fold_values(const float* w_fold, const float* kv, float* u, int32_t B, void* stream);
 int ldm_bneck_pv(const float* u, const float* p, const float* pos_bias, float* y, int32_t B, int32_t dtype,
                  void* stream);
-/* CA1's probabilities (ldm_attention_folded_probs) and ldm_bneck_pv in ONE launch (the reverse loop with
- * LDM_CA1_FUSED=1; measured 0.8-1.4 us per iteration slower than the two launches): 4B producer blocks write P [B,4,16,16] to p, 32B consumer blocks wait for their
- * sample's four heads (in-launch hand-off) and write y as ldm_bneck_pv.  z4 token-major [B,16,512], kf
- * [B,4,16,512], bf [B,4,16].  cnt: (2B + 1) x 64 int32, zero-filled before the first call (counter i at cnt[64 i];
- * every call leaves them zero; cnt[128 B] != 0 afterwards reports a timed-out wait, whose outputs are NaN).  B <= 8. */
 /* CA1's probabilities P [B,4,16,16] only, one block of eight waves per (sample, head): the reverse loop's form
  * (LDM_CA1P_FORM=0 keeps ldm_attention_folded_probs).  z4 token-major [B,16,512], kf [B,4,16,512], bf [B,4,16]. */
 int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, int32_t B, void* stream);
-int ldm_ca1_bneck(const float* z4, const float* kf, const float* bf, const float* u, const float* pos_bias, float* p,
-                  float* y, int32_t* cnt, int32_t B, int32_t dtype, void* stream);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that

@@ -27,7 +27,6 @@ namespace bf {
 
 constexpr int E = 512, HEADS = 4, DH = 128, S = 16, L = 16, TAPS = 9;
 constexpr int K = TAPS * HEADS * S;   // 576: k = (t * HEADS + h) * S + s
-constexpr int kCntPad = 64;           // ca1_bneck_kernel: one hand-off counter per 256-byte line
 
 // U[b][co][k] = sum_d W'[co][h*DH + d][t] * V[b][h][s][d]; kv = the style K/V projection [B][2E][S] (V rows
 // E + h*DH + d, channel-major).  Block (b, h, 32-row co tile), 288 threads = 32 co x 9 taps, V_h staged in LDS.
@@ -105,8 +104,7 @@ __global__ __launch_bounds__(64 * NWV) void bneck_pv_kernel(const float* __restr
     *reinterpret_cast<floatx4*>(y + ((size_t)b * L + l) * E + co) = o;
 }
 
-// CA1's probabilities alone, one block of eight waves per (sample, head) (round 5): ca1_bneck_kernel's producer
-// as a kernel of its own — the scores' E = 512 contraction split over the eight waves (v_mfma_f32_16x16x4_f32,
+// CA1's probabilities alone, one block of eight waves per (sample, head) (round 5) — the scores' E = 512 contraction split over the eight waves (v_mfma_f32_16x16x4_f32,
 // two 16-byte loads per lane per 16 e), the partial score tiles summed in wave order in LDS, the bias and the
 // softmax over the 16 keys by wave 0, P stored with plain stores (the next launch reads it).  The generic
 // attention kernel's PONLY instance runs the same contraction through its query / key staging.
@@ -151,135 +149,6 @@ __global__ __launch_bounds__(512) void ca1_probs_kernel(const float* __restrict_
         for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
         pb[(size_t)(4 * lg + r) * S + col] = ex / sum;
     }
-}
-
-// CA1's probabilities and the bottleneck in ONE launch (round 5): blocks [0, 4B) are producers, one per (sample,
-// head), each forming P_h = softmax(z4 . kf_h + bf_h) for its sample (eight waves split the E = 512 contraction,
-// v_mfma_f32_16x16x4_f32, meeting in LDS in wave order); blocks [4B, 4B + 32B) are bneck_pv_kernel's consumers,
-// which issue their U loads first and then wait for their sample's four heads.  The launch boundary between the two
-// kernels (and the probabilities kernel's own ramp) is what the fusion removes.  Hand-off (MI355X_MICROARCH.md,
-// Valid forms, the sc1 row): the producer's one storing wave writes P with sc1 stores, drains them (vmcnt(0)) and
-// its lane 0 adds to the sample's counter (agent scope); a consumer's thread 0 polls that counter (relaxed agent
-// loads), the block joins a barrier, and P is read with sc1 loads only.  The whole grid (4B + 32B <= 288 blocks of
-// NWV waves) is resident at once (two blocks per CU fit), so no dispatch order is assumed; the poll is bounded
-// and a consumer that times out writes NaN and sets cnt[2B].  cnt [2B + 1] int32: per-sample producer arrivals,
-// per-sample consumer passes (the last consumer of a sample zeroes both), the timeout word, each at cnt[i * 64] (one
-// per 256-byte line: the polls and adds of 256 blocks on one line serialised); zero between launches.
-template <int DT, int NWV>
-__global__ __launch_bounds__(64 * NWV) void ca1_bneck_kernel(const float* __restrict__ z, const float* __restrict__ kf,
-                                                             const float* __restrict__ bfv, const float* __restrict__ u,
-                                                             const float* __restrict__ pbias, float* __restrict__ p,
-                                                             float* __restrict__ y, int32_t* __restrict__ cnt, int B) {
-    constexpr int NCH = K / 16, PER = NCH / NWV;
-    static_assert(NCH % NWV == 0 && NWV >= 8, "chunks per wave; eight producer waves");
-    __shared__ floatx4 red[NWV][64];
-    __shared__ int to_flag;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int col = lane & 15, lg = lane >> 4;
-    const int nP = B * HEADS;
-    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, B * HEADS * L * S * 4, 0x00020000);
-    if ((int)blockIdx.x < nP) {
-        // ---- producer (b, h): scores D[l][s] = sum_e z4[b][l][e] kf[b][h][s][e]; lane (col, lg) feeds A[col][k] =
-        //      z4[col][e] and B[k][col] = kf[col][e] with e = e0 + 16 i + 4 lg + j at step (i, j)
-        const int b = blockIdx.x / HEADS, h = blockIdx.x % HEADS;
-        if (wave < 8) {
-            const int e0 = wave * (E / 8);
-            const float* za = z + ((size_t)b * L + col) * E + e0 + 4 * lg;
-            const float* ka = kf + (((size_t)b * HEADS + h) * S + col) * E + e0 + 4 * lg;
-            floatx4 zz[4], kk[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                zz[i] = *reinterpret_cast<const floatx4*>(za + 16 * i);
-                kk[i] = *reinterpret_cast<const floatx4*>(ka + 16 * i);
-            }
-            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zz[i][j], kk[i][j], acc, 0, 0, 0);
-            red[wave][lane] = acc;
-        }
-        __syncthreads();
-        if (wave != 0) return;
-        floatx4 v = red[0][lane];
-#pragma unroll
-        for (int w = 1; w < 8; ++w) v = v + red[w][lane];
-        // D row l = 4 lg + r, column s = col: softmax over the 16 lanes of one lg group
-        const float bias = bfv[((size_t)b * HEADS + h) * S + col];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float x = v[r] + bias;
-            float mx = x;
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-            const float ex = expf(x - mx);
-            float sum = ex;
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-            const int off = ((((b * HEADS + h) * L) + 4 * lg + r) * S + col) * 4;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, ex / sum), pr, off, 0, 16);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every sc1 store of the block's one storing wave landed
-        if (lane == 0) __hip_atomic_fetch_add(cnt + b * kCntPad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    // ---- consumer (16-row co tile, sample b): bneck_pv_kernel's contraction
-    const int cblk = (int)blockIdx.x - nP;
-    const int co0 = (cblk % (E / 16)) * 16, b = cblk / (E / 16);
-    const int row = lane & 15;
-    const int l = lane & 15, oy = l >> 3, ox = l & 7;
-    const floatx4* ua = reinterpret_cast<const floatx4*>(u + ((size_t)b * E + co0 + row) * K) + lg;
-    floatx4 fa[PER], fb[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) fa[i] = ua[(wave * PER + i) * 4];   // (independent of P: in flight during the wait)
-    const floatx4 bias = *reinterpret_cast<const floatx4*>(pbias + (size_t)l * E + co0 + 4 * lg);
-    if (threadIdx.x == 0) {
-        int spins = 0, timed_out = 0;
-        while (__hip_atomic_load(cnt + b * kCntPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < HEADS) {
-            if (++spins > (1 << 18)) {   // bounded: report instead of hanging, and poison this block's output
-                __hip_atomic_store(cnt + 2 * B * kCntPad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                timed_out = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (__hip_atomic_fetch_add(cnt + (B + b) * kCntPad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E / 16 - 1) {
-            __hip_atomic_store(cnt + b * kCntPad, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(cnt + (B + b) * kCntPad, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        to_flag = timed_out;
-    }
-    __syncthreads();
-    const int poison = to_flag;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = wave * PER + i;   // chunk = (tap, head)
-        const int t = c / HEADS, h = c % HEADS;
-        const int iy = oy - 1 + t / 3, ix = ox - 1 + t % 3;
-        const bool in = (unsigned)iy < 2u && (unsigned)ix < 8u;
-        const int off = ((((b * HEADS + h) * L) + (in ? iy * 8 + ix : 0)) * S + 4 * lg) * 4;
-        const floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(pr, off, 0, 16));
-        fb[i] = in ? v : floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[i][j], acc, 0, 0, 0);
-    red[wave][lane] = acc;
-    __syncthreads();
-    if (wave != 0) return;
-    floatx4 v = red[0][lane];
-#pragma unroll
-    for (int w = 1; w < NWV; ++w) v = v + red[w][lane];
-    floatx4 o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        float sv = round16(v[r] + bias[r], DT);
-        o[r] = poison ? __builtin_nanf("") : (sv < 0.f ? 0.f : sv);
-    }
-    *reinterpret_cast<floatx4*>(y + ((size_t)b * L + l) * E + co0 + 4 * lg) = o;
 }
 
 }  // namespace bf
@@ -351,36 +220,6 @@ int ca1_probs(const float* z, const float* kf, const float* bfv, float* p, int B
     return 0;
 }
 
-// CA1's probabilities + the bottleneck in one launch (ca1_bneck_kernel).  cnt: (2B + 1) x 64 zero-filled int32 (zero
-// again after every launch).  Measured in the loop (config 2, gpurun_out/ca1f, ca1f2; per iteration, two rounds):
-// counters on one line 80.83 / 81.21 us (256 blocks polling and adding on one line serialise), one counter per
-// 256-byte line 74.11 / 74.75, the two launches 73.28 / 73.32: the producers' scores + softmax + hand-off sit on
-// the critical path and cost more than the launch boundary they remove.  Off by default; LDM_CA1_FUSED=1 runs it.
-bool ca1_bneck_fused() {
-    static const bool on = [] {
-        const char* e = std::getenv("LDM_CA1_FUSED");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
-int ca1_bneck(const float* z, const float* kf, const float* bfv, const float* u, const float* pb, float* p, float* y,
-              int32_t* cnt, int B, int dtype, hipStream_t st) {
-    LDM_REQUIRE(z && kf && bfv && u && pb && p && y && cnt && B > 0 && B <= 8, "CA1 + bottleneck: bad argument");
-    LDM_REQUIRE((((uintptr_t)z | (uintptr_t)kf | (uintptr_t)u | (uintptr_t)pb | (uintptr_t)y) & 15) == 0,
-                "CA1 + bottleneck: operands must be 16-byte aligned");
-    LDM_REQUIRE(dtype >= LDM_DT_F32 && dtype <= LDM_DT_BF16, "CA1 + bottleneck: unknown operand precision");
-    const dim3 grid(B * bf::HEADS + B * (bf::E / 16));
-    if (dtype == LDM_DT_F16)
-        hipLaunchKernelGGL((bf::ca1_bneck_kernel<LDM_DT_F16, 9>), grid, dim3(576), 0, st, z, kf, bfv, u, pb, p, y, cnt, B);
-    else if (dtype == LDM_DT_BF16)
-        hipLaunchKernelGGL((bf::ca1_bneck_kernel<LDM_DT_BF16, 9>), grid, dim3(576), 0, st, z, kf, bfv, u, pb, p, y, cnt, B);
-    else
-        hipLaunchKernelGGL((bf::ca1_bneck_kernel<0, 9>), grid, dim3(576), 0, st, z, kf, bfv, u, pb, p, y, cnt, B);
-    LDM_CHECK_LAUNCH("ca1_bneck_kernel");
-    return 0;
-}
-
 }  // namespace ldm
 
 extern "C" int32_t ldm_bneck_fold_supported(int32_t B, int32_t H, int32_t W) {
@@ -394,11 +233,6 @@ extern "C" int ldm_bneck_fold_values(const float* w_fold, const float* kv, float
 extern "C" int ldm_bneck_pv(const float* u, const float* p, const float* pos_bias, float* y, int32_t B, int32_t dtype,
                             void* stream) {
     return ldm::bneck_pv(u, p, pos_bias, y, B, dtype, (hipStream_t)stream);
-}
-
-extern "C" int ldm_ca1_bneck(const float* z4, const float* kf, const float* bf, const float* u, const float* pos_bias,
-                             float* p, float* y, int32_t* cnt, int32_t B, int32_t dtype, void* stream) {
-    return ldm::ca1_bneck(z4, kf, bf, u, pos_bias, p, y, cnt, B, dtype, (hipStream_t)stream);
 }
 
 extern "C" int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, int32_t B, void* stream) {

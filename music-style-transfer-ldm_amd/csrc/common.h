@@ -212,9 +212,6 @@ int attention_folded_probs(const float* z, const float* kf, const float* bf, flo
 bool bneck_fold_supported(int B, int H, int W);
 int bneck_fold_values(const float* wf, const float* kv, float* u, int B, hipStream_t st);
 int bneck_pv(const float* u, const float* p, const float* pb, float* y, int B, int dtype, hipStream_t st);
-bool ca1_bneck_fused();
-int ca1_bneck(const float* z, const float* kf, const float* bfv, const float* u, const float* pb, float* p, float* y,
-              int32_t* cnt, int B, int dtype, hipStream_t st);
 
 // uconv.hip: the step kernels of the reverse loop (NHWC activations, see ldm_capi.h)
 struct StepConv {

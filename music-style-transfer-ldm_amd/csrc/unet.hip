@@ -99,7 +99,6 @@ struct UNetWs {
     float* ustep;                   // split-K counters + slabs of the LDS-staged step kernels (zero-filled)
     float* uks;                     // split-K counters + slabs of the K-split step kernels (uconv.hip)
     float *ubn, *p1;                // the bottleneck's folded values U and CA1's probabilities (bfold.hip)
-    int32_t* cnt1;                  // ca1_bneck_kernel's hand-off counters ((2B + 1) x 64, zero-filled)
     int64_t total;
 };
 
@@ -209,7 +208,6 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     const bool bfold = use_bneck_fold(s, wts);
     w.ubn = take(bfold ? B * 512 * 576 : 0);
     w.p1 = take(bfold ? B * 4 * L1 * L1 : 0);
-    w.cnt1 = reinterpret_cast<int32_t*>(take(bfold ? (2 * B + 1) * 64 : 0));
     w.total = off;
     return w;
 }
@@ -373,13 +371,9 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     LDM_TRY(run(3, 3));
     if (use_bneck_fold(s, &w)) {
         // CA1's probabilities, then the bottleneck on its folded values U (formed before the loop)
-        if (ca1_bneck_fused()) {
-            LDM_TRY(ca1_bneck(ws.z4, ws.kf1, ws.bf1, ws.ubn, w.step_pb[1], ws.p1, ws.zb, ws.cnt1, s.B, w.step_dtype, st));
-        } else {
-            if (ca1_probs_own()) LDM_TRY(ca1_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, st));
-            else LDM_TRY(attention_folded_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, 512, 4, L1, L1, st));
-            LDM_TRY(bneck_pv(ws.ubn, ws.p1, w.step_pb[1], ws.zb, s.B, w.step_dtype, st));
-        }
+        if (ca1_probs_own()) LDM_TRY(ca1_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, st));
+        else LDM_TRY(attention_folded_probs(ws.z4, ws.kf1, ws.bf1, ws.p1, s.B, 512, 4, L1, L1, st));
+        LDM_TRY(bneck_pv(ws.ubn, ws.p1, w.step_pb[1], ws.zb, s.B, w.step_dtype, st));
         return run(5, 8);
     }
     LDM_TRY(attention_folded(ws.z4, ws.kv1, ws.kf1, ws.bf1, ws.a1, s.B, 512, 4, L1, L1, st));

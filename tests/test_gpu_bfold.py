@@ -102,64 +102,6 @@ def test_bneck_fold_applies_at_the_bench_shape():
     assert lib.ldm_bneck_fold_supported(8, 16, 128) == 0      # not the 2 x 8 plane
 
 
-@pytest.mark.parametrize("B", [1, 3, 8])
-def test_ca1_bneck_one_launch_matches_float64(cuda, B):
-    """CA1's probabilities and the bottleneck in one launch (ca1_bneck_kernel: producer blocks hand P to the
-    bottleneck's blocks inside the launch) against float64 of the literal order and against the two launches;
-    the hand-off counters are zero again after every call (three calls in a row), and reruns are bitwise."""
-    from ldm_amd import _lib as L
-    ops = _operands(B, 200 + B)
-    p64, y64 = _reference64(*ops)
-    z4, kf, bf, kv, wf, pb = (t.to(cuda).contiguous() for t in ops)
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    u = torch.empty(B, 512, 576, device=cuda)
-    L.call("ldm_bneck_fold_values", _ptr(wf), _ptr(kv), _ptr(u), B, st)
-    cnt = torch.zeros((2 * B + 1) * 64, dtype=torch.int32, device=cuda)
-    outs = []
-    for _ in range(3):
-        p = torch.full((B, 4, 16, 16), float("nan"), device=cuda)
-        y = torch.full((B, 16, 512), float("nan"), device=cuda)
-        L.call("ldm_ca1_bneck", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(u), _ptr(pb), _ptr(p), _ptr(y), _ptr(cnt), B, 0, st)
-        torch.cuda.synchronize()
-        assert int(cnt.abs().sum()) == 0, cnt.tolist()
-        outs.append((p, y))
-    p, y = outs[0]
-    assert rel_err(p.cpu().numpy(), p64.numpy()) < 1e-5
-    err = rel_err(y.cpu().numpy(), y64.numpy())
-    print(f"B={B}: CA1 + bottleneck in one launch vs float64 {err:.2e}")
-    assert err < 1e-5
-    for p2, y2 in outs[1:]:
-        assert torch.equal(p, p2) and torch.equal(y, y2)
-    # the two-launch form: same contraction order, probabilities within fp32 rounding of each other
-    p_two = torch.empty_like(p)
-    y_two = torch.empty_like(y)
-    L.call("ldm_attention_folded_probs", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(p_two), B, 512, 4, 16, 16, st)
-    L.call("ldm_bneck_pv", _ptr(u), _ptr(p_two), _ptr(pb), _ptr(y_two), B, 0, st)
-    torch.cuda.synchronize()
-    assert rel_err(p.cpu().numpy(), p_two.cpu().numpy()) < 1e-6
-    assert rel_err(y.cpu().numpy(), y_two.cpu().numpy()) < 1e-6
-
-
-@pytest.mark.parametrize("dt,t16", [(1, torch.float16), (2, torch.bfloat16)])
-def test_ca1_bneck_one_launch_rounds_output_to_16_bits(cuda, dt, t16):
-    from ldm_amd import _lib as L
-    B = 2
-    z4, kf, bf, kv, wf, pb = (t.to(cuda).contiguous() for t in _operands(B, 9))
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    u = torch.empty(B, 512, 576, device=cuda)
-    L.call("ldm_bneck_fold_values", _ptr(wf), _ptr(kv), _ptr(u), B, st)
-    cnt = torch.zeros((2 * B + 1) * 64, dtype=torch.int32, device=cuda)
-    p = torch.empty(B, 4, 16, 16, device=cuda)
-    y32 = torch.empty(B, 16, 512, device=cuda)
-    y16 = torch.empty(B, 16, 512, device=cuda)
-    L.call("ldm_ca1_bneck", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(u), _ptr(pb), _ptr(p), _ptr(y32), _ptr(cnt), B, 0, st)
-    L.call("ldm_ca1_bneck", _ptr(z4), _ptr(kf), _ptr(bf), _ptr(u), _ptr(pb), _ptr(p), _ptr(y16), _ptr(cnt), B, dt, st)
-    torch.cuda.synchronize()
-    assert int(cnt.abs().sum()) == 0
-    assert torch.equal(y16, y16.to(t16).float())
-    assert rel_err(y16.cpu().numpy(), y32.cpu().numpy()) < (1e-3 if dt == 1 else 8e-3)
-
-
 @pytest.mark.parametrize("B", [1, 8])
 def test_ca1_probs_kernel_matches_float64(cuda, B):
     """The reverse loop's CA1 probabilities kernel (ca1_probs_kernel) against float64 and against the generic
