@@ -190,7 +190,13 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         bf = torch.randn(B, 4, Lt, device=dev)
         o = torch.empty(B, Lt, E, device=dev)
         probs = bfold and name == "attn1_folded"
-        if probs:
+        own = probs and bool(lib.ldm_ca1_probs_form())   # the loop's CA1 launch: ca1_probs_kernel (the default)
+        if own:
+            us = _graph_time_us(lambda: lib.ldm_ca1_probs(z.data_ptr(), kf.data_ptr(), bf.data_ptr(), o.data_ptr(), B,
+                                                          torch.cuda.current_stream().cuda_stream), reps)
+            fl = 2.0 * B * 4 * Lt * Lt * E
+            by = 4.0 * B * (Lt * E + 4 * E * Lt + 4 * Lt * Lt)
+        elif probs:
             us = _graph_time_us(lambda: lib.ldm_attention_folded_probs(z.data_ptr(), kf.data_ptr(), bf.data_ptr(),
                                                                        o.data_ptr(), B, E, 4, Lt, Lt,
                                                                        torch.cuda.current_stream().cuda_stream), reps)
@@ -204,7 +210,8 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
             by = 4.0 * B * (Lt * E * 2 + 4 * E * Lt + 2 * E * Lt)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
                      "flops": fl, "bytes": by, "bound": "hbm",
-                     "kernel": "attention_mfma_kernel (folded" + (", probabilities only)" if probs else ")")}
+                     "kernel": "ca1_probs_kernel (folded, probabilities only)" if own else
+                               "attention_mfma_kernel (folded" + (", probabilities only)" if probs else ")")}
     return out
 
 

@@ -213,6 +213,9 @@ int ldm_bneck_pv(const float* u, const float* p, const float* pos_bias, float* y
 /* CA1's probabilities P [B,4,16,16] only, one block of eight waves per (sample, head): the reverse loop's form
  * (LDM_CA1P_FORM=0 keeps ldm_attention_folded_probs).  z4 token-major [B,16,512], kf [B,4,16,512], bf [B,4,16]. */
 int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, int32_t B, void* stream);
+/* 1 when the reverse loop forms CA1's probabilities with ldm_ca1_probs, 0 when with ldm_attention_folded_probs
+ * (LDM_CA1P_FORM=0): what bench.py times for the loop's CA1 launch. */
+int32_t ldm_ca1_probs_form(void);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that

@@ -350,6 +350,18 @@ __global__ __launch_bounds__(256) void unscale_check_kernel(const ldm_tensor_slo
                                                             const int64_t* __restrict__ chunk_start, int chunk_len,
                                                             const float* __restrict__ inv_scale,
                                                             int32_t* __restrict__ found_inf) {
+#define KNAME "unscale_check_kernel"
+#if LDM_DEBUG_BOUNDS
+    {
+        const int32_t ti = chunk_tensor[blockIdx.x];
+        const bool bad_ix = ti < 0 || ti >= (int32_t)gridDim.x || chunk_start[blockIdx.x] < 0;
+        if (bad_ix || slots[ti].grad == nullptr) {
+            if (threadIdx.x == 0) printf("%s: chunk %u: bad slot index %d / start %ld\n", KNAME, blockIdx.x, ti, (long)chunk_start[blockIdx.x]);
+            return;
+        }
+    }
+#endif
+#undef KNAME
     const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
     const int64_t s0 = chunk_start[blockIdx.x];
     const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);
@@ -392,6 +404,18 @@ __global__ __launch_bounds__(256) void adam_kernel(const ldm_tensor_slot* __rest
                                                    const AdamScalars* __restrict__ kdev = nullptr) {
     if (found_inf && found_inf[0]) return;   // GradScaler.step skips the update on inf/nan
     if (kdev) k = *kdev;                     // capturable form: scalars of the device-side step count
+#define KNAME "adam_kernel"
+#if LDM_DEBUG_BOUNDS
+    {
+        const int32_t ti = chunk_tensor[blockIdx.x];
+        const bool bad_ix = ti < 0 || ti >= (int32_t)gridDim.x || chunk_start[blockIdx.x] < 0;
+        if (bad_ix || slots[ti].grad == nullptr) {
+            if (threadIdx.x == 0) printf("%s: chunk %u: bad slot index %d / start %ld\n", KNAME, blockIdx.x, ti, (long)chunk_start[blockIdx.x]);
+            return;
+        }
+    }
+#endif
+#undef KNAME
     const ldm_tensor_slot sl = slots[chunk_tensor[blockIdx.x]];
     const int64_t s0 = chunk_start[blockIdx.x];
     const int64_t e0 = min(s0 + (int64_t)chunk_len, sl.numel);

@@ -238,3 +238,5 @@ extern "C" int ldm_bneck_pv(const float* u, const float* p, const float* pos_bia
 extern "C" int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, int32_t B, void* stream) {
     return ldm::ca1_probs(z4, kf, bf, p, B, (hipStream_t)stream);
 }
+
+extern "C" int32_t ldm_ca1_probs_form(void) { return ldm::ca1_probs_own() ? 1 : 0; }

@@ -238,6 +238,14 @@ int step_ks_mask();   // layers running the K-split step form (LDM_UCONV_KS)
 #ifndef LDM_STEP_DIAG
 #define LDM_STEP_DIAG 0
 #endif
+
+// LDM_DEBUG_BOUNDS (on in the diagnostic build): the multi-tensor optimizer kernels check the chunk map they
+// index the slot table with (chunk_tensor[i] in [0, nchunks), chunk_start >= 0, a non-null gradient) and print
+// and skip a bad chunk instead of dereferencing it (round 5's aperture violation in unscale_check_kernel read
+// a slot table that the graph's own scratch had overwritten)
+#ifndef LDM_DEBUG_BOUNDS
+#define LDM_DEBUG_BOUNDS LDM_STEP_DIAG
+#endif
 // Two consecutive step layers in one launch with an in-launch hand-off (uconv.hip upair_kernel); pairs start
 // at layer 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1).
 bool step_pair_supported(int la, int W);

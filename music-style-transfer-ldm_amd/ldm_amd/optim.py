@@ -24,12 +24,23 @@ class _SlotTable:
     Tables are cached by the tensors' addresses (the same parameters, gradients and state give the same
     table every step).  The chunk map depends only on the sizes and is uploaded once per size list; the
     slot rows (whose gradient addresses move when zero_grad() drops the grads) go up with an asynchronous
-    copy from pinned memory, so building a table never synchronises the host with the device."""
+    copy from pinned memory, so building a table never synchronises the host with the device.
+
+    Inside a graph capture a table is neither allocated nor filled on the device.  Its rows go to a pinned
+    host buffer and its device rows are a buffer reserved BEFORE the capture (reserve_capture_buffers), and
+    fill_captured() uploads them after the capture has ended.  Why (round 6): a device buffer
+    allocated while capturing comes from the graph's private pool and may be a block that a temporary of the
+    SAME capture used and freed earlier (the forward / backward scratch).  Every replay then rewrites that
+    block before the optimizer reads it, so a table written there once, outside the graph's own stream order,
+    is garbage by the time unscale_check_kernel indexes slots[chunk_tensor[i]]: round 5's side-stream
+    upload variant faulted on exactly that (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in unscale_check_kernel
+    at the first replay).  A chunk map for a new size list would be a captured copy from a pageable numpy
+    buffer that is freed after the capture; both are refused while capturing."""
 
     _cache = {}
     _maps = {}
     _captured = []
-    _reserve = []
+    _reserve = []   # (pinned host int64 buffer, device int64 buffer) pairs, allocated outside any capture
 
     def __new__(cls, params, grads, m, v):
         key = tuple((p.data_ptr(), g.data_ptr(), 0 if a is None else a.data_ptr(), 0 if b is None else b.data_ptr(),
@@ -38,11 +49,15 @@ class _SlotTable:
         hit = cls._cache.get((dev, key))
         if hit is not None:
             return hit
+        capturing = torch.cuda.is_current_stream_capturing()
         self = super().__new__(cls)
         rows = np.array(key, dtype=np.int64).reshape(-1, 5)
         numels = tuple(int(k[4]) for k in key)
         mp = cls._maps.get((dev, numels))
         if mp is None:
+            if capturing:
+                raise RuntimeError("ldm_amd.optim: a slot table's chunk map is built outside a graph capture only "
+                                   "(run the step eagerly once before capturing it)")
             nch = (rows[:, 4] + CHUNK - 1) // CHUNK
             ct = np.repeat(np.arange(len(rows), dtype=np.int32), nch)
             first = np.repeat(np.cumsum(nch) - nch, nch)
@@ -50,20 +65,23 @@ class _SlotTable:
             mp = (torch.from_numpy(ct).to(dev), torch.from_numpy(cs).to(dev), int(len(ct)))
             cls._maps[(dev, numels)] = mp
         self.chunk_tensor, self.chunk_start, self.nchunks = mp
-        self.slots = torch.empty(rows.shape, dtype=torch.int64, device=dev)
-        if torch.cuda.is_current_stream_capturing():
-            # no host allocation may run inside a capture, and a captured copy re-reads its host buffer at
-            # every replay: take one of the pinned buffers reserved before the capture and keep it for good
-            if not cls._reserve or cls._reserve[-1].numel() < rows.size:
-                raise RuntimeError("ldm_amd.optim: call reserve_capture_buffers() before capturing an optimizer step")
-            host = cls._reserve.pop()[:rows.size].view(rows.shape)
+        if capturing:
+            res = cls._reserve[-1] if cls._reserve else None
+            if res is None or res[0].numel() < rows.size or res[1].device != dev:
+                raise RuntimeError("ldm_amd.optim: slot tables are built and filled outside a graph capture only; "
+                                   "call reserve_capture_buffers(device=...) before capturing an optimizer step")
+            host, dbuf = cls._reserve.pop()
+            host = host[:rows.size].view(rows.shape)
             host.copy_(torch.from_numpy(rows))
             self._host = host
+            self.slots = dbuf[:rows.size].view(rows.shape)   # reserved before the capture: never a graph-pool block
+            self._filled = False
             cls._captured.append(self)
             self._captured_key = (dev, key)
         else:
+            self.slots = torch.empty(rows.shape, dtype=torch.int64, device=dev)
             host = torch.from_numpy(rows).pin_memory()    # caching host allocator: reused once the copy ran
-        self.slots.copy_(host, non_blocking=True)
+            self.slots.copy_(host, non_blocking=True)
         self.key = key
         if len(cls._cache) > 64:
             cls._cache.clear()
@@ -74,14 +92,32 @@ class _SlotTable:
         pass
 
 
-def reserve_capture_buffers(n=4, words=1 << 14):
-    """Pinned host buffers for the slot tables built while a step is being captured into a hipGraph (one
-    per optimizer / unscale table in the step); call before torch.cuda.graph.  Returns the list that will
-    hold the tables the capture builds: pass it to release_captured() when the graph is dropped."""
+def reserve_capture_buffers(n=4, words=1 << 14, device="cuda"):
+    """Pinned host buffers and device buffers for the slot tables built while a step is being captured into
+    a hipGraph (one pair per optimizer / unscale table in the step); call before torch.cuda.graph, outside
+    the capture.  Returns the list that will hold the tables the capture builds: pass it to fill_captured()
+    once the capture has ended (before the first replay), and to release_captured() when the graph is
+    dropped."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ldm_amd.optim.reserve_capture_buffers: call it before the capture starts")
+    dev = torch.device(device)
+    _SlotTable._reserve = [r for r in _SlotTable._reserve if r[1].device == dev]
     while len(_SlotTable._reserve) < n:
-        _SlotTable._reserve.append(torch.empty(words, dtype=torch.int64, pin_memory=True))
+        _SlotTable._reserve.append((torch.empty(words, dtype=torch.int64, pin_memory=True),
+                                    torch.empty(words, dtype=torch.int64, device=dev)))
     _SlotTable._captured = []
     return _SlotTable._captured
+
+
+def fill_captured(tables):
+    """Upload the rows of the slot tables a capture built (on the current stream, outside the capture; the
+    graph's replays on this stream come after the copies).  Idempotent."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ldm_amd.optim.fill_captured: the tables are filled after the capture has ended")
+    for tab in tables:
+        if not tab._filled:
+            tab.slots.copy_(tab._host, non_blocking=True)
+            tab._filled = True
 
 
 def release_captured(tables):

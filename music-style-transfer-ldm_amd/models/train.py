@@ -276,7 +276,7 @@ class LDMTrainer:
             if self._graph is not None:
                 hoptim.release_captured(self._graph_tables)
                 self._graph = None
-            tables = hoptim.reserve_capture_buffers()
+            tables = hoptim.reserve_capture_buffers(device=self.device)
             # new versions for the capture: every weight pack of the step misses the version-keyed caches and
             # is recorded into the graph (a cache hit would bake a pack made outside it into every replay)
             for p in self._trainable:
@@ -290,6 +290,7 @@ class LDMTrainer:
             g = torch.cuda.CUDAGraph()
             with hgraphs.capture(g):
                 outs = self._loss_vec(self._step(*static))
+            hoptim.fill_captured(tables)   # the optimizer's slot tables: filled once, outside the graph
             self._graph, self._graph_in, self._graph_out, self._graph_sig = g, static, outs, sig
             self._graph_tables = tables
         for dst, src in zip(self._graph_in, args):

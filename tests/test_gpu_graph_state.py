@@ -153,3 +153,60 @@ def test_capturable_adam_state_dict_round_trip(cuda, target):
     assert all(float(mine.state[p]["step"]) == 4.0 for p in ps)
     for a, b in zip(ps_ref, ps):
         assert rel_err(b.detach().double().cpu().numpy(), a.detach().double().numpy()) < 1e-6
+
+
+def test_capture_allocation_reuses_a_scratch_block_of_the_same_capture(cuda):
+    """The mechanism behind round 5's aperture violation in unscale_check_kernel: a tensor
+    allocated while capturing may be a block that a temporary of the same capture used and freed, so the graph
+    itself rewrites it at every replay.  A table written into such a block once, outside the graph's stream
+    order (the reverted side-stream upload of the optimizer's slot rows), holds the scratch values by the time
+    a later node reads it.  Plain torch ops, no kernel of this package: the allocator's behaviour alone."""
+    from ldm_amd.graphs import capture
+    n = 4096
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with capture(g):
+        tmp = torch.empty(n, dtype=torch.int64, device=cuda)
+        tmp.fill_(-7)                                   # a step's scratch: written, then freed
+        scratch_ptr = tmp.data_ptr()
+        del tmp
+        table = torch.empty(n, dtype=torch.int64, device=cuda)
+        seen = table * 1                                # a later node reads the "table"
+    assert table.data_ptr() == scratch_ptr              # the capture handed the freed scratch block out again
+    table.copy_(torch.arange(n, device=cuda))           # filled once, eagerly, after the capture
+    g.replay()
+    torch.cuda.synchronize()
+    assert bool((seen == -7).all())                     # the replay's scratch write clobbered it
+
+
+def test_slot_tables_are_built_and_filled_outside_the_capture(cuda):
+    """ldm_amd.optim builds no device table inside a capture: without reserved buffers it raises; with them the
+    captured launch reads a buffer allocated before the capture, which fill_captured() uploads after it ends
+    (so no graph scratch can alias it and no copy node runs per replay)."""
+    from ldm_amd import optim as hoptim
+    from ldm_amd.graphs import capture
+    ps = [torch.randn(1000, device=cuda), torch.randn(5000, device=cuda)]
+    gs = [torch.randn_like(p) for p in ps]
+    hoptim.scale_tensors_(gs, 1.0)                      # the chunk map of this size list: built eagerly
+    torch.cuda.synchronize()
+    hoptim._SlotTable._cache.clear()
+    hoptim._SlotTable._reserve.clear()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="outside a graph capture"):
+        with capture(g):
+            hoptim.scale_tensors_(gs, 0.5)
+    torch.cuda.synchronize()
+    hoptim._SlotTable._cache.clear()
+    tables = hoptim.reserve_capture_buffers(device=cuda)
+    reserved = {int(r[1].data_ptr()) for r in hoptim._SlotTable._reserve}
+    want = [gg.clone() * 0.5 for gg in gs]
+    g = torch.cuda.CUDAGraph()
+    with capture(g):
+        hoptim.scale_tensors_(gs, 0.5)
+    assert len(tables) == 1 and int(tables[0].slots.data_ptr()) in reserved
+    hoptim.fill_captured(tables)
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(gs, want):
+        assert torch.equal(a, b)
+    hoptim.release_captured(tables)
