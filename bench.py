@@ -44,10 +44,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("sample", "transfer", "train"), default="sample",
+    ap.add_argument("--workload", choices=("sample", "transfer", "train", "stress"), default="sample",
                     help="sample = config 2 (the BASELINE metric, default); transfer = config 5 (content/style "
                          "transfer loop, T'=100, eta=1.0); train = configs 3/4 (encode -> UNet train step -> decode, "
-                         "batch 32/GPU, RCCL grad all-reduce when N>1)")
+                         "batch 32/GPU, RCCL grad all-reduce when N>1); stress = SURVEY's secondary shape S "
+                         "(UNet(1, 1) on the raw [1,1,128,512] mel, 50-step DDIM, batch 1/GPU)")
     ap.add_argument("--batch", type=int, default=None, help="latents per GPU (8 sample/transfer, 32 train)")
     ap.add_argument("--timesteps", type=int, default=None, help="50 for sample, T'=100 for transfer")
     ap.add_argument("--eta", type=float, default=None, help="0.0 for sample, 1.0 for transfer")
@@ -64,7 +65,7 @@ def parse():
                     help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
     a = ap.parse_args()
     if a.batch is None:
-        a.batch = 32 if a.workload == "train" else 8
+        a.batch = {"train": 32, "stress": 1}.get(a.workload, 8)
     if a.timesteps is None:
         a.timesteps = 100 if a.workload == "transfer" else 50
     if a.eta is None:
@@ -439,6 +440,121 @@ def run_train(args, world, rank, dev, M):
     }
 
 
+# SURVEY.md §8(d) shape S: UNet(1, 1) on [B,1,128,512], s5 [B,256,32,128], s6 [B,512,16,64] — per sample-step
+# FLOPs by layer (2 * MACs; the convT layers over their input grid): enc1 / dec1 75.5 M each, enc2-4 and dec4-2
+# 2.416 G each, CA2 (L = S = 4096 tokens, E = 256) 19.33 G of which the attention core is 4 E L S = 17.18 G, CA1
+# (1024 tokens, E = 512) 4.29 G (core 2.15 G), bottleneck 4.83 G: 43.10 GFLOP
+STRESS_GFLOP_PER_SAMPLE = 43.10
+
+
+def run_stress(args, world, rank, dev, M):
+    """Shape S: a DDIM reverse loop (args.timesteps - 1 UNet + update iterations, the
+    reference's update of model.py:442-458) with the denoiser a UNet(1, 1) on the raw [B,1,128,512] mel and
+    synthetic style maps s5 [B,256,32,128], s6 [B,512,16,64].  The UNet's latent width (1) is one the fused
+    engine does not take, so every iteration is the per-layer path (NCHW conv kernels, the KV-tiled flash
+    attention over 4096 / 1024 tokens) + the DDIM update kernel; the whole loop is one hipGraph."""
+    from ldm_amd import ops
+    from ldm_amd.graphs import capture
+    B = args.batch
+    torch.manual_seed(0)
+    unet = M.UNet(1, 1, 64).to(dev).eval()                 # random-init weights of the architecture
+    sched = M.ForwardDiffusion()
+    g = torch.Generator().manual_seed(1 + rank)
+    z_T = torch.randn((B, 1, 128, 512), generator=g).to(dev)
+    s5 = torch.rand((B, 256, 32, 128), generator=g).to(dev)
+    s6 = torch.rand((B, 512, 16, 64), generator=g).to(dev)
+    emb = {"s5": s5, "s6": s6}
+    times = torch.linspace(sched.num_timesteps - 1, 0, args.timesteps).long()
+    n_iter = len(times) - 1
+    coefs = sched.reverse_coefs(times).to(dev)
+    coef_rows = [coefs[i].contiguous() for i in range(n_iter)]
+    t_table = times[:-1].view(-1, 1).expand(-1, B).contiguous().to(dev)
+    x = torch.empty_like(z_T)
+    x0_logs = torch.empty((n_iter,) + tuple(z_T.shape), device=dev)
+    eps_logs = torch.empty_like(x0_logs)
+
+    def loop():
+        x.copy_(z_T)
+        for i in range(n_iter):
+            eps = unet(x, t_table[i], emb)
+            ops.ddim_step_(x, eps, coef_rows[i], float(args.eta), x0_logs[i], eps_logs[i])
+
+    with torch.no_grad():
+        loop()                                              # packs weights, plans, allocations: outside capture
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with capture(graph):
+            loop()
+        for _ in range(args.warmup):
+            graph.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    if not torch.isfinite(x).all():
+        raise SystemExit("non-finite sample")
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    us_iter = elapsed / (n_iter * args.steps) * 1e6
+    flops_iter = STRESS_GFLOP_PER_SAMPLE * 1e9 * B
+    t_roof = flops_iter / (FP32_PEAK_TFLOPS * 1e12)
+    result = {
+        "metric": METRIC, "value": round(n_iter * args.steps * world / elapsed, 2), "unit": "steps/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (N(0,1) z_T, U[0,1) style maps; random-init weights)",
+        "config": {"workload": f"shape S (SURVEY §8(d), secondary): {args.timesteps}-step DDIM reverse sample ({n_iter} "
+                               f"iterations per step) with UNet(1, 1) on the raw [{B},1,128,512] mel, s5 [{B},256,32,128], "
+                               f"s6 [{B},512,16,64], eta={args.eta}, per-layer kernels + flash attention, hipGraph replay",
+                   "global_batch": B * world, "latent": [B, 1, 128, 512], "parallelism": f"dp{world} (batch shards)"},
+        "us_per_denoise_iteration": round(us_iter, 2),
+        "step_roofline": {"t_roof_us": round(t_roof * 1e6, 2), "t_measured_us": round(us_iter, 2),
+                          "frac": round(t_roof * 1e6 / us_iter, 4),
+                          "achieved_tflops": round(flops_iter / (us_iter * 1e-6) / 1e12, 2)},
+    }
+    if rank == 0 and not args.no_kernel_timing:
+        # the dominant kernel: CA2's attention core over 4096 x 4096 tokens (KV-tiled flash forward), timed as
+        # the loop launches it (q [B,256,4096], kv [B,512,4096] of the projections), HIP events around a graph
+        E, Lq = 256, 32 * 128
+        q = torch.randn(B, E, Lq, device=dev)
+        kv = torch.randn(B, 2 * E, Lq, device=dev)
+        assert ops.attention_uses_flash(E, 4, Lq, Lq)
+        us = _graph_time_us(lambda: ops.attention_core(q, kv, 4), 10)
+        fl = 4.0 * B * E * Lq * Lq
+        result["roofline"] = {"kernel": "fa::flash_fwd_kernel (CA2 attention core, L = S = 4096, E = 256)",
+                              "bound": "mfma", "achieved": round(fl / us / 1e6, 2), "peak": FP32_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(fl / us / 1e6 / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                              "flops_per_launch": fl, "avg_launch_us": round(us, 3)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import ldm_torch_cpu as TC
+        env = cpu_env()
+        torch.set_num_threads(env["threads"])
+        sd = {k: v.detach().float().cpu().clone() for k, v in unet.state_dict().items()}
+        ab = TC.schedule(200)[2]
+        xc = z_T.cpu().clone()
+        s5c, s6c = s5.cpu(), s6.cpu()
+        with torch.no_grad():
+            med, ts = _median_s(lambda: TC.reverse_loop(sd, ab, xc, s5c, s6c, times[:2], args.eta, p=""),
+                                warmups=1, runs=3)
+        result["cpu_baseline"] = {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": env["threads"],
+                                  "kind": "port", "cpu_model": env["model"], "affinity_cores": env["affinity_cores"],
+                                  "sample": f"median of {len(ts)} single DDIM iterations after 1 warm-up (UNet(1, 1) "
+                                            f"forward at shape S + update, batch {B}, fp32), torch-CPU restatement "
+                                            f"oracle/ldm_torch_cpu.py; runs {min(ts):.2f}-{max(ts):.2f} s"}
+        result["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+    return result
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -533,7 +649,14 @@ def main():
     import models.model as M
     from ldm_amd.engine import GraphedDDIM
 
-    if args.workload == "train":
+    if args.workload in ("train", "stress"):
+        if args.workload == "stress":
+            result = run_stress(args, world, rank, dev, M)
+            if rank == 0:
+                print(json.dumps(result), flush=True)
+            if world > 1:
+                dist.destroy_process_group()
+            return
         result = run_train(args, world, rank, dev, M)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             torch.manual_seed(0)

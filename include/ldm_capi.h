@@ -93,7 +93,9 @@ typedef struct ldm_epilogue {
 
 typedef struct ldm_conv_plan {
     int32_t kind;          /* 0 direct (VALU), 1 MFMA 32x32x2 f32, 2 MFMA 16x16x4 f32, 3 LDS-staged */
-                           /* 16-bit-operand MFMA 32x32x16 (tm = BM/64, tn = LDM_DT_F16 / _BF16)    */
+                           /* 16-bit-operand MFMA 32x32x16 (tm = BM/64, tn = LDM_DT_F16 / _BF16),    */
+                           /* 4 small-plane 16-bit-operand MFMA 32x32x16 (sconv.hip; tn = the dtype, */
+                           /* wk = waves per block)                                                  */
     int32_t tm, tn, wk;    /* MFMA tiles per wave along M / N, waves splitting K per block      */
     int32_t ks;            /* blocks splitting K (>1: partial tiles + fixed-order last-arriver sum) */
     int32_t balance;       /* 4-phase transposed convs: phase p splits K ks*ntap_p ways (equal K per block) */
@@ -106,6 +108,12 @@ int ldm_conv_make_plan(const ldm_conv_desc* d, ldm_conv_plan* plan);
  * GEMM for large-plane NCHW layers (Cin % 32 == 0, >= 4096 positions per phase; bias / eval-BN /
  * activation epilogues only).  Returns 0 and fills plan, or 1 when the layer is not of that class. */
 int ldm_conv_tiled_plan(const ldm_conv_desc* d, int32_t dtype, ldm_conv_plan* plan);
+/* The kind-4 plan for d at operand precision dtype (LDM_DT_F16 / LDM_DT_BF16): the small-plane implicit GEMM
+ * (sconv.hip) for k3 p1 convs (stride 1 / 2) and k3 s2 op1 / stride-1 transposed convs whose phase grid tiles into
+ * 32-position runs (Wq | 32, or Wq % 32 == 0), Cin % 32 == 0 (>= 64), Cout % 64 == 0, fp32 NCHW maps; every
+ * epilogue but the position bias and the fused DDIM update.  Its weights use the kind-3 pack (ldm_conv_pack_weight).
+ * Returns 0 and fills plan, or 1 when the layer is not of that class (LDM_AMD_SCONV=0: never). */
+int ldm_conv_sconv_plan(const ldm_conv_desc* d, int32_t dtype, ldm_conv_plan* plan);
 /* Force a specific plan (autotuning / tests).  Fills packed_floats / ws_floats; validates.
  * ks < 0 requests the phase-balanced split with base -ks (4-phase layers only). */
 int ldm_conv_make_plan_forced(const ldm_conv_desc* d, int kind, int tm, int tn, int wk, int ks,
@@ -216,6 +224,9 @@ int ldm_ca1_probs(const float* z4, const float* kf, const float* bf, float* p, i
 /* 1 when the reverse loop forms CA1's probabilities with ldm_ca1_probs, 0 when with ldm_attention_folded_probs
  * (LDM_CA1P_FORM=0): what bench.py times for the loop's CA1 launch. */
 int32_t ldm_ca1_probs_form(void);
+/* A/B switch of the Cin = 1 stride-2 conv's packed form (two output channels per v_pk_fma_f32; bitwise the scalar
+ * form's results): 1 on, 0 off; returns the previous setting.  Default: LDM_CIN1_PK. */
+int ldm_set_cin1_packed(int on);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that
@@ -441,6 +452,13 @@ int ldm_batchnorm_backward(const float* dy, const float* y, const float* x, cons
                            const float* save_invstd, const float* weight, const float* bias, int32_t act, int32_t B,
                            int32_t C, int32_t HW, float* dx, float* dweight, float* dbias, float* workspace,
                            void* stream);
+/* ldm_batchnorm_backward (dx required) that also writes dx_sum[c] = the sum of dx (as stored) over (b, h, w): the
+ * bias gradient of the conv whose output x is, without a sweep of its own over dx (round 6).  workspace as
+ * ldm_batchnorm_train (ldm_reduce_workspace_floats covers the extra slice partials). */
+int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, const float* x, const float* save_mean,
+                                 const float* save_invstd, const float* weight, const float* bias, int32_t act,
+                                 int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
+                                 float* dx_sum, float* workspace, void* stream);
 /* The same in two stages for SyncBatchNorm: sums[2c] = sum g, sums[2c+1] = sum g*xhat over this rank
  * (g = dy*act'(y)) and sums[2C] = this rank's B*H*W (sums holds 2C+1 doubles); dbias / dweight get the
  * local sums (parameter grads stay local, as in torch.nn.SyncBatchNorm; the DP gradient all-reduce

@@ -156,6 +156,10 @@ bool tconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan);
 int tconv_pack(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* w, float* packed, hipStream_t st);
 int tconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
                   float* y, hipStream_t st);
+// plan kind 4 (sconv.hip): small-plane 16-bit-operand implicit GEMM, packed like kind 3 (tm = 1)
+bool sconv_plan(const ldm_conv_desc& d, int dtype, ldm_conv_plan& plan);
+int sconv_forward(const ldm_conv_desc& d, const ldm_conv_plan& p, const float* x, const float* w, const EpiArgs& ep,
+                  float* y, hipStream_t st);
 
 // Device-side epilogue parameters (by value in kernel args).
 struct EpiArgs {

@@ -31,6 +31,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "conv_epi.h"
 
 #pragma clang fp contract(off)
 
@@ -39,46 +40,6 @@
 #endif
 
 namespace ldm {
-
-struct ConvArgs {
-    const float* x;
-    const float* w;
-    float* y;
-    int32_t B, Cin, Hin, Win, Cout, Hout, Wout;
-    int32_t KK;     // kh*kw
-    int32_t Mpad;   // rows of the packed weight
-    int32_t transposed;
-    int32_t xcd_nfast;     // weight-heavy layer (weights > input bytes)
-    int32_t tile_order;    // 0 natural (N, M, phase), 1 XCD-grouped N-fast, 2 XCD-grouped M-fast
-    int32_t ks;            // blocks splitting K (cross-block split-K)
-    int32_t out_nhwc;      // output / skip / fused-update tensors are NHWC (the input layout is a template flag)
-    int32_t nN, nM;        // N / M tiles per phase
-    int32_t balance;       // 4-phase layers: phase p splits K ks_p = ks_base * ntap_p ways (equal work per block)
-    int32_t bofs[kMaxPhase];    // balance: first block of each phase (after the XCD renumbering)
-    int32_t bks_log2[kMaxPhase];  // balance: log2 ks_p
-    int32_t nblocks_bal;          // balance: grid size
-    float* part;           // ks > 1: partial tiles [phase][M-tile][N-tile][ks][BM*BN]
-    int32_t* cnt;          // ks > 1: arrival counter per tile (zero between launches)
-    FastDiv fd_ks;         // M-tile' -> (M-tile, split)
-    FastDiv fd_hw, fd_w;   // n -> (b, q) and q -> (qy, qx) of the phase grid
-    FastDiv fd_cpt;        // K chunk -> (tap, channel chunk)
-    FastDiv fd_np, fd_inner;   // block -> (phase, tile), tile -> (outer, inner) of the XCD order
-    FastDiv fd_nn, fd_nm;      // natural order: block -> (N-tile, M-tile, phase)
-    FastDiv fd_dwo, fd_dho, fd_dco;   // direct kernel: output index -> (b, co, oy, ox)
-    PhaseTable pt;
-    // Per-phase scalars of the MFMA kernel, indexed [phase] and read at static offsets (one batch of
-    // scalar loads, then a select by phase: a load indexed by the runtime phase would be a second,
-    // dependent round of kernarg reads).  Tap t = ja*nb + jb of a phase sits at
-    // (dy, dx) = (dy0 + sg*ja, dx0 + sg*jb) — the same order as pt.dy / pt.dx (checked on the host).
-    struct {
-        int32_t ry[kMaxPhase], rx[kMaxPhase];
-        int32_t dy0[kMaxPhase], dx0[kMaxPhase];
-        int32_t na[kMaxPhase], nb[kMaxPhase];
-        int32_t kchunks[kMaxPhase], wofs[kMaxPhase];
-        int32_t sg;
-    } pk;
-    EpiArgs ep;
-};
 
 // mask-and-or select (a ?: chain is turned into branches by the compiler); single-phase kernels
 // (PH4 = false) read slot 0 only, which keeps 27 scalars of kernarg traffic out of their prologue
@@ -197,99 +158,6 @@ static int layout_for_plan(const ldm_conv_desc& d, const ldm_conv_plan& p, Phase
         floats += (int64_t)pt.kchunks[i] * Mpad * ck;
     }
     return 0;
-}
-
-// ------------------------------------------------------------------------------------------------
-// epilogue (op order of the reference: conv+bias -> BN(eval) -> act -> +bcast -> +skip)
-// ------------------------------------------------------------------------------------------------
-// Epilogue operands of one output element, loaded ahead of time (before the K loop) so their memory
-// latency overlaps the GEMM instead of trailing it.
-struct EpiPre {
-    float bias, bcast, skip, x;
-};
-
-__device__ __forceinline__ EpiPre epi_prefetch(const ConvArgs& a, int m, int b, size_t oidx, int pix) {
-    const EpiArgs& e = a.ep;
-    EpiPre p;
-    p.bias = e.pos_bias ? e.pos_bias[m * a.Hout * a.Wout + pix] : (e.bias ? e.bias[m] : 0.f);
-    p.bcast = e.bcast ? e.bcast[(size_t)b * a.Cout + m] : 0.f;
-    p.skip = e.skip ? e.skip[oidx] : 0.f;
-    p.x = e.ddim_coef ? e.ddim_x[oidx] : 0.f;
-    return p;
-}
-
-// The same loads, unconditional: one buffer resource per optional operand, with zero records when the
-// operand is absent (its loads then return 0 without touching memory).  No branch, so the loads issue
-// back to back and the waitcnt pass can count them (a branchy prefetch ends in a vmcnt(0) drain
-// in front of the K loop).
-struct EpiSrc {
-    __amdgpu_buffer_rsrc_t bias, bcast, skip, x;
-};
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t opt_rsrc(const float* p, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(uni_ptr(p), (short)0, uni(p ? bytes : 0), 0x00020000);
-}
-
-__device__ __forceinline__ EpiSrc epi_sources(const ConvArgs& a, bool live) {
-    const EpiArgs& e = a.ep;
-    const int ybytes = live ? a.B * a.Cout * a.Hout * a.Wout * 4 : 0;
-    EpiSrc s;
-    s.bias = e.pos_bias ? opt_rsrc(e.pos_bias, live ? a.Cout * a.Hout * a.Wout * 4 : 0)
-                        : opt_rsrc(e.bias, live ? a.Cout * 4 : 0);
-    s.bcast = opt_rsrc(e.bcast, live ? a.B * a.Cout * 4 : 0);
-    s.skip = opt_rsrc(e.skip, ybytes);
-    s.x = opt_rsrc(e.ddim_coef ? e.ddim_x : nullptr, ybytes);
-    return s;
-}
-
-__device__ __forceinline__ EpiPre epi_prefetch_buf(const EpiSrc& s, int Cout, int m, int b, int oidx, int boff) {
-    EpiPre p;
-    p.bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bias, boff, 0, 0));
-    p.bcast = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.bcast, (b * Cout + m) * 4, 0, 0));
-    p.skip = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.skip, oidx * 4, 0, 0));
-    p.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.x, oidx * 4, 0, 0));
-    return p;
-}
-
-__device__ __forceinline__ void epi_finish(const ConvArgs& a, int m, size_t oidx, float v, const EpiPre& p) {
-    const EpiArgs& e = a.ep;
-#if (LDM_DIAG & 32)   // diagnostic: minimal epilogue (bias + relu + store) to size the code-footprint cost
-    v = v + p.bias;
-    a.y[oidx] = v < 0.f ? 0.f : v;
-    return;
-#endif
-    const int ro = e.round_out;   // autocast output semantics (EpiArgs::round_out): 0 leaves every value as is
-    if (e.bias || e.pos_bias) v = v + p.bias;
-    v = round16(v, ro);
-    if (e.bn_w) {
-        // aten batch_norm_cpu_collect_linear_and_constant_terms: alpha = invstd*w, beta = b - mean*alpha
-        const float invstd = 1.0f / sqrtf(e.bn_v[m] + e.bn_eps);
-        const float alpha = invstd * e.bn_w[m];
-        const float beta = e.bn_b[m] - e.bn_m[m] * alpha;
-        v = round16(v * alpha + beta, ro);
-    }
-    v = round16(apply_act(v, e.act), ro);
-    if (e.act_out) e.act_out[oidx] = v;
-    if (e.bcast) v = round16(v + p.bcast, ro);
-    if (e.skip) v = round16(v + p.skip, ro);
-    if (e.ddim_coef) {
-        float x0;
-        e.ddim_x[oidx] = ddim_update(p.x, v, e.ddim_coef, e.ddim_eta, x0);
-        if (e.ddim_x0_log) e.ddim_x0_log[oidx] = x0;
-        if (e.ddim_eps_log) e.ddim_eps_log[oidx] = v;
-        if (a.y) a.y[oidx] = v;
-        return;
-    }
-    a.y[oidx] = v;
-}
-
-__device__ __forceinline__ int out_index(const ConvArgs& a, int m, int b, int oy, int ox) {
-    return a.out_nhwc ? ((b * a.Hout + oy) * a.Wout + ox) * a.Cout + m : ((b * a.Cout + m) * a.Hout + oy) * a.Wout + ox;
-}
-
-__device__ __forceinline__ void epilogue_store(const ConvArgs& a, int m, int b, int oy, int ox, float v) {
-    const size_t oidx = out_index(a, m, b, oy, ox);
-    epi_finish(a, m, oidx, v, epi_prefetch(a, m, b, oidx, oy * a.Wout + ox));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -997,11 +865,22 @@ __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float 
 // Cin = 1, stride 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
 // 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (6 + K) input window in registers,
 // every output channel from it, weights in LDS.
-template <int K, int LP, int RO, int YS>
+// PK = 1 (round 6): two output channels per packed FMA.  v_pk_fma_f32 computes each half exactly as v_fma_f32
+// does, so each output's chain fma(x, w, acc) over (ky, kx) is the scalar form's, bit for bit; the halves are
+// channels co and co + 1 (their weights one aligned 8-byte LDS read from a [tap][channel] copy), the input value
+// the same register for both (op_sel).  Round 5's packed attempt paired the FOUR OUTPUT COLUMNS instead; the
+// columns' inputs win[ky][kx + 2j] are not register pairs, and that variant failed the config-3 parity bound —
+// which fma rounding cannot explain.
+template <int K, int LP, int RO, int YS, int PK = 0>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
+    __shared__ __attribute__((aligned(8))) float wt[PK ? K * K * 64 : 1];   // PK: [ky*K + kx][co]
     __shared__ ChanEpi es[64];   // per-channel epilogue constants, formed once per block (not per lane and channel)
-    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) ws[i] = round16(a.w[i], LP);   // [co][ky*K + kx]
+    for (int i = threadIdx.x; i < a.Cout * K * K; i += blockDim.x) {
+        const float w = round16(a.w[i], LP);
+        ws[i] = w;   // [co][ky*K + kx]
+        if constexpr (PK != 0) wt[(i % (K * K)) * 64 + i / (K * K)] = w;
+    }
     for (int i = threadIdx.x; i < a.Cout; i += blockDim.x) es[i] = chan_epi(a, i);
     __syncthreads();
     const int W4 = a.Wout >> 2;
@@ -1029,6 +908,32 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     }
     const size_t plane = (size_t)a.Hout * a.Wout;
     size_t o = ((size_t)b * a.Cout * a.Hout + oy) * a.Wout + ox0;
+    if constexpr (PK != 0) {   // (the host takes this form for an even Cout only)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        for (int co = 0; co < a.Cout; co += 2, o += 2 * plane) {
+            f2 acc[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const f2 w2 = *reinterpret_cast<const f2*>(wt + (ky * K + kx) * 64 + co);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float xv = win[ky][kx + 2 * j];
+                        acc[j] = __builtin_elementwise_fma(f2{xv, xv}, w2, acc[j]);
+                    }
+                }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const ChanEpi ce = es[co + h];
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[j][h]);
+                store4<YS>(a, o + h * plane, v);
+            }
+        }
+        return;
+    }
     for (int co = 0; co < a.Cout; ++co, o += plane) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1046,6 +951,12 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         store4<YS>(a, o, v);
     }
 }
+
+// the packed form of conv_cin1_x4_kernel: LDM_CIN1_PK (default 0 until measured), or ldm_set_cin1_packed
+static int g_cin1_packed = [] {
+    const char* e = std::getenv("LDM_CIN1_PK");
+    return e ? std::atoi(e) : 0;
+}();
 
 // ConvTranspose2d(Cin -> 1, k4, s2, p1) (the decoder's output layer): lane = (b, qy, 4 input columns
 // qx0..qx0+3) -> the 2 x 8 outputs they feed (all four parities); per input channel a 3 x 6 window.
@@ -1535,6 +1446,11 @@ extern "C" int ldm_conv_pack_weight(const ldm_conv_desc* d, const ldm_conv_plan*
     if (plan->kind == 0) return 0;
     LDM_REQUIRE(packed, "conv pack: null output");
     if (plan->kind == 3) return tconv_pack(*d, *plan, w, packed, (hipStream_t)stream);
+    if (plan->kind == 4) {   // sconv.hip reads the kind-3 pack with 64-row padding
+        ldm_conv_plan k3 = *plan;
+        k3.kind = 3, k3.tm = 1;
+        return tconv_pack(*d, k3, w, packed, (hipStream_t)stream);
+    }
     ConvArgs a;
     int rc = make_args(*d, *plan, a);
     if (rc) return rc;
@@ -1630,6 +1546,7 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
     LDM_REQUIRE(p.ws_floats == 0 || ws, "conv forward: this plan splits K across blocks and needs a workspace");
     LDM_REQUIRE(!ep.ddim_coef || ep.ddim_x, "conv forward: fused DDIM update needs x");
     if (p.kind == 3) return tconv_forward(d, p, x, w, ep, y, st);
+    if (p.kind == 4) return sconv_forward(d, p, x, w, ep, y, st);
     ConvArgs a;
     int rc = make_args(d, p, a);
     if (rc) return rc;
@@ -1653,16 +1570,21 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             a.fd_dwo = FastDiv::make(d.Wout / 4);
             const int64_t lanes = (int64_t)d.B * d.Hout * (d.Wout / 4);
             LDM_REQUIRE(!ep.x16, "conv: the Cin = 1 kernel reads fp32 inputs only");
+            const bool pk = g_cin1_packed != 0 && d.Cout % 2 == 0;
             lp_dispatch(a.ep, [&](auto lp, auto ro) {
                 constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
                 const dim3 g((unsigned)((lanes + 255) / 256));
-                if (LP != 0 && ep.y16) {
-                    if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, LP>), g, dim3(256), 0, st, a);
-                    else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, LP>), g, dim3(256), 0, st, a);
-                } else {
-                    if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, 0>), g, dim3(256), 0, st, a);
-                    else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, 0>), g, dim3(256), 0, st, a);
-                }
+                auto go = [&](auto pkc) {
+                    constexpr int PK = decltype(pkc)::value;
+                    if (LP != 0 && ep.y16) {
+                        if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, LP, PK>), g, dim3(256), 0, st, a);
+                        else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, LP, PK>), g, dim3(256), 0, st, a);
+                    } else {
+                        if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, 0, PK>), g, dim3(256), 0, st, a);
+                        else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, 0, PK>), g, dim3(256), 0, st, a);
+                    }
+                };
+                if (pk) go(std::integral_constant<int, 1>{}); else go(std::integral_constant<int, 0>{});
             });
             LDM_CHECK_LAUNCH("conv_cin1_x4_kernel");
             return 0;
@@ -1794,4 +1716,12 @@ extern "C" int32_t ldm_conv_storage16(const ldm_conv_desc* d, const ldm_conv_pla
 extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* plan, const float* x, const float* w,
                                 const ldm_epilogue* ep, float* y, void* stream) {
     return ldm_conv_forward_ws(d, plan, x, w, ep, y, nullptr, stream);
+}
+
+// A/B switch of the Cin = 1 kernel's packed form (tests/test_gpu_store16.py compares both bitwise); returns the
+// previous setting
+extern "C" int ldm_set_cin1_packed(int on) {
+    const int prev = ldm::g_cin1_packed;
+    ldm::g_cin1_packed = on ? 1 : 0;
+    return prev;
 }

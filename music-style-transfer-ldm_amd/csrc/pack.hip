@@ -135,7 +135,9 @@ extern "C" int ldm_pack_many_prepare(const ldm_conv_desc* descs, const ldm_conv_
     for (int i = 0; i < n; ++i) {
         PackJob j{};
         LDM_REQUIRE(w[i] && out[i], "pack_many_prepare: null weight / output");
-        int rc = plans[i].kind == 3 ? tconv_pack_job(descs[i], plans[i], j) : conv_pack_job(descs[i], plans[i], j);
+        ldm_conv_plan pl = plans[i];
+        if (pl.kind == 4) pl.kind = 3, pl.tm = 1;   // sconv.hip reads the kind-3 pack (64-row padding)
+        int rc = pl.kind == 3 ? tconv_pack_job(descs[i], pl, j) : conv_pack_job(descs[i], pl, j);
         if (rc) return rc;
         LDM_REQUIRE(j.total > 0 && j.total < (1LL << 31) - kBlockElems, "pack_many_prepare: weight too large");
         // the kernel writes whole 8-element runs: phase segments (and so the total) are multiples of 8 elements

@@ -268,7 +268,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
                                                                 int64_t n, int64_t S, const double* __restrict__ sums,
                                                                 double count_arg, void* __restrict__ dx,
                                                                 const double* __restrict__ part, int P,
-                                                                float* __restrict__ dweight, float* __restrict__ dbias) {
+                                                                float* __restrict__ dweight, float* __restrict__ dbias,
+                                                                float* __restrict__ dxs_part) {
+    __shared__ float redf[kThreads / 64];
     const int k = blockIdx.x, c = blockIdx.y;
     const double count = count_arg > 0.0 ? count_arg : sums[2 * C];
     const float mu = mean[c], is = invstd[c];
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16, dxh = sf & LDM_ST_DX16;
+    float sdx = 0.f;
     slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
         float g[W], yv[W] = {}, xv[W], d[W];
         ld_st<ST, W>(dy, o, dyh, g);
@@ -304,7 +307,27 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
             d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
         }
         st_st<ST, W>(dx, o, dxh, d);
+        if (dxs_part) {   // the sum of dx as stored (a 16-bit dx: its rounded values)
+#pragma unroll
+            for (int j = 0; j < W; ++j) sdx += dxh ? round16(d[j], ST) : d[j];
+        }
     });
+    // dxs_part: this slice's sum of dx (fixed order: thread stride, wave tree, waves in order), for the bias
+    // gradient of the conv that produced x (chan_sum_finalize_kernel sums the slices in order)
+    if (dxs_part) {
+        const float t = block_sum(sdx, redf);
+        if (threadIdx.x == 0) dxs_part[(size_t)c * gridDim.x + k] = t;
+    }
+}
+
+// out[c] = sum_k part[c][k] (slices in order)
+__global__ __launch_bounds__(kThreads) void chan_sum_finalize_kernel(const float* __restrict__ part, int C, int P,
+                                                                     float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float a = 0.f;
+    for (int k = 0; k < P; ++k) a += part[(size_t)c * P + k];
+    out[c] = a;
 }
 
 // ---- fused-epilogue activation backward: dv = dy*act'(v); partial sums of dv and dy per (b,c,slice)
@@ -565,7 +588,8 @@ extern "C" int64_t ldm_reduce_workspace_floats(int32_t B, int32_t C, int32_t HW)
     if (B < 0 || C <= 0 || HW <= 0) return 0;
     if (B == 0) B = 1;   // an empty local shard (SyncBatchNorm) still runs the finalize stage
     const int64_t n = (int64_t)B * HW;
-    const int64_t bn = 2 * ((int64_t)C * bn_slices(n, C) * 2 + 2 * (int64_t)C + 2);   // doubles -> floats
+    // doubles -> floats, + the dx-sum slice partials of ldm_batchnorm_backward_dxsum (C * P floats)
+    const int64_t bn = 2 * ((int64_t)C * bn_slices(n, C) * 2 + 2 * (int64_t)C + 2) + (int64_t)C * bn_slices(n, C);
     const int64_t ac = (int64_t)B * C * act_slices(B, C, HW) * 2;
     return bn > ac ? bn : ac;
 }
@@ -722,7 +746,7 @@ extern "C" int ldm_batchnorm_backward_reduce(const float* dy, const float* y, co
 static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, const float* save_mean,
                                const float* save_invstd, const float* weight, const float* bias, const StCode& sc,
                                int act, int32_t B, int32_t C, int32_t HW, const double* sums, double count, void* dx,
-                               const double* part, float* dweight, float* dbias, void* stream) {
+                               const double* part, float* dweight, float* dbias, void* stream, float* dxs_part = nullptr) {
     if (B == 0) return 0;
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
@@ -733,7 +757,7 @@ static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, con
         w_dispatch(vw, [&](auto wc) {
             hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0,
                                (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n,
-                               S, sums, count, dx, part, part ? P : 0, dweight, dbias);
+                               S, sums, count, dx, part, part ? P : 0, dweight, dbias, dxs_part);
         });
     });
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
@@ -773,6 +797,32 @@ extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const flo
     // the apply sums the partials itself and writes dweight / dbias (no finalize launch)
     return bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, nullptr, (double)n,
                                dx, part, dweight, dbias, stream);
+}
+
+// ldm_batchnorm_backward plus dx_sum[c] = sum of dx over (b, h, w): the bias gradient of the conv whose output is
+// the BN's input (no separate sweep over dx for it).  The slice partials go after the backward's own workspace.
+extern "C" int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, const float* x, const float* save_mean,
+                                            const float* save_invstd, const float* weight, const float* bias,
+                                            int32_t act_code, int32_t B, int32_t C, int32_t HW, float* dx,
+                                            float* dweight, float* dbias, float* dx_sum, float* workspace, void* stream) {
+    LDM_REQUIRE(workspace && dx && dx_sum && B > 0 && C > 0 && HW > 0, "bn_backward_dxsum: bad argument");
+    const StCode sc = st_code(act_code);
+    const int act = sc.act & 0xff;
+    LDM_REQUIRE(dy && x && save_mean && save_invstd && (y || !bn_need_y(act)), "bn_backward_dxsum: bad argument");
+    LDM_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_backward_dxsum: workspace must be 8-byte aligned");
+    const int64_t n = (int64_t)B * HW;
+    const int P = bn_slices(n, C);
+    double* part = reinterpret_cast<double*>(workspace);
+    float* dxs = workspace + 2 * ((int64_t)C * P * 2 + 2 * (int64_t)C + 2);
+    int rc = bn_bwd_partial_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, part, stream);
+    if (rc) return rc;
+    rc = bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, nullptr, (double)n, dx,
+                             part, dweight, dbias, stream, dxs);
+    if (rc) return rc;
+    hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       (hipStream_t)stream, dxs, C, P, dx_sum);
+    LDM_CHECK_LAUNCH("chan_sum_finalize_kernel");
+    return 0;
 }
 
 extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,

@@ -1075,6 +1075,194 @@ __global__ __launch_bounds__(64 * WM * KK) void wgrad_lp16p_kernel(LpArgs a) {
     }
 }
 
+// The fp32-map form (wgrad_lp_kernel, XS = 0: the train step's UNet layers, whose maps stay fp32) on the same
+// NBUF-deep ring as wgrad_lp16p_kernel (round 6): the double-buffered form waited vmcnt(0) + __syncthreads() per
+// chunk and hipcc drained its one in-flight DMA before the first ds_read, so every chunk paid a whole memory round
+// trip.  Here every wave issues exactly NL = ND + NG DMAs per chunk (slots past the tile's pieces load nothing
+// into a trash KB), "chunk k landed" is vmcnt(ahead * NL) + a raw s_barrier, chunk k + NBUF - 1 refills chunk
+// k - 1's buffer, and the fragment reads are asm ds_read_b128 (see wgrad_lp16p_kernel).  Same blocks, chunks,
+// k-steps, fragments and MFMA order as wgrad_lp_kernel: bitwise its sums.
+template <int S, int KK, int BM, int WM, int QC, int DT, int NBUF>
+__global__ __launch_bounds__(64 * WM * KK) void wgrad_lpp_kernel(LpArgs a) {
+    constexpr int NW = WM * KK, MF = BM / WM / 32, T = KK * KK, NB = lp_nb(S, KK);
+    constexpr int PPR = QC / 4, RPI = 64 / PPR, NKS = QC / 16;
+    constexpr int NDG = BM / RPI, ND = (NDG + NW - 1) / NW, NG = lp_staged_pieces(S, KK, QC, NW), NL = ND + NG;
+    static_assert(MF >= 1 && MF * 32 * WM == BM, "row split");
+    static_assert(NBUF >= 3 && NBUF <= 4 && (NBUF - 2) * NL <= 63, "ring depth (vmcnt immediate)");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ky = wave % KK, wm = wave / KK;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * BM, c0 = blockIdx.x * kLC;
+    const int HQ = a.Hq * a.Wq;
+    const int bufF = lp_buf_floats(BM, QC, a.pitch_c);
+    char* const trash = reinterpret_cast<char*>(smem + NBUF * bufF);
+    const int ch_begin = blockIdx.z * a.per_split;
+    const int ch_end = min(a.nchunk, ch_begin + a.per_split);
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.dense), (short)0, uni(a.B * a.M * HQ * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.gath), (short)0, uni(a.B * a.C * a.Hg * a.Wg * 4), 0x00020000);
+
+    // chunk-invariant slot offsets (floats): Dense row m's 4-position piece, window piece (channel, row, column)
+    int doff[ND], goff[NG], grow[NG], gcol[NG];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const int gi = wave + j * NW;
+        const int row = gi * RPI + lane / PPR;
+        const int ql = ((lane % PPR) ^ lp_swz<PPR>(row)) * 4;
+        const int m = m0 + row;
+        doff[j] = (gi < NDG && m < a.M) ? m * HQ + (ql / a.cols) * a.Wq + ql % a.cols : -1;
+    }
+    const int wq4 = a.wca >> 2, pq = a.pitch_c >> 2, npiece = kLC * pq;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int pc = (wave + j * NW) * 64 + lane;
+        const int cl = pc / pq, rem = pc - (pc / pq) * pq;
+        const int wrow = rem / wq4, wx = (rem - wrow * wq4) * 4;
+        const bool ok = pc < npiece && c0 + cl < a.C && wrow < a.wr;
+        goff[j] = ((c0 + cl) * a.Hg + wrow) * a.Wg + wx;
+        grow[j] = ok ? wrow : -(1 << 20);   // (an invalid piece fails the row test of every chunk)
+        gcol[j] = wx;
+    }
+    auto issue = [&](int buf, int b, int qy0, int qx0) {
+        char* base = reinterpret_cast<char*>(smem + buf * bufF);
+        const int dbase = b * a.M * HQ + qy0 * a.Wq + qx0;
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const int gi = wave + j * NW;
+            const int voff = doff[j] >= 0 ? (dbase + doff[j]) * 4 : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_ptr_t)(gi < NDG ? base + gi * 1024 : trash), 16, voff, 0, 0, 0);
+        }
+        const int row0 = qy0 * S - 1, colA = qx0 * S - 4;   // pad 1, e = 3
+        const int gbase = (b * a.C * a.Hg + row0) * a.Wg + colA;
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            const int gi = wave + j * NW;
+            const bool ok = (unsigned)(row0 + grow[j]) < (unsigned)a.Hg && (unsigned)(colA + gcol[j]) < (unsigned)a.Wg;
+            const int voff = ok ? (gbase + goff[j]) * 4 : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, (lds_ptr_t)(gi * 64 < npiece ? base + BM * QC * 4 + gi * 1024 : trash),
+                                                     16, voff, 0, 0, 0);
+        }
+    };
+
+    floatx16 acc[MF][KK];
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int t = 0; t < KK; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][t][i] = 0.f;
+    // per-lane LDS byte offsets inside a buffer for k-step ks: A pieces of fragment f, window run start
+    int aoff[NKS][MF][2], boff[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int q0 = ks * 16 + 8 * h;
+        const int rl = q0 / a.cols, xl0 = q0 - rl * a.cols;
+#pragma unroll
+        for (int f = 0; f < MF; ++f) {
+            const int row = (wm * MF + f) * 32 + r;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) aoff[ks][f][u] = (row * QC + ((((q0 >> 2) + u) ^ lp_swz<PPR>(row)) << 2)) * 4;
+        }
+        boff[ks] = (BM * QC + r * a.pitch_c + (rl * S + ky) * a.wca + xl0 * S) * 4;
+    }
+
+    int ib = ch_begin / a.cps, iqy, iqx;   // the issue cursor, walked without divisions
+    {
+        const int rr = ch_begin - ib * a.cps;
+        if (a.cols == a.Wq) {
+            iqy = rr * a.rows, iqx = 0;
+        } else {
+            const int segs = a.Wq / QC;
+            iqy = rr / segs, iqx = (rr - iqy * segs) * QC;
+        }
+    }
+    auto advance = [&]() {
+        iqx += a.cols;
+        if (iqx >= a.Wq) {
+            iqx = 0, iqy += a.rows;
+            if (iqy >= a.Hq) iqy = 0, ++ib;
+        }
+    };
+    const int n = ch_end - ch_begin;
+#pragma unroll
+    for (int k = 0; k < NBUF - 1; ++k)
+        if (k < n) issue(k, ib, iqy, iqx), advance();
+    int buf = 0, ibuf = NBUF - 1;
+    for (int k = 0; k < n; ++k) {
+        const int ahead = min(n - 1 - k, NBUF - 2);
+        if constexpr (NBUF == 3) {
+            if (ahead >= 1) lp_wait_vm_barrier<NL>(); else lp_wait_vm_barrier<0>();
+        } else {
+            if (ahead >= 2) lp_wait_vm_barrier<2 * NL>(); else if (ahead == 1) lp_wait_vm_barrier<NL>(); else lp_wait_vm_barrier<0>();
+        }
+        if (k + NBUF - 1 < n) {
+            issue(ibuf, ib, iqy, iqx);
+            advance();
+        }
+        ibuf = ibuf + 1 == NBUF ? 0 : ibuf + 1;
+        const char* sb = reinterpret_cast<const char*>(smem + buf * bufF);
+        buf = buf + 1 == NBUF ? 0 : buf + 1;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            u32x4 ra[MF][2], rb[NB];
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) ra[f][u] = lp_lds_read(sb + aoff[ks][f][u]);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) rb[i] = lp_lds_read(sb + boff[ks] + 16 * i);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) asm volatile("" : "+v"(ra[f][u]));
+#pragma unroll
+            for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(rb[i]));
+            floatx8 fa[MF];
+#pragma unroll
+            for (int f = 0; f < MF; ++f) {
+                const floatx4 lo = __builtin_bit_cast(floatx4, ra[f][0]), hi = __builtin_bit_cast(floatx4, ra[f][1]);
+                fa[f] = floatx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+            float v[4 * NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const floatx4 p = __builtin_bit_cast(floatx4, rb[i]);
+                v[4 * i + 0] = p[0], v[4 * i + 1] = p[1], v[4 * i + 2] = p[2], v[4 * i + 3] = p[3];
+            }
+#pragma unroll
+            for (int kx = 0; kx < KK; ++kx) {
+                floatx8 fb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fb[j] = v[3 + kx + S * j];
+#pragma unroll
+                for (int f = 0; f < MF; ++f) acc[f][kx] = mma32x16<DT>(fa[f], fb, acc[f][kx]);
+            }
+        }
+    }
+
+    const int c = c0 + r;
+    if (c < a.C) {
+        float* out = a.partial + (size_t)blockIdx.z * a.M * a.C * T + (size_t)c * T + ky * KK;
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int m = m0 + (wm * MF + f) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (m < a.M) {
+                    float* o = out + (size_t)m * a.C * T;
+                    if constexpr (KK == 4) {
+                        *reinterpret_cast<floatx4*>(o) = floatx4{acc[f][0][reg], acc[f][1][reg], acc[f][2][reg], acc[f][3][reg]};
+                    } else {
+#pragma unroll
+                        for (int kx = 0; kx < KK; ++kx) o[kx] = acc[f][kx][reg];
+                    }
+                }
+            }
+    }
+}
+
 struct LpPlan {
     int S, KK, BM, WM, QC, splits, lds_bytes;
     int lds16;   // 1: a and lds_bytes hold the 16-bit geometry (wgrad_lp16_kernel)
@@ -1166,6 +1354,44 @@ bool lp16_plan(LpPlan& p) {
     return true;
 }
 
+// the fp32-map ring (wgrad_lpp_kernel): the depth LDM_WGRAD_RING asks for (default 3), shallower where the LDS is
+// short; 2 keeps the double-buffered wgrad_lp_kernel
+static int lp_ring_depth() {
+    static const int ring = [] {
+        const char* e = std::getenv("LDM_WGRAD_RING");
+        const int v = e ? (int)std::strtol(e, nullptr, 0) : 3;
+        return v < 2 ? 2 : (v > 4 ? 4 : v);
+    }();
+    return ring;
+}
+void lp32_ring(LpPlan& p) {
+    for (int nb = lp_ring_depth(); nb >= 3; --nb) {
+        const int bytes = nb * lp_buf_floats(p.BM, p.QC, p.a.pitch_c) * 4 + 1024;   // (+ the trash KB)
+        if (bytes <= 160 * 1024) {
+            p.nbuf = nb;
+            p.lds_bytes = bytes;
+            return;
+        }
+    }
+}
+
+template <int S, int KK, int BM, int WM, int QC, int DT, int NBUF>
+int launch_lpp(const LpPlan& p, hipStream_t st) {
+    constexpr int NW = WM * KK;
+    LDM_REQUIRE((kLC * (p.a.pitch_c / 4) + 63) / 64 <= lp_staged_pieces(S, KK, QC, NW) * NW, "wgrad ring (fp32): window slots");
+    LDM_REQUIRE(p.a.cols * p.a.rows == QC, "wgrad ring (fp32): chunk geometry");
+    auto kfn = wgrad_lpp_kernel<S, KK, BM, WM, QC, DT, NBUF>;
+    static bool opted = false;
+    if (!opted) {
+        LDM_HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        opted = true;
+    }
+    dim3 grid((p.a.C + kLC - 1) / kLC, (p.a.M + BM - 1) / BM, p.splits);
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), p.lds_bytes, st, p.a);
+    LDM_CHECK_LAUNCH("wgrad_lpp_kernel");
+    return 0;
+}
+
 template <int S, int KK, int BM, int WM, int QC, int DT>
 int launch_lp16(const LpPlan& p, hipStream_t st) {
     auto kfn = wgrad_lp16_kernel<S, KK, BM, WM, QC, DT>;
@@ -1219,6 +1445,8 @@ int launch_lp_dt(const LpPlan& p, hipStream_t st) {
         return launch_lp16<S, KK, BM, WM, QC, DT>(p, st);
     }
     if (p.a.dense16 || p.a.gath16) return launch_lp_xs<S, KK, BM, WM, QC, DT, DT>(p, st);
+    if (p.nbuf == 4) return launch_lpp<S, KK, BM, WM, QC, DT, 4>(p, st);
+    if (p.nbuf == 3) return launch_lpp<S, KK, BM, WM, QC, DT, 3>(p, st);
     return launch_lp_xs<S, KK, BM, WM, QC, DT, 0>(p, st);
 }
 template <int S, int KK, int QC, int DT>
@@ -1386,6 +1614,7 @@ int wgrad2_run(const ldm_conv_desc& d, const float* dense, const float* gath, fl
                 lp.lds16 = 1;
             }
         }
+        if (ok && !st16) wg::lp32_ring(lp);   // both maps fp32: the LDS-DMA ring
         if (ok && (!st16 || lp.lds16 || lp_staged_fits(lp))) {
             lp.a.dense = dense;
             lp.a.gath = gath;

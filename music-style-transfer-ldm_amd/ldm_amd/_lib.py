@@ -149,6 +149,7 @@ SIGNATURES = {
     "ldm_bneck_pv": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_vp]),
     "ldm_ca1_probs": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_int32, c_vp]),
     "ldm_ca1_probs_form": (c_int32, []),
+    "ldm_set_cin1_packed": (c_int32, [c_int32]),
     "ldm_q_sample": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_predict_start": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_sched_backward": (c_int32, [c_int32, c_fp, c_fp, c_int32, c_vp, c_fp, c_fp, c_int32, c_int64, c_vp]),
@@ -165,6 +166,7 @@ SIGNATURES = {
                                   c_fp, c_int32, c_float, c_fp, c_fp, c_int64, c_fp, c_vp]),
     # backward / optimiser
     "ldm_conv_tiled_plan": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, ctypes.POINTER(ConvPlan)]),
+    "ldm_conv_sconv_plan": (c_int32, [ctypes.POINTER(ConvDesc), c_int32, ctypes.POINTER(ConvPlan)]),
     "ldm_conv_storage16": (c_int32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvPlan)]),
     "ldm_conv_wgrad_storage16": (c_int32, [ctypes.POINTER(ConvDesc)]),
     "ldm_batchnorm_stats_code": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_int32, c_vp, c_fp, c_vp]),
@@ -175,6 +177,8 @@ SIGNATURES = {
                                    c_vp]),
     "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
                                          c_int32, c_fp, c_fp, c_fp, c_fp, c_vp]),
+    "ldm_batchnorm_backward_dxsum": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
+                                               c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_backward_reduce": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
                                                 c_int32, c_vp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_backward_apply": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,

@@ -5,6 +5,7 @@ requires grad) the call is wrapped in a torch.autograd.Function whose backward r
 backward kernels (ldm_amd.backward); a missing backward raises instead of silently detaching.
 """
 import contextlib
+import os
 
 import torch
 
@@ -12,6 +13,7 @@ from . import _lib as L
 from . import ops
 
 _BACKWARD = {}   # name -> callable(ctx, *grad_outputs) registered by ldm_amd.backward
+STATS = {"conv_bias_from_bn": 0}   # conv backwards that took their bias gradient from the BN's dx sum (tests)
 
 
 def register_backward(name):
@@ -108,10 +110,17 @@ def _conv_backward(ctx, gy):
     act = cfg["act"]
     if act == "gelu":
         raise NotImplementedError("conv backward with a fused GELU epilogue (apply GELU as its own op)")
+    # a train-mode BatchNorm's backward (its input is this conv's output) may have summed the gradient per channel
+    # as it wrote it (ops.batchnorm_backward dx_sum): that sum IS this conv's bias gradient
+    chan_sum = getattr(gy, "_ldm_chan_sum", None)
     gy = gy.contiguous()   # (a 16-bit map's gradient stays 16-bit: the kernels below read it as stored)
     need_v = nx or nw or nb
-    gv, gb, gbc = ops.act_backward(gy, act, act_out=a, need_dv=need_v, need_bias=nb and bn is None,
-                                   need_bcast=nbc)
+    if act == "none" and bn is None and not nbc and chan_sum is not None:
+        gv, gb, gbc = gy, (chan_sum if nb else None), None
+        STATS["conv_bias_from_bn"] += 1
+    else:
+        gv, gb, gbc = ops.act_backward(gy, act, act_out=a, need_dv=need_v, need_bias=nb and bn is None,
+                                       need_bcast=nbc)
     if bn is not None and need_v:
         g_, _b, _m, var, eps = bn
         zero = torch.zeros_like(var)
@@ -287,7 +296,8 @@ def _bn_train_backward(ctx, gy):
     nx, nw, nb = ctx.needs_input_grad[3:6]
     dx, dw, db = ops.batchnorm_backward(gy, y, x, sm, si, w, ctx.store["act"], need_dx=nx,
                                         need_w=nw and w is not None, need_b=nb and b is not None,
-                                        sync=ctx.store.get("sync", False), bias=b)
+                                        sync=ctx.store.get("sync", False), bias=b,
+                                        dx_sum=os.environ.get("LDM_AMD_BN_DXSUM", "1") != "0")
     return dx, dw, db
 
 

@@ -168,16 +168,21 @@ def get_plan(desc, force=None):
 _TILED_CACHE = {}
 
 
-def tiled_plan(desc, dt):
-    """The kind-3 plan (tconv.hip: LDS-staged 16-bit-operand implicit GEMM) for desc at operand precision dt,
-    or None when the layer is not of that kernel's class.  LDM_AMD_TILED=0 turns the path off."""
+def tiled_plan(desc, dt, adds=False):
+    """The 16-bit-operand LDS-staged plan for desc at operand precision dt: kind 3 (tconv.hip, large planes; no
+    + bcast / + skip epilogue, so not when `adds`), else kind 4 (sconv.hip, small planes, any epilogue), or None
+    when the layer is of neither class.  LDM_AMD_TILED=0 turns both off (LDM_AMD_SCONV=0 kind 4 alone)."""
     if dt == 0 or os.environ.get("LDM_AMD_TILED", "1") == "0":
         return None
-    key = (desc.key(), int(dt))
+    key = (desc.key(), int(dt), bool(adds))
     if key not in _TILED_CACHE:
+        lib = L.load()
         plan = L.ConvPlan()
-        rc = L.load().ldm_conv_tiled_plan(byref(desc), int(dt), byref(plan))
-        _TILED_CACHE[key] = plan if rc == 0 else None
+        ok = not adds and lib.ldm_conv_tiled_plan(byref(desc), int(dt), byref(plan)) == 0
+        if not ok:
+            plan = L.ConvPlan()
+            ok = lib.ldm_conv_sconv_plan(byref(desc), int(dt), byref(plan)) == 0
+        _TILED_CACHE[key] = plan if ok else None
     return _TILED_CACHE[key]
 
 
@@ -198,7 +203,7 @@ def packed_weight(weight, desc, plan, owner=None, tag=None):
         return weight
     owner = weight if owner is None else owner
     key = (owner._version, tag, desc.Cin, desc.Cout, desc.kh, desc.kw, desc.stride, desc.pad, desc.out_pad,
-           desc.transposed, plan.kind, plan.tm, plan.tn if plan.kind == 3 else 0)
+           desc.transposed, plan.kind, plan.tm, plan.tn if plan.kind in (3, 4) else 0)
     per = _PACK_CACHE.get(owner)
     if per is None:
         per = {}
@@ -336,8 +341,8 @@ def conv_forward(x, weight, bias=None, *, stride=1, padding=1, transposed=False,
         return out if out is not None else torch.empty((0, Cout, desc.Hout, desc.Wout), device=x.device,
                                                        dtype=torch.float32)
     dt = autocast_dt() if dtype is None else int(dtype)
-    if plan is None and bcast is None and skip is None:
-        plan = tiled_plan(desc, dt)
+    if plan is None:
+        plan = tiled_plan(desc, dt, adds=bcast is not None or skip is not None)
     plan = plan or get_plan(desc)
     wbuf = packed_weight(weight, desc, plan, *(wkey or ()))
     st = conv_storage16(desc, plan, dt)
@@ -573,7 +578,7 @@ def _allreduce_sum(t, group):
 
 
 def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=True, need_w=True, need_b=True,
-                       sync=False, bias=None):
+                       sync=False, bias=None, dx_sum=False):
     """Train-mode BN backward.  sync: SyncBatchNorm over the default group (True) or a given group.  The
     per-rank sums and the per-rank element count travel in ONE fp64 all-reduce of 2C+1 values; the apply
     stage reads the global count on the device (reduce.hip), so there is no host synchronisation.  For act
@@ -596,6 +601,15 @@ def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=Tr
     code = L.ACT[act] | st_code(st, x16=xh, y16=yh, dy16=dyh, dx16=xh and need_dx)
     pg = _sync_group(sync)
     if pg is None:
+        if dx_sum and dx is not None:
+            # + the per-channel sum of dx (the bias gradient of the conv that produced x), from the apply pass
+            # itself: attached to dx for that conv's backward (functional._conv_backward)
+            dxs = torch.empty(C, device=dy.device, dtype=torch.float32)
+            L.call("ldm_batchnorm_backward_dxsum", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
+                   save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, dx.data_ptr(), _p(dw), _p(db),
+                   dxs.data_ptr(), ws.data_ptr(), stream_handle())
+            dx._ldm_chan_sum = dxs
+            return dx, dw, db
         L.call("ldm_batchnorm_backward", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
                save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, _p(dx), _p(dw), _p(db),
                ws.data_ptr(), stream_handle())

@@ -241,3 +241,78 @@ def test_wgrad_mixed_maps(cuda, which):
         got = ops.conv_backward_weight(_rand((B, Cin, H, W), 61).to(cuda), g16.to(cuda), desc, dtype=dt)   # x fp32
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("dt", [0, 2])
+@pytest.mark.parametrize("k", [3, 4])
+def test_cin1_packed_form_is_bitwise_the_scalar_form(cuda, k, dt):
+    """conv_cin1_x4_kernel's packed form (two output channels per v_pk_fma_f32, each half an fma exactly as
+    v_fma_f32 rounds it, the same (ky, kx) order per output) against the scalar form, bitwise: the VAE / style
+    encoders' first layers (fp32 and bf16 operands, 16-bit output under bf16) and the data gradient of the decoder's
+    64 -> 1 output convT (a Cin = 1 conv); plus the fp32 form against float64 torch (1e-5).  Reference layers:
+    model.py:17 (Conv2d(1, 64, 3, 2, 1)), model.py:49 (ConvTranspose2d(64, 1, 4, 2, 1))."""
+    from ldm_amd import _lib as L, ops
+    lib = L.load()
+    x = _rand((4, 1, 64, 256), 41 + k)
+    w1 = _rand((64, 1, k, k), 42, -0.3, 0.3).to(cuda)
+    b1 = _rand((64,), 43, -0.1, 0.1).to(cuda)
+    kw = dict(stride=2, padding=1, act="relu", dtype=dt)
+    if dt:
+        kw["out_dtype"] = T[dt]
+    d2 = ops.make_desc(4, 64, 32, 128, 1, 4, 4, 2, 1, 0, True)
+    w2 = _rand((64, 1, 4, 4), 44, -0.2, 0.2).to(cuda)
+    r = _rand((4, 1, 64, 256), 45).to(cuda)
+    outs = []
+    prev = lib.ldm_set_cin1_packed(0)
+    try:
+        for pk in (0, 1):
+            lib.ldm_set_cin1_packed(pk)
+            y = ops.conv_forward(x.to(cuda), w1, b1, **kw)
+            dx = ops.conv_backward_data(r, w2, d2, dtype=dt)
+            torch.cuda.synchronize()
+            outs.append((y, dx))
+    finally:
+        lib.ldm_set_cin1_packed(prev)
+    (y0, dx0), (y1, dx1) = outs
+    assert torch.equal(y0, y1), float((y0.float() - y1.float()).abs().max())
+    assert torch.equal(dx0, dx1), float((dx0 - dx1).abs().max())
+    if dt == 0:
+        import torch.nn.functional as F
+        y64 = torch.relu(F.conv2d(x.double(), w1.cpu().double(), b1.cpu().double(), stride=2, padding=1))
+        assert float((y1.cpu().double() - y64).abs().max()) <= 1e-5 * float(y64.abs().max())
+
+
+@pytest.mark.parametrize("store16", [False, True])
+def test_conv_bias_grad_from_batchnorm_dx_sum(cuda, store16, monkeypatch):
+    """conv -> train-mode BatchNorm + ReLU (the VAE blocks, model.py:16-25, as models.model._conv_bn_act runs them):
+    the BN backward sums its dx per channel as it writes it (ldm_batchnorm_backward_dxsum) and the conv's backward
+    takes that sum as its bias gradient instead of sweeping dx again.  It equals the sum of the gradient reaching the
+    conv output (a tensor hook) to fp32 summation order, 16-bit storage included; LDM_AMD_BN_DXSUM=0 runs the sweep."""
+    from ldm_amd import functional as HF
+    if store16:
+        monkeypatch.setenv("LDM_AMD_STORE16_MIN", "1")
+    conv = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1).to(cuda)
+    bn = torch.nn.BatchNorm2d(128).to(cuda).train()
+    x = _rand((4, 64, 64, 128), 902).to(cuda)
+    gy = _rand((4, 128, 32, 64), 903).to(cuda)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("LDM_AMD_BN_DXSUM", flag)
+        conv.zero_grad()
+        seen = {}
+        before = HF.STATS["conv_bias_from_bn"]
+        ctx = torch.autocast("cuda", dtype=torch.bfloat16) if store16 else torch.autocast("cuda", enabled=False)
+        with ctx:
+            y = HF.conv(x, conv.weight, conv.bias, stride=2, padding=1, act="none")
+            y.register_hook(lambda g: seen.__setitem__("g", g))
+            z = HF.batchnorm(y, bn, "relu")
+        (z.float() * gy).sum().backward()
+        torch.cuda.synchronize()
+        took = HF.STATS["conv_bias_from_bn"] - before
+        g = seen["g"].float()
+        want = g.sum((0, 2, 3))
+        got = conv.bias.grad.clone()
+        scale = float(g.abs().sum((0, 2, 3)).max())
+        assert float((got - want).abs().max()) <= 1e-5 * scale, (flag, float((got - want).abs().max()), scale)
+        res.append(took)
+    assert res[0] > 0 and res[1] == 0
