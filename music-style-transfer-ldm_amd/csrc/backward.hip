@@ -133,7 +133,51 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
     if (g == 0 && i < MN) dw[i] = accumulate ? dw[i] + v : v;
 }
+// The same sums on 16-byte pieces (round 6): a thread owns four consecutive outputs, each summed in the order
+// above, so a wave-load moves 1 KB instead of 256 B (the partials of the train step's layers are ~38 MB per
+// layer: the scalar form read them at ~4.5 TB/s).  G comes from the piece count, ~2^18 threads as before.
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const floatx4* __restrict__ partial, int S, int MN4,
+                                                            floatx4* __restrict__ dw, int accumulate, int G) {
+    __shared__ floatx4 red[256];
+    const int NO = 256 / G;
+    const int ol = threadIdx.x % NO, g = threadIdx.x / NO;
+    const int i = blockIdx.x * NO + ol;
+    const int per = (S + G - 1) / G;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (i < MN4) {
+        const int s1 = min(S, (g + 1) * per);
+        int s = g * per;
+        for (; s + 8 <= s1; s += 8) {
+            floatx4 p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = partial[(size_t)(s + u) * MN4 + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v = v + p[u];
+        }
+        for (; s < s1; ++s) v = v + partial[(size_t)s * MN4 + i];
+    }
+    if (G > 1) {
+        red[threadIdx.x] = v;
+        for (int st = G / 2; st >= 1; st /= 2) {
+            __syncthreads();
+            if (g < st) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + st * NO];
+        }
+        __syncthreads();
+        v = red[ol];
+    }
+    if (g == 0 && i < MN4) dw[i] = accumulate ? dw[i] + v : v;
+}
 static void wgrad_reduce(const float* partial, int S, int MN, float* dw, int accumulate, hipStream_t st) {
+    static const bool vec = [] {   // LDM_WGRAD_REDUCE4=0: the scalar form (A/B timing)
+        const char* e = std::getenv("LDM_WGRAD_REDUCE4");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (vec && MN % 4 == 0 && (((uintptr_t)partial | (uintptr_t)dw) & 15) == 0) {
+        const int MN4 = MN / 4, G = wgrad_groups(S, MN4), NO = 256 / G;
+        hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((MN4 + NO - 1) / NO), dim3(256), 0, st,
+                           reinterpret_cast<const floatx4*>(partial), S, MN4, reinterpret_cast<floatx4*>(dw), accumulate, G);
+        return;
+    }
     const int G = wgrad_groups(S, MN), NO = 256 / G;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + NO - 1) / NO), dim3(256), 0, st, partial, S, MN, dw, accumulate,
                        G);

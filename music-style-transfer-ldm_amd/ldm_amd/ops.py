@@ -174,12 +174,15 @@ def tiled_plan(desc, dt, adds=False):
     when the layer is of neither class.  LDM_AMD_TILED=0 turns both off (LDM_AMD_SCONV=0 kind 4 alone)."""
     if dt == 0 or os.environ.get("LDM_AMD_TILED", "1") == "0":
         return None
-    key = (desc.key(), int(dt), bool(adds))
+    # kind 4 under fp16 only with LDM_AMD_SCONV_F16=1: there the general kernel keeps fp32 operands, and the
+    # reference-fp16 GradScaler step's parity bound (tests/test_gpu_train_fp16.py) was set on that form
+    k4 = int(dt) == 2 or os.environ.get("LDM_AMD_SCONV_F16", "0") == "1"
+    key = (desc.key(), int(dt), bool(adds), k4)
     if key not in _TILED_CACHE:
         lib = L.load()
         plan = L.ConvPlan()
         ok = not adds and lib.ldm_conv_tiled_plan(byref(desc), int(dt), byref(plan)) == 0
-        if not ok:
+        if not ok and k4:
             plan = L.ConvPlan()
             ok = lib.ldm_conv_sconv_plan(byref(desc), int(dt), byref(plan)) == 0
         _TILED_CACHE[key] = plan if ok else None

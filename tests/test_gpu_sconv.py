@@ -51,6 +51,11 @@ def _rel(a, b):
     return float((a.double().cpu() - b).abs().max()) / max(float(b.abs().max()), 1e-30)
 
 
+@pytest.fixture(autouse=True)
+def _sconv_f16(monkeypatch):
+    monkeypatch.setenv("LDM_AMD_SCONV_F16", "1")   # fp16 takes kind 4 here too (the train step: bf16 only)
+
+
 @pytest.mark.parametrize("dt", [2, 1])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_sconv_forward_vs_float64(cuda, case, dt):

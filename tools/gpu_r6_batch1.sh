@@ -10,9 +10,11 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 420 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_sconv.py \
     tests/test_gpu_wgrad_ring32.py tests/test_gpu_store16.py > $OUT/tests_kernels.log 2>&1 || { tail -40 $OUT/tests_kernels.log; exit 1; }
 tail -1 $OUT/tests_kernels.log
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_train.py \
-    tests/test_gpu_train_config3.py tests/test_gpu_train_fp16.py tests/test_gpu_config4_rank.py \
-    tests/test_gpu_reference_shapes.py tests/test_gpu_graph_state.py > $OUT/tests_train.log 2>&1 || { tail -40 $OUT/tests_train.log; exit 1; }
+# (-s: nothing captured, so a runtime / RCCL abort message stays in the log)
+timeout -k 10 600 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread tests/test_gpu_config4_rank.py \
+    tests/test_gpu_dp_graph.py tests/test_gpu_train.py tests/test_gpu_train_config3.py tests/test_gpu_train_fp16.py \
+    tests/test_gpu_reference_shapes.py tests/test_gpu_graph_state.py tests/test_gpu_shape_s.py \
+    > $OUT/tests_train.log 2>&1 || { grep -v "^  File" $OUT/tests_train.log | tail -40; exit 1; }
 tail -1 $OUT/tests_train.log
 LDM_CIN1_PK=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_train_config3.py \
     > $OUT/tests_pk.log 2>&1 || { tail -30 $OUT/tests_pk.log; exit 1; }
@@ -38,6 +40,7 @@ for round in 1 2; do
   run_train nopk_$round LDM_CIN1_PK=0 || exit 1
   run_train nosconv_$round LDM_AMD_SCONV=0 LDM_CIN1_PK=1 || exit 1
   run_train nodxsum_$round LDM_AMD_BN_DXSUM=0 LDM_CIN1_PK=1 || exit 1
+  run_train noreduce4_$round LDM_WGRAD_REDUCE4=0 LDM_CIN1_PK=1 || exit 1
 done
 for sp in 1 2; do
   timeout -k 10 180 python -u bench.py --steps 20 --warmup 3 --split $sp --no-cpu-baseline --no-kernel-timing \
@@ -47,6 +50,9 @@ for sp in 1 2; do
       > $OUT/transfer_$sp.json 2> $OUT/transfer.err || { tail -20 $OUT/transfer.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/transfer_$sp.json')); print('transfer split $sp', d['us_per_denoise_iteration'], 'us/iter')"
 done
+timeout -k 10 240 python -u bench.py --workload stress --steps 3 --warmup 1 > $OUT/stress.json 2> $OUT/stress.err \
+    || { tail -20 $OUT/stress.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/stress.json')); print('stress', d['us_per_denoise_iteration'], 'us/iter', d.get('roofline'), d.get('cpu_baseline', {}).get('value'))"
 cd /tmp && export TMPDIR=/tmp
 LDM_CIN1_PK=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof_train -o run -- \
     python3 $GRAFT_REPO_ROOT/bench.py --workload train --steps 5 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof_train.log 2>&1 \
