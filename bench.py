@@ -117,21 +117,20 @@ STEP_LAYERS = [  # (name, Cin, Cout, mode 0 conv s1 / 1 conv s2 / 2 convT s2, in
     ("enc1", 32, 64, 0, 1), ("enc2", 64, 128, 1, 1), ("enc3", 128, 256, 1, 2), ("enc4", 256, 512, 1, 4),
     ("bottleneck", 512, 512, 0, 8), ("dec4", 512, 256, 2, 8), ("dec3", 256, 128, 2, 4), ("dec2", 128, 64, 2, 2)]
 def _layer_forms():
-    """(USTEP_LAYERS, KS_LAYERS): the layers use_step 2 runs on ustep.hip / on uconv.hip's K-split form, as the
-    library reports them (ldm_step_layer_forms; LDM_USTEP_LAYERS / LDM_UCONV_KS override its defaults)."""
+    """KS_LAYERS: the layers the loop runs on uconv.hip's K-split form, as the library reports them
+    (ldm_step_layer_forms; LDM_UCONV_KS overrides its default)."""
     from ldm_amd import _lib as L
-    u, k = L.step_layer_forms()
-    return tuple(l for l in range(9) if (u >> l) & 1), tuple(l for l in range(9) if (k >> l) & 1)
+    k = L.step_layer_forms()
+    return tuple(l for l in range(9) if (k >> l) & 1)
 
 
 def time_step_layers(engine, B, H, W, dev, reps=50):
     """Average launch duration of each kernel of the reverse loop's UNet step, launched exactly as the loop
-    launches it (the engine's packed step weights and folded biases; ustep.hip for USTEP_LAYERS under
-    use_step 2, else uconv.hip), timed as a dependent chain of `reps` launches in one hipGraph with HIP
+    launches it (the engine's packed step weights and folded biases on uconv.hip), timed as a dependent chain of `reps` launches in one hipGraph with HIP
     events on the launching stream.  dec1 runs fused with the DDIM update and is not timed alone."""
     from ldm_amd import _lib as L
     lib = L.load()
-    USTEP_LAYERS, KS_LAYERS = _layer_forms()
+    KS_LAYERS = _layer_forms()
     shape = engine.shape(B, 32, H, W)
     w = engine.weights(shape)
     out = {}
@@ -162,16 +161,13 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         bc = torch.randn(B, cout, device=dev) if layer == 1 else None
         sk = torch.randn(B, hout, wout, cout, device=dev) if mode == 2 else None
         dt = int(w.step_dtype)
-        v3 = int(w.use_step) == 2 and dt == 0 and layer in USTEP_LAYERS and B % 4 == 0 and (H, W) == (16, 64)
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else int(lib.ldm_step_workspace_floats(B, H, W))
+        nws = int(lib.ldm_step_workspace_floats(B, H, W))
         ws = torch.zeros(max(1, nws), device=dev)
         args = (x.data_ptr(), w.step_w[layer], bias, None if bc is None else bc.data_ptr(),
                 None if sk is None else sk.data_ptr(), y.data_ptr())
 
         def run():
             stp = torch.cuda.current_stream().cuda_stream
-            if v3:
-                return lib.ldm_ustep_conv(layer, B, *args, ws.data_ptr() if nws else None, stp)
             return lib.ldm_step_conv_ws(layer, B, H, W, *args, dt, ws.data_ptr() if nws else None, stp)
 
         L.check(run(), name)
@@ -180,8 +176,7 @@ def time_step_layers(engine, B, H, W, dev, reps=50):
         fl = 2.0 * B * cout * hout * wout * cin * taps
         by = (2.0 if dt else 4.0) * cin * cout * 9 + 4.0 * (B * cin * hin * win + B * cout * hout * wout)
         out[name] = {"us": round(us, 3), "tflops": round(fl / us / 1e6, 2), "gbs": round(by / us / 1e3, 1),
-                     "flops": fl, "bytes": by, "kernel": (("ustep_kernel<%d>" % layer) if v3 else
-                                                          ("uconv_kernel (K split)" if layer in KS_LAYERS else "uconv_kernel"))
+                     "flops": fl, "bytes": by, "kernel": ("uconv_kernel (K split)" if layer in KS_LAYERS else "uconv_kernel")
                      + ("" if dt == 0 else (" fp16 operands" if dt == 1 else " bf16 operands"))}
     # the folded cross-attentions of the loop (CA1: its probabilities only when the bottleneck takes the values)
     for name, E, Lt in (("attn2_folded", 256, H * W // 16), ("attn1_folded", 512, H * W // 64)):

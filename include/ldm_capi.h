@@ -309,8 +309,8 @@ typedef struct ldm_unet_weights {
     /* Step kernels of the reverse loop (used when use_step != 0 together with use_fold, for latent C = 32
      * and num_filters = 64): the nine convs packed by ldm_step_pack_weight (enc4 / bottleneck: their
      * folded weights), and the folded position biases transposed to [Hout*Wout][Cout].  use_step 1: the
-     * register-direct kernels (uconv.hip, any latent with H, W multiples of 8); 2: the LDS-staged kernels
-     * (ustep.hip) where they apply (latent 16 x 64, B a multiple of 4), else as 1. */
+     * register-direct kernels (uconv.hip, any latent with H, W multiples of 8); 2: the same (it selected the
+     * LDS-staged kernels of rounds 2-5, measured slower and removed in round 6). */
     const float* step_w[9];
     const float* step_pb[2];
     int32_t use_step;
@@ -395,33 +395,12 @@ int ldm_step_conv_ws(int32_t layer, int32_t B, int32_t H, int32_t W, const float
 int ldm_step_dec1_ddim(int32_t B, int32_t H, int32_t W, const float* d2, const float* packed, const float* bias,
                        const float* coef, float eta, float* xs, float* x0_log, float* eps_log, int32_t dtype,
                        void* stream);
-/* 1 when this library is the diagnostic build (make DIAG=1: lib/libldm_amd_diag.so), which adds the reverse-loop
- * forms measured and not kept: the layer pairs below and the LDS-staged ustep.hip kernels.  In the shipped
- * build (0) ldm_step_set_pairs only records the mask (no pair runs) and the ldm_ustep_* entry points report
- * that they are absent (-1 / an error code). */
-int32_t ldm_step_diag_build(void);
-/* Layer pairs of the reverse loop (ldm_ddim_sample with use_step): bit l of `mask` runs layers l and l + 1
- * as ONE launch whose first blocks compute layer l and hand their output tiles to layer l + 1's blocks
- * inside the launch (write-through stores, a sharded arrival count; the consumer blocks stream their
- * weights before they wait).  Pairs start at l = 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1, with
- * LDM_UCONV_DEC1_THIN=0 only);
- * other bits are ignored.  Takes effect for loops issued (or graphs captured) afterwards; returns the
- * previous mask.  A negative mask only reads it.  Default: LDM_UPAIR, else the measured choice. */
-int32_t ldm_step_set_pairs(int32_t mask);
-/* Which form each reverse-loop layer runs under use_step 2 (bit l = layer l): ustep_layers on the LDS-staged
- * ustep.hip kernels (LDM_USTEP_LAYERS, default none), ks_layers on uconv.hip's K-split form
- * (LDM_UCONV_KS, default enc4 + bottleneck); every other layer on uconv.hip's single-block form. */
-int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers);
+/* Which reverse-loop layers run uconv.hip's K-split form (bit l = layer l; LDM_UCONV_KS, default enc4 +
+ * bottleneck + dec4); every other layer runs the single-block form. */
+int ldm_step_layer_forms(int32_t* ks_layers);
 /* ldm_step_conv with an operand precision LDM_DT_* (ldm_step_conv = LDM_DT_F32). */
 int ldm_step_conv_dt(int32_t layer, int32_t B, int32_t H, int32_t W, const float* x, const float* packed,
                      const float* bias, const float* bcast, const float* skip, float* y, int32_t dtype, void* stream);
-/* The LDS-staged variant (ustep.hip) of the same layers at the canonical latent H = 16, W = 64 with B a
- * multiple of 4 (else -1).  The deep layers split K across blocks: they need a zero-filled workspace of
- * ldm_ustep_workspace_floats(layer, B) floats (0: none), which they leave zero-filled; layers running one
- * after another on a stream may share one.  Same packed weights and epilogue as ldm_step_conv. */
-int64_t ldm_ustep_workspace_floats(int32_t layer, int32_t B);
-int ldm_ustep_conv(int32_t layer, int32_t B, const float* x, const float* packed, const float* bias,
-                   const float* bcast, const float* skip, float* y, float* workspace, void* stream);
 
 /* ---- train step backward (LDMTrainer.train_step, train.py:163-208: scaler.scale(loss).backward()) ---
  * Data gradients of a conv are the forward kernel on the dual descriptor (conv <-> transposed conv);

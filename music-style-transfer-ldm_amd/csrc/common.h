@@ -236,29 +236,14 @@ struct StepConv {
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st);
 int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats = nullptr);
 int step_ks_mask();   // layers running the K-split step form (LDM_UCONV_KS)
-// LDM_STEP_DIAG (make DIAG=1, lib/libldm_amd_diag.so): the reverse-loop forms measured and not kept — the
-// LDS-staged step kernels (ustep.hip) and the in-launch layer pairs (uconv.hip upair_kernel).  The shipped
-// library reports them unsupported.
-#ifndef LDM_STEP_DIAG
-#define LDM_STEP_DIAG 0
-#endif
-
-// LDM_DEBUG_BOUNDS (on in the diagnostic build): the multi-tensor optimizer kernels check the chunk map they
+// LDM_DEBUG_BOUNDS (make DIAG=1: the diagnostic library lib/libldm_amd_diag.so): the multi-tensor optimizer kernels check the chunk map they
 // index the slot table with (chunk_tensor[i] in [0, nchunks), chunk_start >= 0, a non-null gradient) and print
 // and skip a bad chunk instead of dereferencing it (round 5's aperture violation in unscale_check_kernel read
 // a slot table that the graph's own scratch had overwritten)
 #ifndef LDM_DEBUG_BOUNDS
-#define LDM_DEBUG_BOUNDS LDM_STEP_DIAG
+#define LDM_DEBUG_BOUNDS 0
 #endif
-// Two consecutive step layers in one launch with an in-launch hand-off (uconv.hip upair_kernel); pairs start
-// at layer 0 (enc1+enc2), 6 (dec3+dec2), 7 (dec2+dec1).
-bool step_pair_supported(int la, int W);
-int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& sb, hipStream_t st);
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st);
-// ustep.hip: the LDS-staged step kernels at the canonical latent (16 x 64, batch a multiple of 4)
-bool ustep_supported(int B, int H, int W);
-int64_t ustep_workspace_floats(int layer, int B, int64_t* cnt_floats = nullptr);
-int ustep_conv(int layer, int B, const StepConv& s, float* ws, hipStream_t st);
 
 // wgrad.hip: the tap-shared weight-gradient kernel (ldm_conv_backward_weight where it applies)
 bool wgrad2_plan_ws(const ldm_conv_desc& d, int64_t& ws_floats);

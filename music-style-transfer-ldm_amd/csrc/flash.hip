@@ -32,12 +32,14 @@ __device__ __forceinline__ floatx4 mma(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// [D][64] tile of a channel-major slab (row c at src + c*n, tokens t0 .. t0+63, zero past n) -> LDS
-// [D][kKP]; every load of the thread in flight before its first store.
+// [D][64] tile of a channel-major slab (row c at src + c*n, tokens t0 .. t0+63, zero past n) -> registers
+// (every load of the thread in flight at once), then -> LDS [D][kKP].  Split in two so that a kernel can issue
+// the next tile's loads before it computes on the current one.
 template <int D>
-__device__ __forceinline__ void stage_cs(const float* __restrict__ src, int n, int t0, float* __restrict__ dst) {
-    constexpr int NIT = D * (kTok / 4) / 256;
-    float4 v[NIT];
+constexpr int cs_pieces() { return D * (kTok / 4) / 256; }
+template <int D>
+__device__ __forceinline__ void load_cs(const float* __restrict__ src, int n, int t0, float4 (&v)[cs_pieces<D>()]) {
+    constexpr int NIT = cs_pieces<D>();
     const bool vec = (n & 3) == 0 && t0 + kTok <= n;
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
@@ -53,8 +55,11 @@ __device__ __forceinline__ void stage_cs(const float* __restrict__ src, int n, i
             v[u].w = t + 3 < n ? p[3] : 0.f;
         }
     }
+}
+template <int D>
+__device__ __forceinline__ void store_cs(const float4 (&v)[cs_pieces<D>()], float* __restrict__ dst) {
 #pragma unroll
-    for (int u = 0; u < NIT; ++u) {
+    for (int u = 0; u < cs_pieces<D>(); ++u) {
         const int e = u * 256 + (int)threadIdx.x;
         *reinterpret_cast<float4*>(dst + (e / (kTok / 4)) * kKP + 4 * (e % (kTok / 4))) = v[u];
     }
@@ -120,9 +125,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ out, float* __restrict__ lse, int E,
                                                         int heads, int L, int S, float scale) {
     constexpr int NJ = D / 16;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* Ks = sm;              // [D][kKP]
-    float* Vs = sm + D * kKP;    // [D][kKP]
+    extern __shared__ __attribute__((aligned(16))) float sm[];   // 2 x {K [D][kKP], V [D][kKP]}
     const int nqt = (L + kTok - 1) / kTok;
     const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
     const int h = bh % heads, b = bh / heads;
@@ -143,21 +146,36 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
     for (int ct = 0; ct < NJ; ++ct) o[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
 
-    for (int s0 = 0; s0 < S; s0 += kTok) {
-        __syncthreads();
-        stage_cs<D>(kb, S, s0, Ks);
-        stage_cs<D>(vb, S, s0, Vs);
-        __syncthreads();
-        // S^T[s][l] for the tile's 64 keys (4 tiles of 16): lane holds keys s0 + 16 st + 4 lg + r of query l
+    // K / V tiles double-buffered in LDS, the next tile's loads in registers while the current one is multiplied:
+    // tile t+1 is stored into the buffer tile t-1 used (every wave left it at the barrier closing iteration t-1),
+    // then tile t+2's loads are issued; one barrier per tile.  (Round 6: the single-buffered form waited out
+    // a load round trip per 64-key tile, 364 us per launch at L = S = 4096.)
+    const int nt = (S + kTok - 1) / kTok;
+    float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
+    load_cs<D>(kb, S, 0, rk);
+    load_cs<D>(vb, S, 0, rv);
+    store_cs<D>(rk, sm);
+    store_cs<D>(rv, sm + D * kKP);
+    if (nt > 1) {
+        load_cs<D>(kb, S, kTok, rk);
+        load_cs<D>(vb, S, kTok, rv);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const int s0 = t * kTok;
+        const float* Ks = sm + (t & 1) * (2 * D * kKP);   // [D][kKP]
+        const float* Vs = Ks + D * kKP;                   // [D][kKP]
+        // S^T[s][l] for the tile's 64 keys (4 tiles of 16): lane holds keys s0 + 16 st + 4 lg + r of query l; the
+        // four key tiles' chains interleaved (each chain still sums jj, i in order)
         floatx4 sc[4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            sc[st] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < 4; ++st) sc[st] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int jj = 0; jj < NJ; ++jj)
+        for (int jj = 0; jj < NJ; ++jj)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) sc[st] = mma(Ks[(16 * jj + 4 * lg + i) * kKP + 16 * st + col], qf[jj][i], sc[st]);
-        }
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int st = 0; st < 4; ++st) sc[st] = mma(Ks[(16 * jj + 4 * lg + i) * kKP + 16 * st + col], qf[jj][i], sc[st]);
         // online softmax over s (the 4 lanes of query col share its statistics)
         float tmax = -INFINITY;
 #pragma unroll
@@ -181,19 +199,33 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
         tsum += __shfl_xor(tsum, 32);
         lsum = lsum * alpha + tsum;
         m = mnew;
-        // O^T[c][l] = alpha O^T + sum_s V[c][s] P[l][s]
+        // O^T[c][l] = alpha O^T + sum_s V[c][s] P[l][s] (the NJ channel tiles' chains interleaved)
 #pragma unroll
-        for (int ct = 0; ct < NJ; ++ct) {
-            o[ct] *= alpha;
+        for (int ct = 0; ct < NJ; ++ct) o[ct] *= alpha;
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const float4 va = *reinterpret_cast<const float4*>(Vs + (16 * ct + col) * kKP + 16 * st + 4 * lg);
-                o[ct] = mma(va.x, p[st][0], o[ct]);
-                o[ct] = mma(va.y, p[st][1], o[ct]);
-                o[ct] = mma(va.z, p[st][2], o[ct]);
-                o[ct] = mma(va.w, p[st][3], o[ct]);
+        for (int st = 0; st < 4; ++st) {
+            float4 va[NJ];
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) va[ct] = *reinterpret_cast<const float4*>(Vs + (16 * ct + col) * kKP + 16 * st + 4 * lg);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) o[ct] = mma(va[ct].x, p[st][0], o[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) o[ct] = mma(va[ct].y, p[st][1], o[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) o[ct] = mma(va[ct].z, p[st][2], o[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) o[ct] = mma(va[ct].w, p[st][3], o[ct]);
+        }
+        if (t + 1 < nt) {
+            float* nb = sm + ((t + 1) & 1) * (2 * D * kKP);
+            store_cs<D>(rk, nb);
+            store_cs<D>(rv, nb + D * kKP);
+            if (t + 2 < nt) {
+                load_cs<D>(kb, S, (t + 2) * kTok, rk);
+                load_cs<D>(vb, S, (t + 2) * kTok, rv);
             }
         }
+        __syncthreads();
     }
     if (!lok) return;
     // lane holds O[l][c] for c = 16 ct + 4 lg + r
@@ -335,9 +367,7 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restri
                                                            const float* __restrict__ delta, float* __restrict__ dq,
                                                            int E, int heads, int L, int S, float scale) {
     constexpr int NJ = D / 16;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* Ks = sm;              // [D][kKP]
-    float* Vs = sm + D * kKP;    // [D][kKP]
+    extern __shared__ __attribute__((aligned(16))) float sm[];   // 2 x {K [D][kKP], V [D][kKP]}
     const int nqt = (L + kTok - 1) / kTok;
     const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
     const int h = bh % heads, b = bh / heads;
@@ -357,40 +387,68 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restri
 #pragma unroll
     for (int ct = 0; ct < NJ; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    for (int s0 = 0; s0 < S; s0 += kTok) {
-        __syncthreads();
-        stage_cs<D>(kb, S, s0, Ks);
-        stage_cs<D>(vb, S, s0, Vs);
-        __syncthreads();
+    // K / V tiles double-buffered as in flash_fwd_kernel
+    const int nt = (S + kTok - 1) / kTok;
+    float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
+    load_cs<D>(kb, S, 0, rk);
+    load_cs<D>(vb, S, 0, rv);
+    store_cs<D>(rk, sm);
+    store_cs<D>(rv, sm + D * kKP);
+    if (nt > 1) {
+        load_cs<D>(kb, S, kTok, rk);
+        load_cs<D>(vb, S, kTok, rv);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const int s0 = t * kTok;
+        const float* Ks = sm + (t & 1) * (2 * D * kKP);   // [D][kKP]
+        const float* Vs = Ks + D * kKP;                   // [D][kKP]
         float ds[4][4];
+        floatx4 sv[4], dp[4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            floatx4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < 4; ++st) sv[st] = dp[st] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int jj = 0; jj < NJ; ++jj)
+        for (int jj = 0; jj < NJ; ++jj)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
                     const int a = (16 * jj + 4 * lg + i) * kKP + 16 * st + col;
-                    sv = mma(Ks[a], qf[jj][i], sv);
-                    dp = mma(Vs[a], of[jj][i], dp);
+                    sv[st] = mma(Ks[a], qf[jj][i], sv[st]);
+                    dp[st] = mma(Vs[a], of[jj][i], dp[st]);
                 }
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const bool ok = s0 + 16 * st + 4 * lg + r < S;
-                const float pv = ok ? expf(sv[r] - ll) : 0.f;
-                ds[st][r] = pv * (dp[r] - dl);
+                const float pv = ok ? expf(sv[st][r] - ll) : 0.f;
+                ds[st][r] = pv * (dp[st][r] - dl);
+            }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            float4 ka[NJ];
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) ka[ct] = *reinterpret_cast<const float4*>(Ks + (16 * ct + col) * kKP + 16 * st + 4 * lg);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) acc[ct] = mma(ka[ct].x, ds[st][0], acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) acc[ct] = mma(ka[ct].y, ds[st][1], acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) acc[ct] = mma(ka[ct].z, ds[st][2], acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct) acc[ct] = mma(ka[ct].w, ds[st][3], acc[ct]);
+        }
+        if (t + 1 < nt) {
+            float* nb = sm + ((t + 1) & 1) * (2 * D * kKP);
+            store_cs<D>(rk, nb);
+            store_cs<D>(rv, nb + D * kKP);
+            if (t + 2 < nt) {
+                load_cs<D>(kb, S, (t + 2) * kTok, rk);
+                load_cs<D>(vb, S, (t + 2) * kTok, rv);
             }
         }
-#pragma unroll
-        for (int ct = 0; ct < NJ; ++ct)
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const float4 ka = *reinterpret_cast<const float4*>(Ks + (16 * ct + col) * kKP + 16 * st + 4 * lg);
-                acc[ct] = mma(ka.x, ds[st][0], acc[ct]);
-                acc[ct] = mma(ka.y, ds[st][1], acc[ct]);
-                acc[ct] = mma(ka.z, ds[st][2], acc[ct]);
-                acc[ct] = mma(ka.w, ds[st][3], acc[ct]);
-            }
+        __syncthreads();
     }
     if (!lok) return;
     float* db = dq + ((size_t)b * E + (size_t)h * D + 4 * lg) * L + l;
@@ -410,7 +468,7 @@ static int opt_in_lds(K kernel, size_t bytes) {
 template <int D, bool TOK, bool LSE>
 static int fwd_launch(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
                       float scale, hipStream_t st) {
-    const size_t lds = 2 * (size_t)D * kKP * sizeof(float);
+    const size_t lds = 4 * (size_t)D * kKP * sizeof(float);   // K and V, two buffers each
     static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE>, lds);
     if (opted) return opted;
     const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
@@ -433,7 +491,7 @@ static int bwd_launch(const float* q, const float* kv, const float* out, const f
     hipLaunchKernelGGL(flash_bwd_dkv_kernel<D>, dim3((unsigned)B * heads * ((S + kTok - 1) / kTok)), dim3(256), lds_kv,
                        st, q, kv, dout, lse, delta, dkv, E, heads, L, S, scale);
     LDM_CHECK_LAUNCH("flash_bwd_dkv_kernel");
-    const size_t lds_q = 2 * (size_t)D * kKP * sizeof(float);
+    const size_t lds_q = 4 * (size_t)D * kKP * sizeof(float);   // K and V, two buffers each
     static int o2 = opt_in_lds(flash_bwd_dq_kernel<D>, lds_q);
     if (o2) return o2;
     hipLaunchKernelGGL(flash_bwd_dq_kernel<D>, dim3((unsigned)B * heads * ((L + kTok - 1) / kTok)), dim3(256), lds_q, st,

@@ -76,19 +76,6 @@ struct UArgs {
     int32_t* cnt;         // KS > 1: arrival counter per tile (zero between launches)
 };
 
-// In-launch hand-off of a layer pair (upair_kernel): the producer layer's blocks publish their output tiles
-// with write-through (sc1) stores, drain them, then count themselves on cnt[bid % 8]; the consumer layer's
-// blocks issue their weight (A) loads and epilogue operands first, wait until the eight shards sum to
-// `target`, and read the producer's output only with sc1 loads (MI355X_MICROARCH.md, Valid forms).  The last
-// consumer to pass the wait zeroes the shards (zero between launches, like the split-K tile counters).
-// cnt[9] is a sticky error word: a wait that exceeds its bound sets it instead of hanging the GPU.
-struct PairSync {
-    int32_t* cnt;      // [0..7] producer arrivals, [8] consumer passes, [9] timeout flag (zero-filled once)
-    int32_t target;    // producer blocks that run an epilogue (the producer's tile count)
-    int32_t nA, nB;    // producer / consumer blocks of the launch
-};
-enum : int { ROLE_PLAIN = 0, ROLE_PRODUCER = 1, ROLE_CONSUMER = 2 };
-
 // (ky, kx) of tap t and the conv input offset / the transposed conv's output parity
 __host__ __device__ constexpr int tky(int t) { return t / 3; }
 __host__ __device__ constexpr int tkx(int t) { return t % 3; }
@@ -143,11 +130,9 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS, int ROLE>
-__device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const PairSync& ps) {
+template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS>
+__device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in) {
     constexpr int NPH = MODE == 2 ? 4 : 1;
-    static_assert(ROLE != ROLE_CONSUMER || NCH == S, "a consumer issues its whole weight stream before the wait");
-    static_assert(ROLE != ROLE_PRODUCER || (EPI & EPI_DDIM) == 0, "dec1 ends the step: never a producer");
     constexpr int NST = NCH / S;
     constexpr int CPC = 9;                        // chunks per channel chunk (the 9 taps)
     static_assert(NCH % S == 0 && NCH % CPC == 0, "stage / chunk structure");
@@ -232,8 +217,6 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
     constexpr int WBYTES = 9 * CIN * COUT * AE;
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc(uni_ptr(a.w), (short)0, WBYTES, 0x00020000);
-    [[maybe_unused]] const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
-        uni_ptr(a.y), (short)0, uni(a.B * a.Hout * a.Wout * COUT * 4), 0x00020000);
     const int va = ((m0 + col) * 16 + lg * 4) * AE;            // A: row m0+col, k-local 4*lg .. +3
     const int kw0 = ks * WK + wk;                              // this wave's slice of K
     const int sa0 = uni(kw0 * NCH * COUT * 16 * AE);           // first chunk of this wave
@@ -249,10 +232,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
 #pragma unroll
                 for (int ni = 0; ni < TN; ++ni) acc[u][p][mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    constexpr int XAUX = ROLE == ROLE_CONSUMER ? 16 : UCONV_XAUX;   // 16: sc1 (the producer's stores are sc1)
-    // a consumer whose wait passed its bound writes NaN, so that a pair launch can never return plausible but
-    // wrong activations (the sticky word cnt[9] records it as well)
-    [[maybe_unused]] int poison = 0;
+    constexpr int XAUX = UCONV_XAUX;
     AT fa[NST > 1 ? 2 : 1][S][TM];
     floatx4 fb[NST > 1 ? 2 : 1][S][TN];
     // PART bit 0: weight (A) fragments, bit 1: activation (B) fragments
@@ -368,7 +348,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
     UCONV_STAMP(1);
     using AB = std::integral_constant<int, 3>;
     constexpr bool PLANE = (EPI & EPI_PLANE) != 0;
-    static_assert(!PLANE || (NST == 1 && S % CPC == 0 && ROLE == ROLE_PLAIN), "EPI_PLANE geometry");
+    static_assert(!PLANE || (NST == 1 && S % CPC == 0), "EPI_PLANE geometry");
     if constexpr (PLANE && MODE == 1) {
         // stride 2 onto a 2 x 8 output plane: each sample's whole 4 x 16 input plane (64 positions, 4 loads per
         // lane per channel chunk) goes to the wave's LDS window; tap (ky, kx) of output (qy, qx) reads input
@@ -506,7 +486,7 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
             });
         });
     } else if constexpr ((EPI & EPI_WINDOW) != 0) {
-        static_assert(NST == 1 && S % CPC == 0 && ROLE == ROLE_PLAIN, "EPI_WINDOW geometry");
+        static_assert(NST == 1 && S % CPC == 0, "EPI_WINDOW geometry");
         constexpr int NCC = S / CPC;           // channel chunks of this wave
         // the input rows and columns the wave's 16 TN output columns (one row of the column grid) read:
         // stride 1: rows y0-1..y0+1, columns x0-1..x0+16TN; stride 2: rows 2y0-1..2y0+1, columns
@@ -567,35 +547,6 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 }
             });
         });
-    } else if constexpr (ROLE == ROLE_CONSUMER) {
-        // the weights and the epilogue operands do not depend on the producer: in flight before the wait
-        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-        epi_prefetch();
-        __builtin_amdgcn_sched_barrier(0);
-        if (threadIdx.x == 0) {
-            int spins = 0, timed_out = 0;
-            for (;;) {
-                int s = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) s += __hip_atomic_load(ps.cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (s >= ps.target) break;
-                if (++spins > (1 << 18)) {   // bounded: report instead of hanging, and poison this block's output
-                    __hip_atomic_store(ps.cnt + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    timed_out = 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (__hip_atomic_fetch_add(ps.cnt + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ps.nB - 1) {
-#pragma unroll
-                for (int i = 0; i < 9; ++i) __hip_atomic_store(ps.cnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            reinterpret_cast<int*>(smem)[0] = timed_out;   // (a consumer holds no LDS window: smem is free here)
-        }
-        __syncthreads();
-        poison = reinterpret_cast<const int*>(smem)[0];
-        __syncthreads();   // read before the K reduction or the split-K flag reuse smem
-        load_stage(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
     } else {
         load_stage(std::integral_constant<int, 0>{}, AB{});
         if constexpr (NST == 1) epi_prefetch();
@@ -715,9 +666,6 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = round16(o[r] + pre_s[k][r], DT);
         }
-        if constexpr (ROLE == ROLE_CONSUMER) {
-            if (poison) o = floatx4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
-        }
         if constexpr ((EPI & EPI_DDIM) != 0) {
             // noise_pred = o; the reverse update of model.py:442-458 (ddim_update, one rounding per op)
             const floatx4 xv = pre_s[k];
@@ -732,18 +680,10 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
                 if (a.eps_log) a.eps_log[lbase + r * hw] = o[r];
             }
             *reinterpret_cast<floatx4*>(a.xs + (size_t)ot.pix * COUT + ot.m) = xn;
-        } else if constexpr (ROLE == ROLE_PRODUCER) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o), yr,
-                                                   (ot.pix * COUT + ot.m) * 4, 0, 16);
         } else {
             *reinterpret_cast<floatx4*>(a.y + (size_t)ot.pix * COUT + ot.m) = o;
         }
     });
-    if constexpr (ROLE == ROLE_PRODUCER) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every sc1 store of this thread has landed
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.cnt + (bid_in & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     UCONV_STAMP(4);
 }
 
@@ -751,36 +691,8 @@ __device__ __forceinline__ void uconv_body(const UArgs& a, int bid_in, const Pai
 template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS = 1>
 __global__ __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu((WN * WK + 3) / 4, (WN * WK + 3) / 4)))
 void uconv_kernel(UArgs a) {
-    uconv_body<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS, ROLE_PLAIN>(a, blockIdx.x, PairSync{});
+    uconv_body<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS>(a, blockIdx.x);
 }
-
-// One instance's parameters as a type (for upair_kernel).
-template <int MODE, int CIN, int COUT, int TM, int TN, int WN, int WK, int NCH, int S, int EPI, int DT, int KS = 1>
-struct UBody {
-    static constexpr int kThreads = 64 * WN * WK;
-    static constexpr int kNph = MODE == 2 ? 4 : 1;
-    static constexpr size_t kLds = std::max<size_t>(WK > 1 ? (size_t)WK * WN * kNph * TM * TN * 64 * 16 : 0, KS > 1 ? 16 : 0);
-    template <int ROLE>
-    static __device__ __forceinline__ void run(const UArgs& a, int bid, const PairSync& ps) {
-        uconv_body<MODE, CIN, COUT, TM, TN, WN, WK, NCH, S, EPI, DT, KS, ROLE>(a, bid, ps);
-    }
-};
-
-#if LDM_STEP_DIAG
-// Two consecutive layers in one launch: blocks [0, nA) run layer A, blocks [nA, nA + nB) run layer B, which
-// waits in-launch for A's output (PairSync) after issuing its own weight stream.  Deadlock-free under in-order
-// workgroup dispatch (every producer block is dispatched before any consumer block) and bounded otherwise.
-// Two waves per SIMD: the two roles share a CU.
-template <class BA, class BB>
-__global__ __launch_bounds__(BA::kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void upair_kernel(UArgs a, UArgs b, PairSync ps) {
-    static_assert(BA::kThreads == BB::kThreads, "both roles use the same block shape");
-    if ((int)blockIdx.x < ps.nA)
-        BA::template run<ROLE_PRODUCER>(a, blockIdx.x, ps);
-    else
-        BB::template run<ROLE_CONSUMER>(b, (int)blockIdx.x - ps.nA, ps);
-}
-#endif  // LDM_STEP_DIAG
 
 // packed[c][m][16], c = cc*9 + t, element e = 4*lg + j  ->  input channel cc*16 + e, tap t = ky*3 + kx.
 // conv: w [COUT][CIN][3][3]; transposed conv: w [CIN][COUT][3][3] (torch layouts).  DT: element type of the
@@ -1035,18 +947,8 @@ int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     }
     const int64_t c = (mt + 63) / 64 * 64;
     if (cnt_floats) *cnt_floats = c;
-    return c + ms + 64;   // + the layer-pair counters (uc::PairSync, zero between launches)
+    return c + ms;
 }
-
-#if LDM_STEP_DIAG
-namespace uc {
-static int32_t* pair_counters(float* ws, int B, int H, int W) {
-    int64_t c = 0;
-    const int64_t total = step_ws_floats(B, H, W, &c);
-    return reinterpret_cast<int32_t*>(ws + total - 64);
-}
-}  // namespace uc
-#endif
 
 namespace uc {
 // The launch arguments of layer `layer` (ksv: the K-split form).
@@ -1215,61 +1117,6 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
             return launch<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM>(a, s.dtype, st);
     }
 }
-
-#if LDM_STEP_DIAG
-namespace uc {
-template <class BA, class BB>
-static int launch_pair(const UArgs& a, const UArgs& b, int ksA, int ksB, int32_t* cnt, hipStream_t st) {
-    PairSync ps{cnt, a.nMt * a.nNt, a.nMt * a.nNt * ksA, b.nMt * b.nNt * ksB};
-    const size_t lds = std::max(BA::kLds, BB::kLds);
-    hipLaunchKernelGGL((upair_kernel<BA, BB>), dim3((unsigned)(ps.nA + ps.nB)), dim3(BA::kThreads), lds, st, a, b, ps);
-    LDM_CHECK_LAUNCH("upair_kernel");
-    return 0;
-}
-// the instances of step_conv's table, as types
-template <int DT> using UEnc1 = UBody<0, 32, 64, 2, 1, 4, 1, 18, 18, EPI_RELU, DT>;
-template <int DT> using UEnc2 = UBody<1, 64, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_BCAST, DT>;
-template <int DT> using UDec3K = UBody<2, 256, 128, 2, 2, 1, 4, 9, 9, EPI_RELU | EPI_SKIP, DT, 4>;
-template <int DT> using UDec2 = UBody<2, 128, 64, 1, 2, 1, 4, 18, 18, EPI_RELU | EPI_SKIP, DT>;
-template <int DT> using UDec1 = UBody<0, 64, 32, 2, 2, 1, 4, 9, 9, EPI_DDIM, DT>;
-
-template <int DT>
-static int pair_dt(int la, const UArgs& a, const UArgs& b, int32_t* cnt, hipStream_t st) {
-    switch (la) {
-        case 0: return launch_pair<UEnc1<DT>, UEnc2<DT>>(a, b, 1, 1, cnt, st);
-        case 6: return launch_pair<UDec3K<DT>, UDec2<DT>>(a, b, 4, 1, cnt, st);
-        case 7: return launch_pair<UDec2<DT>, UDec1<DT>>(a, b, 1, 1, cnt, st);
-        default: return fail(2, "step pair: no pair starts at this layer");
-    }
-}
-}  // namespace uc
-
-// (dec1's pair instance is its 32-row form: not while dec1 runs on 16-row tiles)
-bool step_pair_supported(int la, int W) { return la == 0 || la == 6 || (la == 7 && !uc::dec1_thin(W)); }
-
-// Layers la and la + 1 in one launch (uc::upair_kernel): la's blocks hand their output to la + 1's blocks
-// inside the launch.  sa.ws: the step workspace (its tail holds the pair counters).  A dec3 producer runs its
-// K-split form (the single-block form needs more than the 256 registers a shared CU leaves it).
-int step_pair(int la, int B, int H, int W, const StepConv& sa, const StepConv& sb, hipStream_t st) {
-    using namespace uc;
-    LDM_REQUIRE(step_pair_supported(la, W) && sa.ws && sa.dtype == sb.dtype, "step pair: unsupported layer pair");
-    UArgs a, b;
-    UC_TRY(make_args(la, B, H, W, sa, la == 6 ? 1 : 0, a));
-    UC_TRY(make_args(la + 1, B, H, W, sb, 0, b));
-    int32_t* cnt = pair_counters(sa.ws, B, H, W);
-    switch (sa.dtype) {
-        case LDM_DT_F32: return pair_dt<0>(la, a, b, cnt, st);
-        case LDM_DT_F16: return pair_dt<1>(la, a, b, cnt, st);
-        case LDM_DT_BF16: return pair_dt<2>(la, a, b, cnt, st);
-        default: return fail(2, "step pair: unknown operand precision");
-    }
-}
-#else   // the shipped library: layer pairs (measured 10-21 us per iteration slower) are diagnostic only
-bool step_pair_supported(int, int) { return false; }
-int step_pair(int, int, int, int, const StepConv&, const StepConv&, hipStream_t) {
-    return fail(2, "step pair: in-launch layer pairs are in the diagnostic build only (make DIAG=1)");
-}
-#endif  // LDM_STEP_DIAG
 
 int step_layout(const float* x, float* y, int B, int C, int HW, bool to_nhwc, hipStream_t st) {
     const int64_t n = (int64_t)B * C * HW;

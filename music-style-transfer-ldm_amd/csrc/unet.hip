@@ -96,7 +96,6 @@ struct UNetWs {
     float *convws, *temb, *z1, *z2, *z3, *q2, *kv2, *a2, *c2, *z4, *q1, *kv1, *a1, *c1, *zb, *d4, *d3, *d2, *eps;
     float *kf2, *bf2, *kf1, *bf1;   // folded keys of both cross-attentions (reverse loop, use_fold)
     float* xs;                      // the sampler state in NHWC (reverse loop with the step kernels)
-    float* ustep;                   // split-K counters + slabs of the LDS-staged step kernels (zero-filled)
     float* uks;                     // split-K counters + slabs of the K-split step kernels (uconv.hip)
     float *ubn, *p1;                // the bottleneck's folded values U and CA1's probabilities (bfold.hip)
     int64_t total;
@@ -112,50 +111,6 @@ static int64_t conv_ws_floats(const ldm_unet_weights* w) {
         m = m > w->ca_plan_q[j].ws_floats ? m : w->ca_plan_q[j].ws_floats;
         m = m > w->ca_plan_kv[j].ws_floats ? m : w->ca_plan_kv[j].ws_floats;
         m = m > w->ca_plan_o[j].ws_floats ? m : w->ca_plan_o[j].ws_floats;
-    }
-    return m;
-}
-
-// The LDS-staged step kernels (ustep.hip) run when use_step == 2 at their canonical shape.
-static bool use_ustep(const ldm_unet_shape& s, const ldm_unet_weights* w) {
-    return w && w->use_fold && w->use_step == 2 && w->step_dtype == LDM_DT_F32 && s.C == 32 && s.nf == 64 &&
-           ustep_supported(s.B, s.H, s.W);
-}
-
-// Layers that run on ustep.hip under use_step 2, measured in the reverse loop at B = 8: round 2 chose enc1,
-// dec4 and dec2 (profiles/r02/README.md).  Round 3: the transposed layers of uconv.hip load each of their four
-// distinct activation offsets once instead of once per tap (dec4 and dec2 back on uconv.hip: loop 92.5 -> 88.9
-// us per iteration, profiles/r03/dedup), and the stride-1 / small-plane layers form their taps from an LDS
-// window (EPI_WINDOW / EPI_PLANE: 88.9 -> 85.1 with enc1 back on uconv.hip, profiles/r03/taps): none stays on
-// the LDS-DMA form by default.
-static int ustep_mask() {
-    static const int m = [] {
-        const char* e = std::getenv("LDM_USTEP_LAYERS");   // bit l: layer l on ustep.hip (A/B timing)
-        return e ? (int)std::strtol(e, nullptr, 0) : 0;
-    }();
-    return m;
-}
-static bool ustep_layer(int l) { return (ustep_mask() >> l) & 1; }
-
-// Layer pairs run as one launch (uconv.hip step_pair): bit l pairs layer l with l + 1 (ldm_step_set_pairs;
-// initial value LDM_UPAIR, else kPairDefault).
-constexpr int kPairDefault = 0;
-static int g_pairs = -1;
-static int step_pair_mask() {
-    if (g_pairs < 0) {
-        const char* e = std::getenv("LDM_UPAIR");
-        g_pairs = e ? (int)std::strtol(e, nullptr, 0) : kPairDefault;
-    }
-    return g_pairs;
-}
-
-static int64_t ustep_ws_floats(const ldm_unet_shape& s, const ldm_unet_weights* w) {
-    if (!use_ustep(s, w)) return 0;
-    int64_t m = 0;
-    for (int l = 0; l < 9; ++l) {
-        if (!ustep_layer(l)) continue;
-        const int64_t f = ustep_workspace_floats(l, s.B);
-        m = m > f ? m : f;
     }
     return m;
 }
@@ -203,7 +158,6 @@ static UNetWs carve(const ldm_unet_shape& s, const ldm_unet_weights* wts, float*
     w.kf1 = take(B * 4 * 512 * L1);
     w.bf1 = take(B * 4 * L1);
     w.xs = take(B * (int64_t)s.C * HW);
-    w.ustep = take(ustep_ws_floats(s, wts));
     w.uks = take(wts && wts->use_step ? step_ws_floats(s.B, s.H, s.W) : 0);
     const bool bfold = use_bneck_fold(s, wts);
     w.ubn = take(bfold ? B * 512 * 576 : 0);
@@ -329,7 +283,6 @@ static int unet_forward_folded(const ldm_unet_shape& s, const ldm_unet_weights& 
 static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w, const UNetWs& ws, hipStream_t st,
                              const float* temb, const DdimFuse& fuse) {
     const int HW = s.H * s.W;
-    const bool v3 = use_ustep(s, &w);
     const int L2 = HW / 16, L1 = HW / 64;
     // the nine convs' operands: enc1..enc3, enc4 (after CA2), bottleneck (after CA1), dec4..dec2, dec1 + DDIM
     const float* xin[9] = {ws.xs, ws.z1, ws.z2, ws.a2, ws.a1, ws.zb, ws.d4, ws.d3, ws.d2};
@@ -354,16 +307,8 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
     c[8].xs = ws.xs;
     c[8].x0_log = fuse.x0_log;
     c[8].eps_log = fuse.eps_log;
-    const int pairs = step_pair_mask();
-    auto run = [&](int l0, int l1) -> int {   // layers [l0, l1], pairs where enabled
-        for (int l = l0; l <= l1; ++l) {
-            if (l < l1 && ((pairs >> l) & 1) && step_pair_supported(l, s.W) && ws.uks) {
-                LDM_TRY(step_pair(l, s.B, s.H, s.W, c[l], c[l + 1], st));
-                ++l;
-                continue;
-            }
-            LDM_TRY(v3 && ustep_layer(l) ? ustep_conv(l, s.B, c[l], ws.ustep, st) : step_conv(l, s.B, s.H, s.W, c[l], st));
-        }
+    auto run = [&](int l0, int l1) -> int {   // layers [l0, l1]
+        for (int l = l0; l <= l1; ++l) LDM_TRY(step_conv(l, s.B, s.H, s.W, c[l], st));
         return 0;
     };
     LDM_TRY(run(0, 2));
@@ -384,19 +329,10 @@ static int unet_step_kernels(const ldm_unet_shape& s, const ldm_unet_weights& w,
 
 using namespace ldm;
 
-extern "C" int ldm_step_layer_forms(int32_t* ustep_layers, int32_t* ks_layers) {
-    LDM_REQUIRE(ustep_layers && ks_layers, "step_layer_forms: null argument");
-    *ustep_layers = ustep_mask();
+extern "C" int ldm_step_layer_forms(int32_t* ks_layers) {
+    LDM_REQUIRE(ks_layers, "step_layer_forms: null argument");
     *ks_layers = step_ks_mask();   // (their K-split geometry: LDM_UCONV_KS2, uconv.hip kKs2)
     return 0;
-}
-
-extern "C" int32_t ldm_step_diag_build(void) { return LDM_STEP_DIAG; }
-
-extern "C" int32_t ldm_step_set_pairs(int32_t mask) {
-    const int prev = step_pair_mask();
-    if (mask >= 0) g_pairs = mask;
-    return prev;
 }
 
 extern "C" int ldm_unet_layer_desc(const ldm_unet_shape* s, int32_t layer, ldm_conv_desc* d) {

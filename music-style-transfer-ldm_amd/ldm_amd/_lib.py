@@ -86,12 +86,9 @@ SIGNATURES = {
     "ldm_step_conv": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_step_conv_dt": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
                                    c_vp]),
-    "ldm_ustep_workspace_floats": (c_int64, [c_int32, c_int32]),
     "ldm_step_workspace_floats": (c_int64, [c_int32, c_int32, c_int32]),
-    "ldm_step_set_pairs": (c_int32, [c_int32]),
-    "ldm_step_diag_build": (c_int32, []),
     "ldm_step_workspace_counter_floats": (c_int64, [c_int32, c_int32, c_int32]),
-    "ldm_step_layer_forms": (c_int32, [c_vp, c_vp]),
+    "ldm_step_layer_forms": (c_int32, [c_vp]),
     "ldm_step_dec1_ddim": (c_int32, [c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_fp, c_fp, c_fp,
                                      c_int32, c_vp]),
     "ldm_step_conv_ws": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32,
@@ -99,7 +96,6 @@ SIGNATURES = {
     "ldm_mel_quantize": (c_int32, [c_fp, c_fp, c_int64, ctypes.c_float, c_vp]),
     "ldm_mel_dequantize": (c_int32, [c_fp, c_fp, c_int64, ctypes.c_float, c_vp]),
     "ldm_u8_to_unit": (c_int32, [c_fp, c_fp, c_int64, c_vp]),
-    "ldm_ustep_conv": (c_int32, [c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train": (c_int32, [c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float, c_float,
                                       c_int32, c_fp, c_fp, c_fp, c_vp]),
     "ldm_batchnorm_train_out": (c_int32, [c_fp, c_fp, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp, c_float,
@@ -236,7 +232,7 @@ def call(name, *args):
 
 
 def step_layer_forms():
-    """(ustep_layers, ks_layers) bit masks: which form each reverse-loop layer runs (ldm_step_layer_forms)."""
-    u, k = ctypes.c_int32(0), ctypes.c_int32(0)
-    call("ldm_step_layer_forms", ctypes.byref(u), ctypes.byref(k))
-    return int(u.value), int(k.value)
+    """Bit mask of the reverse-loop layers that run uconv.hip's K-split form (ldm_step_layer_forms)."""
+    k = ctypes.c_int32(0)
+    call("ldm_step_layer_forms", ctypes.byref(k))
+    return int(k.value)

@@ -30,8 +30,8 @@ class UNetEngine:
         # Re-associated cross-attentions in the reverse loop (ldm_capi.h use_fold); LDM_AMD_FOLD=0 turns
         # it off (A/B timing, parity of the literal form).
         self.fold = (os.environ.get("LDM_AMD_FOLD", "1") != "0") if fold is None else bool(fold)
-        # Step kernels for the folded reverse loop (ldm_capi.h use_step): 2 (default, or True) the LDS-staged
-        # kernels (ustep.hip) where they apply, else the register-direct ones (uconv.hip); 1 only the latter;
+        # Step kernels for the folded reverse loop (ldm_capi.h use_step): 1 or 2 (default, or True) the
+        # register-direct kernels (uconv.hip; 2 selected the LDS-staged kernels of rounds 2-5, removed in round 6);
         # 0 conv.hip's general kernel (LDM_AMD_STEP, A/B timing).  Built for the LDM's latent 32 / 64 filters.
         if step is None:
             step = int(os.environ.get("LDM_AMD_STEP", "2"))

@@ -10,7 +10,7 @@ pinned to the reference's own outputs by tests/test_oracle_golden.py) run on the
   * final x, the first pred_x0 log and the last noise_pred log within 1e-4 relative (north_star);
   * every step kernel the bench's loop launches (test_bench_config_step_kernels): each of the nine convs on
     the instance the loop picks for it (ldm_step_layer_forms: the K-split uconv.hip form for enc4, the bottleneck
-    and dec4, uconv.hip's single-block form for the others, ustep.hip for none by default; dec1 with its fused
+    and dec4, uconv.hip's single-block form for the others; dec1 with its fused
     DDIM update and both logs), with the
     engine's packed step weights, the folded out-projections and position biases, on NHWC operands at
     B = 8, 16 x 64, against float64 torch (1e-5 relative);
@@ -103,7 +103,6 @@ def test_bench_config_step_kernels(bench_objects, cuda):
     u = ldm.unet
     lib = L.load()
     st = torch.cuda.current_stream().cuda_stream
-    ustep_layers, _ = L.step_layer_forms()     # the layers the loop runs on ustep.hip
     LAYERS = [(32, 64, 0, 1), (64, 128, 1, 1), (128, 256, 1, 2), (256, 512, 1, 4), (512, 512, 0, 8),
               (512, 256, 2, 8), (256, 128, 2, 4), (128, 64, 2, 2)]
     convs = [u.enc1, u.enc2, u.enc3, u.enc4, u.bottleneck, u.dec4, u.dec3, u.dec2, u.dec1]
@@ -122,12 +121,7 @@ def test_bench_config_step_kernels(bench_objects, cuda):
         bias = w.step_pb[layer - 3] if layer in (3, 4) else w.conv_b[layer]
         args = (xd.data_ptr(), w.step_w[layer], bias, None if bcd is None else bcd.data_ptr(),
                 None if skd is None else skd.data_ptr(), y.data_ptr())
-        if (ustep_layers >> layer) & 1:
-            nws = int(lib.ldm_ustep_workspace_floats(layer, B))
-            uws = torch.zeros(max(1, nws), device=cuda)
-            L.call("ldm_ustep_conv", layer, B, *args, uws.data_ptr() if nws else None, st)
-        else:
-            L.call("ldm_step_conv_ws", layer, B, H, W, *args, 0, sws.data_ptr(), st)
+        L.call("ldm_step_conv_ws", layer, B, H, W, *args, 0, sws.data_ptr(), st)
         torch.cuda.synchronize()
         conv = convs[layer]
         x64 = x.double()

@@ -34,14 +34,12 @@ def _case(variant, layer, shape):
 
 @pytest.mark.parametrize("variant,layer,shape",
                          [_case("uconv", l, s) for l in range(8) for s in [(8, 16, 64), (2, 16, 16), (3, 8, 24)]] +
-                         [_case("ustep", l, s) for l in range(8) for s in [(8, 16, 64), (4, 16, 64), (12, 16, 64)]] +
                          [_case("ksplit", l, s) for l in (2, 3, 4, 5, 6) for s in [(8, 16, 64), (2, 16, 16), (3, 8, 24),
                                                                                   (5, 16, 64)]])
 def test_step_layer_vs_float64(cuda, variant, layer, shape):
     """uconv: ldm_step_conv (register-direct, any latent with H, W multiples of 8); ksplit: ldm_step_conv_ws
-    (the same kernel with 32x32 tiles and K split over blocks); ustep: ldm_ustep_conv (LDS-staged, latent
-    16 x 64, B a multiple of 4).  The split forms run twice on one workspace: bitwise-equal results (the
-    split-K sum is in slot order) and the counters left zero."""
+    (the same kernel with 32x32 tiles and K split over blocks).  The split form runs twice on one workspace:
+    bitwise-equal results (the split-K sum is in slot order) and the counters left zero."""
     from ldm_amd import _lib as L
     B, H, W = shape
     Cin, Cout, mode = LAYERS[layer]
@@ -81,24 +79,8 @@ def test_step_layer_vs_float64(cuda, variant, layer, shape):
         assert torch.equal(y, y2)
         ncnt = int(lib.ldm_step_workspace_counter_floats(B, H, W))
         assert 64 <= ncnt < nws
-        # every tile counter and the layer-pair counters at the end are back to zero
+        # every tile counter is back to zero
         assert int(ws[:ncnt].view(torch.int32).abs().sum()) == 0
-        assert int(ws[-64:].view(torch.int32).abs().sum()) == 0
-    else:
-        if not lib.ldm_step_diag_build():
-            pytest.skip("ustep.hip is in the diagnostic build only (make DIAG=1, LDM_AMD_LIB=lib/libldm_amd_diag.so)")
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B))
-        assert nws >= 0
-        ws = torch.zeros(max(nws, 1), device=cuda)
-        L.call("ldm_ustep_conv", layer, B, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp, y.data_ptr(),
-               ws.data_ptr() if nws else None, st)
-        y2 = torch.full_like(y, float("nan"))
-        L.call("ldm_ustep_conv", layer, B, xd.data_ptr(), packed.data_ptr(), bd.data_ptr(), bcp, skp, y2.data_ptr(),
-               ws.data_ptr() if nws else None, st)
-        torch.cuda.synchronize()
-        assert torch.equal(y, y2)
-        if nws:   # the tile counters lead the workspace (a second run with stale ones would lose tiles)
-            assert int(ws[:64].view(torch.int32).abs().sum()) == 0
     torch.cuda.synchronize()
     x64, w64 = x.double(), w.double()
     if mode == 2:
@@ -115,30 +97,11 @@ def test_step_layer_vs_float64(cuda, variant, layer, shape):
     assert rel_err(npy(got), ref.numpy()) < 1e-5
 
 
-def test_ustep_rejects_other_shapes(cuda):
-    from ldm_amd import _lib as L
-    lib = L.load()
-    if not lib.ldm_step_diag_build():   # the shipped build: present as stubs that report their absence
-        x = torch.zeros(8 * 16 * 64 * 32, device=cuda)
-        assert lib.ldm_ustep_workspace_floats(4, 8) == -1
-        assert lib.ldm_ustep_conv(0, 8, x.data_ptr(), x.data_ptr(), x.data_ptr(), None, None, x.data_ptr(), None,
-                                  torch.cuda.current_stream().cuda_stream) != 0
-        assert "diagnostic build" in lib.ldm_last_error().decode()
-        return
-    assert lib.ldm_ustep_workspace_floats(0, 6) == -1     # B not a multiple of 4
-    assert lib.ldm_ustep_workspace_floats(9, 8) == -1     # no such layer
-    assert lib.ldm_ustep_workspace_floats(0, 8) == 0      # enc1 does not split K
-    assert lib.ldm_ustep_workspace_floats(4, 8) > 0
-    x = torch.zeros(6 * 16 * 64 * 32, device=cuda)
-    assert lib.ldm_ustep_conv(0, 6, x.data_ptr(), x.data_ptr(), x.data_ptr(), None, None, x.data_ptr(), None,
-                              torch.cuda.current_stream().cuda_stream) != 0
-
-
 @pytest.mark.parametrize("shape,eta", [((8, 16, 64), 0.0), ((2, 16, 16), 1.0), ((3, 8, 24), 0.4), ((1, 16, 64), 0.0),
                                        ((4, 16, 64), 0.7)])
 def test_step_loop_equals_general_loop(M, cuda, shape, eta):
-    """The reverse loop on the step kernels (NHWC state, fused dec1 update; use_step 1 = uconv.hip,
-    2 = ustep.hip where it applies) == the same folded loop on conv.hip's general kernel, final x and
+    """The reverse loop on the step kernels (NHWC state, fused dec1 update; use_step 1 and 2 =
+    uconv.hip) == the same folded loop on conv.hip's general kernel, final x and
     both logs."""
     from ldm_amd.engine import UNetEngine
     B, H, W = shape

@@ -1,6 +1,6 @@
 #!/bin/bash
 # bfold A/B: the fold parity tests, the bench-object parity, then the loop time per iteration with the fold on and
-# off (tools/pair_times.py, twice around), and the headline bench line.   bash tools/gpu_r5_bfold.sh <tag>
+# off (tools/loop_times.py, twice around), and the headline bench line.   bash tools/gpu_r5_bfold.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-bfold}; mkdir -p $O
@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_bfold.py tests/test_gpu_ben
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "^FAILED|^E " $O/tests.log | head -20; exit $rc; }
 for r in 1 2; do
   for f in 1 0; do
-    LDM_BNECK_FOLD=$f timeout -k 10 120 python -u tools/pair_times.py 0 > $O/loop_${r}_$f.txt 2>&1 || { tail $O/loop_${r}_$f.txt; exit 1; }
+    LDM_BNECK_FOLD=$f timeout -k 10 120 python -u tools/loop_times.py > $O/loop_${r}_$f.txt 2>&1 || { tail $O/loop_${r}_$f.txt; exit 1; }
     echo "round $r fold=$f: $(grep pairs $O/loop_${r}_$f.txt)"
   done
 done

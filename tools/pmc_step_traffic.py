@@ -19,7 +19,7 @@ def per_dispatch(path, counter):
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if ("uconv_kernel" in k or "ustep_kernel" in k) and r["Counter_Name"] == counter:
+            if "uconv_kernel" in k and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return sorted(vals)[len(vals) // 2] if vals else None
 

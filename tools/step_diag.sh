@@ -1,6 +1,6 @@
 #!/bin/bash
 # Diagnostic variants of the step kernels -> lib/libldm_amd_<file><k>.so (never shipped; delete after use):
-#   tools/step_diag.sh uconv|ustep k...   with k: 1 no MFMAs, 2 no operand loads, 3 neither (fixed cost),
+#   tools/step_diag.sh uconv k...   with k: 1 no MFMAs, 2 no operand loads, 3 neither (fixed cost),
 #   4 per-block timestamps (tools/step_times.py --stamps)
 set -e
 cd "$(dirname "$0")/../music-style-transfer-ldm_amd/csrc"

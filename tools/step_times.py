@@ -44,10 +44,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="8x16x64")
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a USTEP_DIAG/UCONV_DIAG=4 build, tools/step_diag.sh)")
+    ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
-    ap.add_argument("--variant", default="hybrid", choices=["uconv", "ustep", "hybrid"],
-                    help="hybrid = what use_step 2 runs (ldm_step_layer_forms)")
     ap.add_argument("--layers", default=None, help="comma list of layer indices (default all)")
     ap.add_argument("--loop-only", default=None, help="comma list of use_step values: only time the loop")
     args = ap.parse_args()
@@ -60,7 +58,6 @@ def main():
     for layer, name in enumerate(NAMES if args.loop_only is None else []):
         if sel is not None and layer not in sel:
             continue
-        v3 = args.variant == "ustep" or (args.variant == "hybrid" and (L.step_layer_forms()[0] >> layer) & 1)
         Cin, Cout, mode = LAYERS[layer]
         Hin, Win = H // DIV[layer], W // DIV[layer]
         Hout, Wout = (Hin, Win) if mode == 0 else ((Hin // 2, Win // 2) if mode == 1 else (2 * Hin, 2 * Win))
@@ -74,44 +71,22 @@ def main():
         y = torch.empty(B, Hout, Wout, Cout, device=dev)
 
         # the split-K forms run with a workspace, as the loop runs them (ldm_step_layer_forms)
-        nws = int(lib.ldm_ustep_workspace_floats(layer, B)) if v3 else int(lib.ldm_step_workspace_floats(B, H, W))
+        nws = int(lib.ldm_step_workspace_floats(B, H, W))
         ws = torch.zeros(max(nws, 1), device=dev)
 
         def run():
             bcp = bc.data_ptr() if layer == 1 else None
             skp = sk.data_ptr() if mode == 2 else None
             stp = torch.cuda.current_stream().cuda_stream
-            if v3:
-                rc = lib.ldm_ustep_conv(layer, B, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
-                                        y.data_ptr(), ws.data_ptr() if nws else None, stp)
-            else:
-                rc = lib.ldm_step_conv_ws(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
-                                          y.data_ptr(), 0, ws.data_ptr(), stp)
+            rc = lib.ldm_step_conv_ws(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
+                                      y.data_ptr(), 0, ws.data_ptr(), stp)
             assert rc == 0
 
         us = graph_us(run, args.reps)
         fl = 2.0 * B * Cout * Hout * Wout * Cin * (9 if mode < 2 else 2.25)
         tot += us
         extra = ""
-        if args.stamps and v3:
-            import numpy as np
-            lib.ldm_debug_ustep_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-            graph_us(run, 10)          # stamps of the last launch of a 10-launch graph chain (warm)
-            torch.cuda.synchronize()
-            buf = np.zeros((4096, 8), dtype=np.uint64)
-            assert lib.ldm_debug_ustep_stamps(buf.ctypes.data, 4096) == 0
-            nb = int((buf[:, 0] > 0).sum())
-            b = buf[:nb].astype(np.float64)
-            clk = 2.4e3   # shader cycles per us (s_memtime), nominal
-            ph = [np.median((b[:, k + 1] - b[:, k]) / clk) for k in range(1, 6)]
-            blk = (b[:, 7] - b[:, 0]) * 0.01
-            span = (b[:, 7].max() - b[:, 0].min()) * 0.01
-            st0 = (b[:, 0] - b[:, 0].min()) * 0.01
-            pct = np.percentile(st0, [10, 50, 90])
-            extra = (f" | blocks {nb} span {span:5.2f} start p10/50/90 {pct[0]:4.2f}/{pct[1]:4.2f}/{pct[2]:4.2f} "
-                     f"blk {np.median(blk):5.2f} (max {blk.max():5.2f}) | setup {ph[0]:4.2f} issue0 {ph[1]:4.2f} "
-                     f"wait0 {ph[2]:4.2f} mma {ph[3]:4.2f} red {ph[4]:4.2f} us")
-        elif args.stamps:
+        if args.stamps:
             import numpy as np
             lib.ldm_debug_uconv_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
             graph_us(run, 10)          # stamps of the last launch of a 10-launch graph chain (warm)
