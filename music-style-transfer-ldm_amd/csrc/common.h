@@ -318,6 +318,53 @@ __device__ __forceinline__ void ld_st(const void* p, size_t o, bool h, float (&v
         }
     }
 }
+// The same load split in two, for loops that keep several pieces in flight: ld_raw issues the load(s) of W
+// consecutive values into raw registers (16-bit: W / 2 words; fp32: W words), cvt_raw converts them once the
+// values are used.  Same values as ld_st.
+template <int W>
+struct RawW {
+    float v[W];
+};
+template <int ST, int W>
+__device__ __forceinline__ void ld_raw(const void* p, size_t o, bool h, RawW<W>& r) {
+    if (ST != 0 && h) {
+        const unsigned short* q = reinterpret_cast<const unsigned short*>(p) + o;
+        if constexpr (W == 8) {
+            const uint4 t = *reinterpret_cast<const uint4*>(q);
+            r.v[0] = __builtin_bit_cast(float, t.x), r.v[1] = __builtin_bit_cast(float, t.y);
+            r.v[2] = __builtin_bit_cast(float, t.z), r.v[3] = __builtin_bit_cast(float, t.w);
+        } else if constexpr (W == 4) {
+            const uint2 t = *reinterpret_cast<const uint2*>(q);
+            r.v[0] = __builtin_bit_cast(float, t.x), r.v[1] = __builtin_bit_cast(float, t.y);
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) r.v[j] = __builtin_bit_cast(float, (unsigned)q[j]);
+        }
+    } else {
+        float t[W];
+        ld_st<0, W>(p, o, false, t);
+#pragma unroll
+        for (int j = 0; j < W; ++j) r.v[j] = t[j];
+    }
+}
+template <int ST, int W>
+__device__ __forceinline__ void cvt_raw(const RawW<W>& r, bool h, float (&v)[W]) {
+    if (ST != 0 && h) {
+        if constexpr (W == 8 || W == 4) {
+#pragma unroll
+            for (int j = 0; j < W / 2; ++j) {
+                const unsigned u = __builtin_bit_cast(unsigned, r.v[j]);
+                v[2 * j] = from16<ST>((unsigned short)(u & 0xffff)), v[2 * j + 1] = from16<ST>((unsigned short)(u >> 16));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) v[j] = from16<ST>((unsigned short)__builtin_bit_cast(unsigned, r.v[j]));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < W; ++j) v[j] = r.v[j];
+    }
+}
 template <int ST, int W>
 __device__ __forceinline__ void st_st(void* p, size_t o, bool h, const float (&v)[W]) {
     if (ST != 0 && h) {

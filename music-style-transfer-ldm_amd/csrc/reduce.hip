@@ -105,6 +105,45 @@ __device__ __forceinline__ void slice_for(int64_t e0, int64_t e1, int C, int c, 
     }
 }
 
+// slice_for with U pieces of a thread in flight at once: within a plane, the loads of U consecutive pieces
+// (ldf(offset, u)) are issued before the first is used (usef(offset, u), in offset order), so a wave keeps U
+// 16-byte loads outstanding instead of one (a sweep at one load per wave ran at 3.4-4.3 TB/s).  The pieces a
+// thread visits and the order it uses them in are slice_for's: every sum keeps its bits.
+template <int N, class F, int I = 0>
+__device__ __forceinline__ void unroll_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        unroll_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+template <int W, int U, class L, class F>
+__device__ __forceinline__ void slice_for_u(int64_t e0, int64_t e1, int C, int c, int HW, L&& ldf, F&& usef) {
+    if (e0 >= e1) return;
+    constexpr int STEP = kThreads * W;
+    int b = (int)(e0 / HW);
+    int p = (int)(e0 - (int64_t)b * HW);
+    int64_t e = e0;
+    while (e < e1) {
+        const int64_t left = e1 - e;
+        const int n = (int)((int64_t)(HW - p) < left ? (int64_t)(HW - p) : left);
+        const size_t base = ((size_t)b * C + c) * HW + p;
+        int i = threadIdx.x * W;
+        if constexpr (U > 1) {
+            for (; i + (U - 1) * STEP < n; i += U * STEP) {
+                unroll_for<U>([&](auto uc) { ldf(base + i + decltype(uc)::value * STEP, uc); });
+                unroll_for<U>([&](auto uc) { usef(base + i + decltype(uc)::value * STEP, uc); });
+            }
+        }
+        for (; i < n; i += STEP) {
+            ldf(base + i, std::integral_constant<int, 0>{});
+            usef(base + i, std::integral_constant<int, 0>{});
+        }
+        e += n;
+        ++b;
+        p = 0;
+    }
+}
+
 // the normalisation of the forward (and its re-evaluation for the ReLU mask in the backward): one
 // helper, so both sides compute the same bits
 __device__ __forceinline__ float bn_affine(float v, float alpha, float beta) { return v * alpha + beta; }
@@ -119,7 +158,7 @@ __device__ __forceinline__ float bn_act_grad(int act, float g, bool has_y, float
 }
 
 // ---- BatchNorm forward ---------------------------------------------------------------------------
-template <int W, int ST>
+template <int W, int ST, int U>
 __global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const void* __restrict__ x, int sf, int C, int HW,
                                                                     int64_t n, int64_t S,
                                                                     double* __restrict__ part) {
@@ -128,15 +167,18 @@ __global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const void* 
     const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     double s = 0.0, q = 0.0;
-    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float v[W];
-        ld_st<ST, W>(x, o, xh, v);
+    RawW<W> rv[U];
+    slice_for_u<W, U>(
+        e0, e1, C, c, HW, [&](size_t o, auto u) { ld_raw<ST, W>(x, o, xh, rv[decltype(u)::value]); },
+        [&](size_t, auto u) {
+            float v[W];
+            cvt_raw<ST, W>(rv[decltype(u)::value], xh, v);
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            s += (double)v[j];
-            q += (double)v[j] * (double)v[j];
-        }
-    });
+            for (int j = 0; j < W; ++j) {
+                s += (double)v[j];
+                q += (double)v[j] * (double)v[j];
+            }
+        });
     s = block_sum(s, red);
     q = block_sum(q, red);
     if (threadIdx.x == 0) {
@@ -166,7 +208,7 @@ __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double*
     if (out1) out1[c] = (float)b;
 }
 
-template <int W, int ST>
+template <int W, int ST, int U>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, void* x, int sf, int C,
                                                             int HW, int64_t n, int64_t S,
                                                             const double* __restrict__ stats, double count_arg,
@@ -200,13 +242,16 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, voi
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     const int ro = (act >> 8) & 0xff, ac = act & 0xff;   // LDM_ACT_ROUND_*: the output of a 16-bit input's BN (autocast)
     const bool xh = sf & LDM_ST_X16, yh = sf & LDM_ST_Y16;
-    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float v[W];
-        ld_st<ST, W>(src, o, xh, v);
+    RawW<W> rv[U];
+    slice_for_u<W, U>(
+        e0, e1, C, c, HW, [&](size_t o, auto u) { ld_raw<ST, W>(src, o, xh, rv[decltype(u)::value]); },
+        [&](size_t o, auto u) {
+            float v[W];
+            cvt_raw<ST, W>(rv[decltype(u)::value], xh, v);
 #pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = apply_act(round16(bn_affine(v[j], alpha, beta), ro), ac);
-        st_st<ST, W>(x, o, yh, v);
-    });
+            for (int j = 0; j < W; ++j) v[j] = apply_act(round16(bn_affine(v[j], alpha, beta), ro), ac);
+            st_st<ST, W>(x, o, yh, v);
+        });
     if (k == 0 && threadIdx.x == 0) {
         if (rmean) rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
         if (rvar) {
@@ -219,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, voi
 }
 
 // ---- BatchNorm backward: g = dy*act'(y); sums (sum g, sum g*xhat); dx = w*invstd*(g - sg/N - xhat*sgx/N)
-template <int W, int ST>
+template <int W, int ST, int U>
 __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __restrict__ dy,
                                                                   const void* __restrict__ y,
                                                                   const void* __restrict__ x, int sf,
@@ -237,18 +282,28 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     float sg = 0.f, sgx = 0.f;
     const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16;
-    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float g[W], yv[W] = {}, xv[W];
-        ld_st<ST, W>(dy, o, dyh, g);
-        if (y) ld_st<ST, W>(y, o, yh, yv);
-        ld_st<ST, W>(x, o, xh, xv);
+    RawW<W> rg[U], ry[U] = {}, rx[U];
+    slice_for_u<W, U>(
+        e0, e1, C, c, HW,
+        [&](size_t o, auto u) {
+            constexpr int q = decltype(u)::value;
+            ld_raw<ST, W>(dy, o, dyh, rg[q]);
+            if (y) ld_raw<ST, W>(y, o, yh, ry[q]);
+            ld_raw<ST, W>(x, o, xh, rx[q]);
+        },
+        [&](size_t, auto u) {
+            constexpr int q = decltype(u)::value;
+            float g[W], yv[W] = {}, xv[W];
+            cvt_raw<ST, W>(rg[q], dyh, g);
+            if (y) cvt_raw<ST, W>(ry[q], yh, yv);
+            cvt_raw<ST, W>(rx[q], xh, xv);
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
-            sg += gj;
-            sgx += gj * ((xv[j] - mu) * is);
-        }
-    });
+            for (int j = 0; j < W; ++j) {
+                const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
+                sg += gj;
+                sgx += gj * ((xv[j] - mu) * is);
+            }
+        });
     const double a = block_sum((double)sg, red);
     const double b = block_sum((double)sgx, red);
     if (threadIdx.x == 0) {
@@ -257,7 +312,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __
     }
 }
 
-template <int W, int ST>
+template <int W, int ST, int U>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __restrict__ dy,
                                                                 const void* __restrict__ y,
                                                                 const void* __restrict__ x, int sf,
@@ -296,22 +351,32 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16, dxh = sf & LDM_ST_DX16;
     float sdx = 0.f;
-    slice_for<W>(e0, e1, C, c, HW, [&](size_t o) {
-        float g[W], yv[W] = {}, xv[W], d[W];
-        ld_st<ST, W>(dy, o, dyh, g);
-        if (y) ld_st<ST, W>(y, o, yh, yv);
-        ld_st<ST, W>(x, o, xh, xv);
+    RawW<W> rg[U], ry[U] = {}, rx[U];
+    slice_for_u<W, U>(
+        e0, e1, C, c, HW,
+        [&](size_t o, auto u) {
+            constexpr int q = decltype(u)::value;
+            ld_raw<ST, W>(dy, o, dyh, rg[q]);
+            if (y) ld_raw<ST, W>(y, o, yh, ry[q]);
+            ld_raw<ST, W>(x, o, xh, rx[q]);
+        },
+        [&](size_t o, auto u) {
+            constexpr int q = decltype(u)::value;
+            float g[W], yv[W] = {}, xv[W], d[W];
+            cvt_raw<ST, W>(rg[q], dyh, g);
+            if (y) cvt_raw<ST, W>(ry[q], yh, yv);
+            cvt_raw<ST, W>(rx[q], xh, xv);
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
-            d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
-        }
-        st_st<ST, W>(dx, o, dxh, d);
-        if (dxs_part) {   // the sum of dx as stored (a 16-bit dx: its rounded values)
+            for (int j = 0; j < W; ++j) {
+                const float gj = bn_act_grad(act, g[j], y != nullptr, yv[j], xv[j], alpha, beta);
+                d[j] = kk * ((gj - sgN) - ((xv[j] - mu) * is) * sgxN);
+            }
+            st_st<ST, W>(dx, o, dxh, d);
+            if (dxs_part) {   // the sum of dx as stored (a 16-bit dx: its rounded values)
 #pragma unroll
-            for (int j = 0; j < W; ++j) sdx += dxh ? round16(d[j], ST) : d[j];
-        }
-    });
+                for (int j = 0; j < W; ++j) sdx += dxh ? round16(d[j], ST) : d[j];
+            }
+        });
     // dxs_part: this slice's sum of dx (fixed order: thread stride, wave tree, waves in order), for the bias
     // gradient of the conv that produced x (chan_sum_finalize_kernel sums the slices in order)
     if (dxs_part) {
@@ -561,6 +626,23 @@ void w_dispatch(int w, F&& f) {
     else f(std::integral_constant<int, 1>{});
 }
 
+// pieces of a thread in flight in the BatchNorm sweeps (slice_for_u): LDM_BN_UNROLL = 1, 2 or 4 (default 2)
+inline int bn_unroll() {
+    static const int v = [] {
+        const char* e = getenv("LDM_BN_UNROLL");
+        const int x = e ? atoi(e) : 2;
+        return x == 1 || x == 4 ? x : 2;
+    }();
+    return v;
+}
+template <class F>
+void u_dispatch(F&& f) {
+    const int u = bn_unroll();
+    if (u == 4) f(std::integral_constant<int, 4>{});
+    else if (u == 1) f(std::integral_constant<int, 1>{});
+    else f(std::integral_constant<int, 2>{});
+}
+
 // the storage fields of an act code (ldm_capi.h LDM_ST_*): 16-bit type, per-tensor flags, and the act + round
 // bits the kernels read
 struct StCode {
@@ -602,10 +684,10 @@ static int bn_stats_launch(const void* x, const StCode& sc, int32_t B, int32_t C
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) {
-            hipLaunchKernelGGL((bn_stats_partial_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads),
+        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
+            hipLaunchKernelGGL((bn_stats_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads),
                                0, (hipStream_t)stream, x, sc.sf, C, HW, n, S, part);
-        });
+        }); });
     });
     LDM_CHECK_LAUNCH("bn_stats_partial_kernel");
     return 0;
@@ -644,11 +726,11 @@ static int bn_apply_launch(const float* x, float* y, int32_t B, int32_t C, int32
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) {
-            hipLaunchKernelGGL((bn_apply_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0,
+        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
+            hipLaunchKernelGGL((bn_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads), 0,
                                (hipStream_t)stream, x, y, sc.sf, C, HW, n, S, stats, count, weight, bias, running_mean,
                                running_var, momentum, eps, sc.act, save_mean, save_invstd, part, part ? P : 0);
-        });
+        }); });
     });
     LDM_CHECK_LAUNCH("bn_apply_kernel");
     return 0;
@@ -710,11 +792,11 @@ static int bn_bwd_partial_launch(const void* dy, const void* y, const void* x, c
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) {
-            hipLaunchKernelGGL((bn_bwd_partial_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads),
+        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
+            hipLaunchKernelGGL((bn_bwd_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads),
                                0, (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW,
                                n, S, part);
-        });
+        }); });
     });
     LDM_CHECK_LAUNCH("bn_bwd_partial_kernel");
     return 0;
@@ -754,11 +836,11 @@ static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, con
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) {
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value>), grid, dim3(kThreads), 0,
+        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads), 0,
                                (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n,
                                S, sums, count, dx, part, part ? P : 0, dweight, dbias, dxs_part);
-        });
+        }); });
     });
     LDM_CHECK_LAUNCH("bn_bwd_apply_kernel");
     return 0;

@@ -237,7 +237,7 @@ class _PackRecord:
 
     def add(self, owner, tail, w, desc, plan, buf):
         # only a pack that reads the owner's own storage can be refreshed from it later (not a cast copy)
-        if plan.kind not in (1, 2, 3) or w.dtype != torch.float32 or not w.is_contiguous() or \
+        if plan.kind not in (1, 2, 3, 4) or w.dtype != torch.float32 or not w.is_contiguous() or \
                 w.untyped_storage().data_ptr() != owner.untyped_storage().data_ptr():
             return
         # no reference to w itself: a slice of a parameter (in_proj rows) keeps its autograd node alive, and

@@ -46,7 +46,8 @@ def _ref_attn(q, kv, heads):
 
 
 CASES = {"ca2_w128": (2, 256, 128, 128), "ca1_ragged": (2, 512, 40, 200), "ca2_ragged": (1, 256, 100, 77),
-         "ca2_long": (1, 256, 1024, 1024), "ca1_256": (1, 512, 256, 256), "s_gt_64_l_small": (3, 256, 16, 130)}
+         "ca2_long": (1, 256, 1024, 1024), "ca1_256": (1, 512, 256, 256), "s_gt_64_l_small": (3, 256, 16, 130),
+         "one_key_tile": (2, 256, 70, 40)}   # S <= 64: the double-buffered K/V loop's single-tile path
 
 
 @pytest.mark.parametrize("case", sorted(CASES))

@@ -89,12 +89,18 @@ def test_tiled_conv(cuda, case, epi, dt):
         assert torch.equal(aout, y)
 
 
-def test_tiled_plan_classes(cuda):
-    """Which layers take the kind-3 path: 16-bit operands only, Cin % 32 == 0, >= 4096 positions."""
+def test_tiled_plan_classes(cuda, monkeypatch):
+    """Which layers take the LDS-staged paths: 16-bit operands only, Cin % 32 == 0; kind 3 (tconv.hip) from 4096
+    positions, kind 4 (sconv.hip, round 6) for the small planes under bf16 (fp16: the general kernel unless
+    LDM_AMD_SCONV_F16=1)."""
     from ldm_amd import ops
+    monkeypatch.delenv("LDM_AMD_SCONV_F16", raising=False)
     big = ops.make_desc(32, 128, 32, 128, 64, 4, 4, 2, 1, 0, True)        # decoder.3 at B = 32
     assert ops.tiled_plan(big, 2) is not None and ops.tiled_plan(big, 0) is None
-    assert ops.tiled_plan(ops.make_desc(8, 256, 4, 16, 512, 3, 3, 2, 1), 2) is None        # UNet-sized: general
+    assert int(ops.tiled_plan(big, 2).kind) == 3
+    unet = ops.make_desc(8, 256, 4, 16, 512, 3, 3, 2, 1)                   # UNet-sized
+    assert int(ops.tiled_plan(unet, 2).kind) == 4                            # bf16: sconv.hip
+    assert ops.tiled_plan(unet, 1) is None                                   # fp16: general
     assert ops.tiled_plan(ops.make_desc(32, 1, 128, 512, 64, 3, 3, 2, 1), 2) is None      # Cin = 1: x4 kernel
     assert ops.tiled_plan(ops.make_desc(32, 48, 64, 64, 64, 3, 3, 1, 1), 2) is None       # Cin % 32 != 0
 
