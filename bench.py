@@ -61,8 +61,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-legs", action="store_true", help="skip the config-1 / config-3 CPU legs")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "pmc_traffic_step.json"),
-                    help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "pmc_traffic_step.json"),
+                    help="per-kernel HBM traffic summary produced from a rocprofv3 --pmc pass (fp32 step kernels)")
+    ap.add_argument("--pmc-lowp", default=os.path.join(ROOT, "profiles", "r06", "pmc_traffic_step_fp16.json"),
+                    help="the same for the fp16 step kernels (config 5, DTYPE=fp16 tools/pmc_step_traffic.sh)")
     a = ap.parse_args()
     if a.batch is None:
         a.batch = {"train": 32, "stress": 1}.get(a.workload, 8)
@@ -403,7 +405,7 @@ def run_train(args, world, rank, dev, M):
     # WRITE_SIZE summed over the step's dispatches), bf16 only (the passes profile the default line)
     traffic = None
     if args.dtype == "bf16" and world == 1:
-        for rnd in ("r05", "r04", "r03"):
+        for rnd in ("r06", "r05", "r04", "r03"):
             pth = os.path.join(ROOT, "profiles", rnd, "train_pmc.json")
             if os.path.exists(pth):
                 try:
@@ -756,16 +758,15 @@ def main():
         dom = max(kt, key=lambda k: kt[k]["us"])      # the longest launch of the step
         dk = kt[dom]
         traffic = None
-        if os.path.exists(args.pmc):
+        pmc_file = args.pmc if args.dtype == "fp32" else (args.pmc_lowp if args.dtype == "fp16" else None)
+        if pmc_file and os.path.exists(pmc_file):   # (bf16 step kernels: no PMC pass recorded)
             try:
-                with open(args.pmc) as f:
+                with open(pmc_file) as f:
                     pmc = json.load(f)
                 traffic = pmc.get("per_launch_bytes", {}).get(dom)
             except (OSError, ValueError):
                 traffic = None
         peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else LOWP_PEAK_TFLOPS
-        if args.dtype != "fp32":
-            traffic = None     # profiles/r05/pmc_traffic_step.json holds the fp32 kernels' counters
         if dk.get("bound") == "hbm":   # a byte-bound launch (the folded-value bottleneck, the attentions)
             result["roofline"] = {"kernel": f"{dk['kernel']} ({dom})", "bound": "hbm",
                                   "achieved": dk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",

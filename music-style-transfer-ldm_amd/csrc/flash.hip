@@ -37,22 +37,31 @@ __device__ __forceinline__ floatx4 mma(float a, float b, floatx4 c) {
 // the next tile's loads before it computes on the current one.
 template <int D>
 constexpr int cs_pieces() { return D * (kTok / 4) / 256; }
-template <int D>
+// Branch-free: a piece past n is loaded from a valid address (the slab's first element) and replaced by zero
+// after the load, so no load sits inside a branch (a load under a branch whose register the other arm writes makes
+// the compiler wait for it at the join, which drains the look-ahead).  VEC: n % 4 == 0, so a float4 of a row is
+// wholly inside or wholly past it.
+template <int D, bool VEC>
 __device__ __forceinline__ void load_cs(const float* __restrict__ src, int n, int t0, float4 (&v)[cs_pieces<D>()]) {
     constexpr int NIT = cs_pieces<D>();
-    const bool vec = (n & 3) == 0 && t0 + kTok <= n;
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
         const int e = u * 256 + (int)threadIdx.x;
         const int c = e / (kTok / 4), t = t0 + 4 * (e % (kTok / 4));
         const float* p = src + (size_t)c * n + t;
-        if (vec) {
-            v[u] = *reinterpret_cast<const float4*>(p);
+        if constexpr (VEC) {
+            const bool in = t < n;
+            const float4 x = *reinterpret_cast<const float4*>(in ? p : src);
+            v[u] = in ? x : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-            v[u].x = t + 0 < n ? p[0] : 0.f;
-            v[u].y = t + 1 < n ? p[1] : 0.f;
-            v[u].z = t + 2 < n ? p[2] : 0.f;
-            v[u].w = t + 3 < n ? p[3] : 0.f;
+            float x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool in = t + k < n;
+                const float y = *(in ? p + k : src);
+                x[k] = in ? y : 0.f;
+            }
+            v[u] = make_float4(x[0], x[1], x[2], x[3]);
         }
     }
 }
@@ -120,7 +129,7 @@ __device__ __forceinline__ void load_qfrag(const float* __restrict__ base, int E
 }
 
 // ---- forward ---------------------------------------------------------------------------------------
-template <int D, bool TOK, bool LSE>
+template <int D, bool TOK, bool LSE, bool VEC>
 __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                         float* __restrict__ out, float* __restrict__ lse, int E,
                                                         int heads, int L, int S, float scale) {
@@ -152,13 +161,13 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
     // a load round trip per 64-key tile, 364 us per launch at L = S = 4096.)
     const int nt = (S + kTok - 1) / kTok;
     float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
-    load_cs<D>(kb, S, 0, rk);
-    load_cs<D>(vb, S, 0, rv);
+    load_cs<D, VEC>(kb, S, 0, rk);
+    load_cs<D, VEC>(vb, S, 0, rv);
     store_cs<D>(rk, sm);
     store_cs<D>(rv, sm + D * kKP);
     if (nt > 1) {
-        load_cs<D>(kb, S, kTok, rk);
-        load_cs<D>(vb, S, kTok, rv);
+        load_cs<D, VEC>(kb, S, kTok, rk);
+        load_cs<D, VEC>(vb, S, kTok, rv);
     }
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
@@ -170,12 +179,26 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
         floatx4 sc[4];
 #pragma unroll
         for (int st = 0; st < 4; ++st) sc[st] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj)
+        // the K fragments of channel group jj + 1 are read while group jj's 16 MFMAs run (one LDS round trip per
+        // group instead of one per MFMA pair)
+        float ka[2][4][4];
+        auto read_k = [&](int jj, float (&f)[4][4]) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int st = 0; st < 4; ++st) sc[st] = mma(Ks[(16 * jj + 4 * lg + i) * kKP + 16 * st + col], qf[jj][i], sc[st]);
+                for (int st = 0; st < 4; ++st) f[i][st] = Ks[(16 * jj + 4 * lg + i) * kKP + 16 * st + col];
+        };
+        read_k(0, ka[0]);
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+            if (jj + 1 < NJ) read_k(jj + 1, ka[(jj + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);   // (the scheduler would sink the reads back next to their MFMAs)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int st = 0; st < 4; ++st) sc[st] = mma(ka[jj & 1][i][st], qf[jj][i], sc[st]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // online softmax over s (the 4 lanes of query col share its statistics)
         float tmax = -INFINITY;
 #pragma unroll
@@ -221,8 +244,8 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
             store_cs<D>(rk, nb);
             store_cs<D>(rv, nb + D * kKP);
             if (t + 2 < nt) {
-                load_cs<D>(kb, S, (t + 2) * kTok, rk);
-                load_cs<D>(vb, S, (t + 2) * kTok, rv);
+                load_cs<D, VEC>(kb, S, (t + 2) * kTok, rk);
+                load_cs<D, VEC>(vb, S, (t + 2) * kTok, rv);
             }
         }
         __syncthreads();
@@ -361,7 +384,7 @@ __global__ __launch_bounds__(256) void flash_bwd_dkv_kernel(const float* __restr
 
 // dQ for 64 queries per block (wave: 16 queries, the N side), streaming K and V through LDS:
 //   S^T = K qs^T, dP^T = V dO^T, dS = P (dP - delta);  dQ^T += K dS^T, times scale
-template <int D>
+template <int D, bool VEC>
 __global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                            const float* __restrict__ dout, const float* __restrict__ lse,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
@@ -390,13 +413,13 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restri
     // K / V tiles double-buffered as in flash_fwd_kernel
     const int nt = (S + kTok - 1) / kTok;
     float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
-    load_cs<D>(kb, S, 0, rk);
-    load_cs<D>(vb, S, 0, rv);
+    load_cs<D, VEC>(kb, S, 0, rk);
+    load_cs<D, VEC>(vb, S, 0, rv);
     store_cs<D>(rk, sm);
     store_cs<D>(rv, sm + D * kKP);
     if (nt > 1) {
-        load_cs<D>(kb, S, kTok, rk);
-        load_cs<D>(vb, S, kTok, rv);
+        load_cs<D, VEC>(kb, S, kTok, rk);
+        load_cs<D, VEC>(vb, S, kTok, rv);
     }
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
@@ -444,8 +467,8 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_kernel(const float* __restri
             store_cs<D>(rk, nb);
             store_cs<D>(rv, nb + D * kKP);
             if (t + 2 < nt) {
-                load_cs<D>(kb, S, (t + 2) * kTok, rk);
-                load_cs<D>(vb, S, (t + 2) * kTok, rv);
+                load_cs<D, VEC>(kb, S, (t + 2) * kTok, rk);
+                load_cs<D, VEC>(vb, S, (t + 2) * kTok, rv);
             }
         }
         __syncthreads();
@@ -469,11 +492,15 @@ template <int D, bool TOK, bool LSE>
 static int fwd_launch(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
                       float scale, hipStream_t st) {
     const size_t lds = 4 * (size_t)D * kKP * sizeof(float);   // K and V, two buffers each
-    static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE>, lds);
+    static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE, true>, lds) | opt_in_lds(flash_fwd_kernel<D, TOK, LSE, false>, lds);
     if (opted) return opted;
     const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
-    hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E, heads, L, S,
-                       scale);
+    if (S % 4 == 0)
+        hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, true>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E, heads,
+                           L, S, scale);
+    else
+        hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, false>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E,
+                           heads, L, S, scale);
     LDM_CHECK_LAUNCH("flash_fwd_kernel");
     return 0;
 }
@@ -492,10 +519,14 @@ static int bwd_launch(const float* q, const float* kv, const float* out, const f
                        st, q, kv, dout, lse, delta, dkv, E, heads, L, S, scale);
     LDM_CHECK_LAUNCH("flash_bwd_dkv_kernel");
     const size_t lds_q = 4 * (size_t)D * kKP * sizeof(float);   // K and V, two buffers each
-    static int o2 = opt_in_lds(flash_bwd_dq_kernel<D>, lds_q);
+    static int o2 = opt_in_lds(flash_bwd_dq_kernel<D, true>, lds_q) | opt_in_lds(flash_bwd_dq_kernel<D, false>, lds_q);
     if (o2) return o2;
-    hipLaunchKernelGGL(flash_bwd_dq_kernel<D>, dim3((unsigned)B * heads * ((L + kTok - 1) / kTok)), dim3(256), lds_q, st,
-                       q, kv, dout, lse, delta, dq, E, heads, L, S, scale);
+    if (S % 4 == 0)
+        hipLaunchKernelGGL((flash_bwd_dq_kernel<D, true>), dim3((unsigned)B * heads * ((L + kTok - 1) / kTok)), dim3(256),
+                           lds_q, st, q, kv, dout, lse, delta, dq, E, heads, L, S, scale);
+    else
+        hipLaunchKernelGGL((flash_bwd_dq_kernel<D, false>), dim3((unsigned)B * heads * ((L + kTok - 1) / kTok)), dim3(256),
+                           lds_q, st, q, kv, dout, lse, delta, dq, E, heads, L, S, scale);
     LDM_CHECK_LAUNCH("flash_bwd_dq_kernel");
     return 0;
 }

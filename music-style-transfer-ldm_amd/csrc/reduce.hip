@@ -105,6 +105,16 @@ __device__ __forceinline__ void slice_for(int64_t e0, int64_t e1, int C, int c, 
     }
 }
 
+// HM: how a BatchNorm kernel instance reads its tensors' storage flags.  0: at run time, per tensor (a mixed call);
+// 1: every tensor of the call 16-bit; 2: every tensor fp32.  With 1 / 2 the flag is a constant, so the load / store
+// paths carry no branch: a branch around a load makes the compiler drain vmcnt at the join, which serialises the
+// pieces slice_for_u keeps in flight (measured: 2-3.5x slower sweeps with run-time flags and U = 2).
+template <int HM>
+__device__ __forceinline__ bool st_flag(int sf, int bit) {
+    if constexpr (HM == 0) return (sf & bit) != 0;
+    else return HM == 1;
+}
+
 // slice_for with U pieces of a thread in flight at once: within a plane, the loads of U consecutive pieces
 // (ldf(offset, u)) are issued before the first is used (usef(offset, u), in offset order), so a wave keeps U
 // 16-byte loads outstanding instead of one (a sweep at one load per wave ran at 3.4-4.3 TB/s).  The pieces a
@@ -158,11 +168,11 @@ __device__ __forceinline__ float bn_act_grad(int act, float g, bool has_y, float
 }
 
 // ---- BatchNorm forward ---------------------------------------------------------------------------
-template <int W, int ST, int U>
+template <int W, int ST, int U, int HM>
 __global__ __launch_bounds__(kThreads) void bn_stats_partial_kernel(const void* __restrict__ x, int sf, int C, int HW,
                                                                     int64_t n, int64_t S,
                                                                     double* __restrict__ part) {
-    const bool xh = sf & LDM_ST_X16;
+    const bool xh = st_flag<HM>(sf, LDM_ST_X16);
     __shared__ double red[kThreads / 64];
     const int k = blockIdx.x, c = blockIdx.y, P = gridDim.x;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
@@ -208,7 +218,7 @@ __global__ __launch_bounds__(kThreads) void slices_finalize_kernel(const double*
     if (out1) out1[c] = (float)b;
 }
 
-template <int W, int ST, int U>
+template <int W, int ST, int U, int HM>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, void* x, int sf, int C,
                                                             int HW, int64_t n, int64_t S,
                                                             const double* __restrict__ stats, double count_arg,
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, voi
     const float beta = (bias ? bias[c] : 0.0f) - mean_f * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     const int ro = (act >> 8) & 0xff, ac = act & 0xff;   // LDM_ACT_ROUND_*: the output of a 16-bit input's BN (autocast)
-    const bool xh = sf & LDM_ST_X16, yh = sf & LDM_ST_Y16;
+    const bool xh = st_flag<HM>(sf, LDM_ST_X16), yh = st_flag<HM>(sf, LDM_ST_Y16);
     RawW<W> rv[U];
     slice_for_u<W, U>(
         e0, e1, C, c, HW, [&](size_t o, auto u) { ld_raw<ST, W>(src, o, xh, rv[decltype(u)::value]); },
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const void* src, voi
 }
 
 // ---- BatchNorm backward: g = dy*act'(y); sums (sum g, sum g*xhat); dx = w*invstd*(g - sg/N - xhat*sgx/N)
-template <int W, int ST, int U>
+template <int W, int ST, int U, int HM>
 __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __restrict__ dy,
                                                                   const void* __restrict__ y,
                                                                   const void* __restrict__ x, int sf,
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
     float sg = 0.f, sgx = 0.f;
-    const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16;
+    const bool dyh = st_flag<HM>(sf, LDM_ST_DY16), yh = st_flag<HM>(sf, LDM_ST_Y16), xh = st_flag<HM>(sf, LDM_ST_X16);
     RawW<W> rg[U], ry[U] = {}, rx[U];
     slice_for_u<W, U>(
         e0, e1, C, c, HW,
@@ -312,7 +322,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_partial_kernel(const void* __
     }
 }
 
-template <int W, int ST, int U>
+template <int W, int ST, int U, int HM>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __restrict__ dy,
                                                                 const void* __restrict__ y,
                                                                 const void* __restrict__ x, int sf,
@@ -349,7 +359,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const void* __re
     const float alpha = is * (w ? w[c] : 1.0f);
     const float beta = (bias ? bias[c] : 0.0f) - mu * alpha;
     const int64_t e0 = (int64_t)k * S, e1 = e0 + S < n ? e0 + S : n;
-    const bool dyh = sf & LDM_ST_DY16, yh = sf & LDM_ST_Y16, xh = sf & LDM_ST_X16, dxh = sf & LDM_ST_DX16;
+    const bool dyh = st_flag<HM>(sf, LDM_ST_DY16), yh = st_flag<HM>(sf, LDM_ST_Y16), xh = st_flag<HM>(sf, LDM_ST_X16),
+               dxh = st_flag<HM>(sf, LDM_ST_DX16);
     float sdx = 0.f;
     RawW<W> rg[U], ry[U] = {}, rx[U];
     slice_for_u<W, U>(
@@ -635,14 +646,23 @@ inline int bn_unroll() {
     }();
     return v;
 }
+// (U, HM) instances: HM 0 (run-time flags) only with U = 1; HM 1 / 2 with U = bn_unroll()
 template <class F>
-void u_dispatch(F&& f) {
+void uh_dispatch(int hm, F&& f) {
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    using H0 = std::integral_constant<int, 0>;
+    if (hm == 0) return f(I1{}, H0{});
     const int u = bn_unroll();
-    if (u == 4) f(std::integral_constant<int, 4>{});
-    else if (u == 1) f(std::integral_constant<int, 1>{});
-    else f(std::integral_constant<int, 2>{});
+    auto go = [&](auto hc) {
+        if (u == 4) f(I4{}, hc);
+        else if (u == 1) f(I1{}, hc);
+        else f(I2{}, hc);
+    };
+    if (hm == 1) go(std::integral_constant<int, 1>{});
+    else go(std::integral_constant<int, 2>{});
 }
-
 // the storage fields of an act code (ldm_capi.h LDM_ST_*): 16-bit type, per-tensor flags, and the act + round
 // bits the kernels read
 struct StCode {
@@ -652,6 +672,12 @@ inline StCode st_code(int32_t code) {
     StCode c{(code >> LDM_ST_SHIFT) & 3, code & (LDM_ST_X16 | LDM_ST_Y16 | LDM_ST_DY16 | LDM_ST_DX16), code & 0xffff};
     if (c.st != LDM_DT_F16 && c.st != LDM_DT_BF16) c.st = 0, c.sf = 0;
     return c;
+}
+// the HM of a call: which of `bits` (the flags of the tensors it reads / writes) are set
+inline int bn_hm(const StCode& sc, int bits) {
+    if (sc.st == 0) return 2;
+    const int f = sc.sf & bits;
+    return f == bits ? 1 : (f == 0 ? 2 : 0);
 }
 // f(integral_constant<int, ST>) for the code's storage type
 template <class F>
@@ -683,9 +709,10 @@ static int bn_stats_launch(const void* x, const StCode& sc, int32_t B, int32_t C
     const int vw = vec_width(HW, x);
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
+    const int hm = bn_hm(sc, LDM_ST_X16);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
-            hipLaunchKernelGGL((bn_stats_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads),
+        w_dispatch(vw, [&](auto wc) { uh_dispatch(hm, [&](auto uc, auto hc) {
+            hipLaunchKernelGGL((bn_stats_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value, decltype(hc)::value>), grid, dim3(kThreads),
                                0, (hipStream_t)stream, x, sc.sf, C, HW, n, S, part);
         }); });
     });
@@ -725,9 +752,10 @@ static int bn_apply_launch(const float* x, float* y, int32_t B, int32_t C, int32
     const int vw = vec_width(HW, x, y);
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
+    const int hm = bn_hm(sc, LDM_ST_X16 | LDM_ST_Y16);
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
-            hipLaunchKernelGGL((bn_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads), 0,
+        w_dispatch(vw, [&](auto wc) { uh_dispatch(hm, [&](auto uc, auto hc) {
+            hipLaunchKernelGGL((bn_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value, decltype(hc)::value>), grid, dim3(kThreads), 0,
                                (hipStream_t)stream, x, y, sc.sf, C, HW, n, S, stats, count, weight, bias, running_mean,
                                running_var, momentum, eps, sc.act, save_mean, save_invstd, part, part ? P : 0);
         }); });
@@ -791,9 +819,10 @@ static int bn_bwd_partial_launch(const void* dy, const void* y, const void* x, c
     const int vw = vec_width(HW, dy, y, x);
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
+    const int hm = bn_hm(sc, LDM_ST_DY16 | LDM_ST_X16 | (y ? LDM_ST_Y16 : 0));
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
-            hipLaunchKernelGGL((bn_bwd_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads),
+        w_dispatch(vw, [&](auto wc) { uh_dispatch(hm, [&](auto uc, auto hc) {
+            hipLaunchKernelGGL((bn_bwd_partial_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value, decltype(hc)::value>), grid, dim3(kThreads),
                                0, (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW,
                                n, S, part);
         }); });
@@ -835,9 +864,10 @@ static int bn_bwd_apply_launch(const void* dy, const void* y, const void* x, con
     const int vw = vec_width(HW, dy, y, x, dx);
     const int64_t S = slice_len(n, P, vw);
     const dim3 grid(P, C);
+    const int hm = bn_hm(sc, LDM_ST_DY16 | LDM_ST_X16 | LDM_ST_DX16 | (y ? LDM_ST_Y16 : 0));
     st_dispatch(sc, [&](auto stc) {
-        w_dispatch(vw, [&](auto wc) { u_dispatch([&](auto uc) {
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value>), grid, dim3(kThreads), 0,
+        w_dispatch(vw, [&](auto wc) { uh_dispatch(hm, [&](auto uc, auto hc) {
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<decltype(wc)::value, decltype(stc)::value, decltype(uc)::value, decltype(hc)::value>), grid, dim3(kThreads), 0,
                                (hipStream_t)stream, dy, y, x, sc.sf, save_mean, save_invstd, weight, bias, act, C, HW, n,
                                S, sums, count, dx, part, part ? P : 0, dweight, dbias, dxs_part);
         }); });

@@ -847,7 +847,19 @@ static int ks_mask() {
     }();
     return m;
 }
-static bool ks_on(int layer) { return kKs[layer].ks > 1 && ((ks_mask() >> layer) & 1); }
+// 16-bit operands (config 5) stream half the weight bytes per block, so the split that pays for fp32 need not pay
+// there: their own mask, LDM_UCONV_KS_LOWP (default kKsDefaultLowp, measured in the fp16 loop)
+constexpr int kKsDefaultLowp = kKsDefault;
+static int ks_mask_lowp() {
+    static const int m = [] {
+        const char* e = std::getenv("LDM_UCONV_KS_LOWP");
+        return e ? (int)std::strtol(e, nullptr, 0) : kKsDefaultLowp;
+    }();
+    return m;
+}
+static bool ks_on(int layer, int dtype = LDM_DT_F32) {
+    return kKs[layer].ks > 1 && (((dtype == LDM_DT_F32 ? ks_mask() : ks_mask_lowp()) >> layer) & 1);
+}
 // (the bottleneck's variants measured alike: 16 x 32 KS 2 79.7, 16 x 64 KS 4 80.1, 32 x 32 KS 4 79.9 us per
 // iteration, profiles/r03/geo; it keeps variant 1)
 constexpr int kKs2Default = (1 << 3) | (1 << 5);
@@ -859,8 +871,8 @@ static int ks2_mask() {
     return m;
 }
 // K-split form of a layer: 0 none, 1 variant 1 (kKs), 2 variant 2 (kKs2)
-static int ks_form(int layer) {
-    if (layer < 0 || layer > 8 || !ks_on(layer)) return 0;
+static int ks_form(int layer, int dtype = LDM_DT_F32) {
+    if (layer < 0 || layer > 8 || !ks_on(layer, dtype)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
 }
 // dec1 on 16-row x 64-position tiles: half of the 32 output channels per block, so a block streams half of the
@@ -1034,7 +1046,7 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
 
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st) {
     using namespace uc;
-    const int ksv = s.ws ? ks_form(layer) : 0;   // without a workspace: the single-block form
+    const int ksv = s.ws ? ks_form(layer, s.dtype) : 0;   // without a workspace: the single-block form
     UArgs a;
     UC_TRY(make_args(layer, B, H, W, s, ksv, a));
     if (ksv == 2) {

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="per-block phase stamps (needs a UCONV_DIAG=4 build, tools/step_diag.sh)")
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--layers", default=None, help="comma list of layer indices (default all)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp16", "bf16"],
+                    help="operand precision of the step kernels (config 5: fp16)")
     ap.add_argument("--loop-only", default=None, help="comma list of use_step values: only time the loop")
     args = ap.parse_args()
     B, H, W = (int(v) for v in args.shape.split("x"))
@@ -64,7 +66,8 @@ def main():
         x = torch.randn(B, Hin, Win, Cin, device=dev)
         w = torch.randn((Cin, Cout, 3, 3) if mode == 2 else (Cout, Cin, 3, 3), device=dev) * 0.05
         packed = torch.empty(int(lib.ldm_step_packed_floats(layer)), device=dev)
-        L.call("ldm_step_pack_weight", layer, w.data_ptr(), packed.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        dt = {"fp32": 0, "fp16": 1, "bf16": 2}[args.dtype]
+        L.call("ldm_step_pack_weight_dt", layer, dt, w.data_ptr(), packed.data_ptr(), torch.cuda.current_stream().cuda_stream)
         bias = torch.randn((Hout * Wout * Cout) if layer in (3, 4) else Cout, device=dev)
         bc = torch.randn(B, Cout, device=dev)
         sk = torch.randn(B, Hout, Wout, Cout, device=dev)
@@ -79,7 +82,7 @@ def main():
             skp = sk.data_ptr() if mode == 2 else None
             stp = torch.cuda.current_stream().cuda_stream
             rc = lib.ldm_step_conv_ws(layer, B, H, W, x.data_ptr(), packed.data_ptr(), bias.data_ptr(), bcp, skp,
-                                      y.data_ptr(), 0, ws.data_ptr(), stp)
+                                      y.data_ptr(), dt, ws.data_ptr(), stp)
             assert rc == 0
 
         us = graph_us(run, args.reps)
