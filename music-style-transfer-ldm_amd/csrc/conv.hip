@@ -768,6 +768,81 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(ConvArgs a) {
     epilogue_store(a, co, b, oy, ox, acc);
 }
 
+// Cin -> 1 conv, k3 s1 p1 (the UNet's dec1 on a raw mel, SURVEY shape S: 64 -> 1 on 128 x 512 at B = 1).
+// conv_direct_kernel gives such a layer one lane per output (65,536 lanes = 1 wave per SIMD) walking all Cin x 9
+// taps serially: 240 us per launch for 16.8 MB of input.  Here a lane owns 4 adjacent outputs of a row (their
+// 3 x 6 window per channel: one 16-byte load and two scalars per row) and one of G = 8 channel groups; the G
+// partial sums of a quad meet in LDS in group order.  Each output's sum: per group, channels ascending, taps in
+// window order (fmaf), then the groups in order — a fixed order, so bitwise reproducible.
+constexpr int kC1Groups = 8;
+__global__ __launch_bounds__(256) void conv_cout1_k3_kernel(ConvArgs a) {
+    constexpr int G = kC1Groups, QB = 256 / G;   // channel groups, output quads per block
+    __shared__ float wsm[512 * 9];
+    __shared__ float4 red[G][QB];
+    const int Cin = a.Cin;
+    for (int i = threadIdx.x; i < Cin * 9; i += 256) wsm[i] = round16(a.w[i], a.ep.lowp);   // [ci][ky*3 + kx]
+    __syncthreads();
+    const int g = threadIdx.x / QB, ql = threadIdx.x - g * QB;
+    const int wq = a.Wout >> 2;
+    const int quad = blockIdx.x * QB + ql;
+    const int nquad = a.B * a.Hout * wq;
+    const bool qv = quad < nquad;
+    const int qq = qv ? quad : 0;
+    const int rest = a.fd_dwo.div(qq);   // (b, oy)
+    const int ox0 = (qq - rest * wq) * 4;
+    const int b = a.fd_dho.div(rest);
+    const int oy = rest - b * a.Hout;
+    const int HW = a.Hin * a.Win;
+    const int cpg = Cin / G;
+    const float* xb = a.x + ((size_t)b * Cin + (size_t)g * cpg) * HW;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    bool rok[3];
+    int roff[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int iy = oy - 1 + r;
+        rok[r] = iy >= 0 && iy < a.Hin;
+        roff[r] = (rok[r] ? iy : 0) * a.Win + ox0;
+    }
+    const bool lok = ox0 > 0, rgt = ox0 + 4 < a.Win;
+    for (int c = 0; c < cpg; ++c) {
+        const float* xp = xb + (size_t)c * HW;
+        const float* wc = wsm + (g * cpg + c) * 9;
+        float win[3][6];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {   // loads first (no branch around them: the masks apply after)
+            const float4 m = *reinterpret_cast<const float4*>(xp + roff[r]);
+            const float l = xp[roff[r] + (lok ? -1 : 0)], rr = xp[roff[r] + (rgt ? 4 : 0)];
+            win[r][0] = rok[r] && lok ? l : 0.f;
+            win[r][1] = rok[r] ? m.x : 0.f;
+            win[r][2] = rok[r] ? m.y : 0.f;
+            win[r][3] = rok[r] ? m.z : 0.f;
+            win[r][4] = rok[r] ? m.w : 0.f;
+            win[r][5] = rok[r] && rgt ? rr : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx)
+                    acc[j] = fmaf(round16(win[ky][j + kx], a.ep.lowp), wc[ky * 3 + kx], acc[j]);
+    }
+    red[g][ql] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (g != 0 || !qv) return;
+    float4 s = red[0][ql];
+#pragma unroll
+    for (int k = 1; k < G; ++k) {
+        const float4 t = red[k][ql];
+        s.x = s.x + t.x, s.y = s.y + t.y, s.z = s.z + t.z, s.w = s.w + t.w;
+    }
+    epilogue_store(a, 0, b, oy, ox0 + 0, s.x);
+    epilogue_store(a, 0, b, oy, ox0 + 1, s.y);
+    epilogue_store(a, 0, b, oy, ox0 + 2, s.z);
+    epilogue_store(a, 0, b, oy, ox0 + 3, s.w);
+}
+
 // Single-input-channel conv (the VAE encoder's and the style encoder's first layers, 1 -> 64 on 128x512
 // mels): one lane per output pixel computes every output channel from one k x k window read, with the
 // Cout x k*k weights in LDS; the stores stay coalesced (consecutive lanes = consecutive ox per channel).
@@ -950,6 +1025,15 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         for (int j = 0; j < 4; ++j) v[j] = chan_apply<RO>(a, ce, acc[j]);
         store4<YS>(a, o, v);
     }
+}
+
+// conv_cout1_k3_kernel for the Cin -> 1 k3 s1 convs (LDM_COUT1=0: conv_direct_kernel, A/B timing)
+static bool cout1_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("LDM_COUT1");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
 }
 
 // the packed form of conv_cin1_x4_kernel: LDM_CIN1_PK (default 1: the B = 32 first layer 48.5 -> 44.6 us per
@@ -1641,6 +1725,16 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
             const int64_t pix = (int64_t)d.B * d.Hout * d.Wout;
             hipLaunchKernelGGL(conv_cin1_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, st, a);
             LDM_CHECK_LAUNCH("conv_cin1_kernel");
+            return 0;
+        }
+        if (!d.transposed && d.Cout == 1 && d.kh == 3 && d.kw == 3 && d.stride == 1 && d.pad == 1 && d.Cin % kC1Groups == 0 &&
+            d.Cin <= 512 && d.Wout % 4 == 0 && d.Win == d.Wout && d.Hin == d.Hout && ((uintptr_t)x & 15) == 0 && cout1_on()) {
+            a.fd_dwo = FastDiv::make(d.Wout / 4);
+            a.fd_dho = FastDiv::make(d.Hout);
+            const int64_t quads = (int64_t)d.B * d.Hout * (d.Wout / 4);
+            constexpr int QB = 256 / kC1Groups;
+            hipLaunchKernelGGL(conv_cout1_k3_kernel, dim3((unsigned)((quads + QB - 1) / QB)), dim3(256), 0, st, a);
+            LDM_CHECK_LAUNCH("conv_cout1_k3_kernel");
             return 0;
         }
         hipLaunchKernelGGL(conv_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);

@@ -28,7 +28,8 @@ def main():
     out, layers = sys.argv[1], sys.argv[2:]
     res = {"per_launch_bytes": {}, "detail": {},
            "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over tools/step_times.py "
-                     "--variant hybrid --layers L, B=8 16x64 latent, median dispatch; FETCH_SIZE x2 (gfx950)"}
+                     f"--layers L --dtype {os.environ.get('DTYPE', 'fp32')} (the instance the loop runs), B=8 16x64 "
+                     "latent, median dispatch; FETCH_SIZE x2 (gfx950)"}
     for L in layers:
         name = NAMES[int(L)]
         fetch_kib = per_dispatch(os.path.join(out, f"l{L}_FETCH_SIZE"), "FETCH_SIZE")
