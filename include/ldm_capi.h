@@ -423,6 +423,20 @@ int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, const float
  * dv may alias dy.  workspace: ldm_reduce_workspace_floats(B,C,HW) floats (NULL when no sums). */
 int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act, int32_t B, int32_t C,
                      int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace, void* stream);
+/* ldm_act_backward with the bias gradient's finalize deferred (the train step's convs: their bias gradients are read
+ * only by the optimizer): the slice partials go to `workspace` (ldm_act_partial_floats(B, C, HW) floats, kept until
+ * the finalize), *q_out receives their slice count for the job (0: nothing deferred — the small-plane kernel
+ * wrote dbias itself).  No bcast gradient.  ldm_act_finalize_many then writes every job's dbias in one launch per 24
+ * jobs, bitwise what ldm_act_backward writes. */
+int ldm_act_backward_defer(const float* dy, const float* act_out, const float* pre_act, int32_t act_code, int32_t B,
+                           int32_t C, int32_t HW, float* dv, float* dbias, float* workspace, int32_t* q_out, void* stream);
+int64_t ldm_act_partial_floats(int32_t B, int32_t C, int32_t HW);
+typedef struct ldm_act_fin_job {
+    const float* part;   /* the deferred call's workspace */
+    float* dbias;        /* [C] */
+    int32_t B, C, Q;     /* Q: the call's *q_out */
+} ldm_act_fin_job;
+int ldm_act_finalize_many(const ldm_act_fin_job* jobs, int32_t n, void* stream);
 /* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
  * y = its output, x = its input, weight / bias its affine parameters (NULL = 1 / 0); dx / dweight / dbias
  * may be NULL.  y may be NULL when act is NONE or RELU: the ReLU mask is then re-evaluated from x with the

@@ -528,11 +528,9 @@ __global__ __launch_bounds__(kThreads) void act_bwd_planes_kernel(const void* __
 // order.  A fixed partition and order, so bitwise reproducible (a single thread walking B*Q partials
 // serially took 150 us for the decoder's one-channel output layer at B = 32; one plane per wave step left
 // the Q = 1 finalize of the plane kernels at 8 serial load round trips per wave).
-__global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float* __restrict__ part, int B, int C,
-                                                                    int Q, int QP, float* __restrict__ dbias,
-                                                                    float* __restrict__ dbcast) {
+__device__ __forceinline__ void act_fin_body(const float* __restrict__ part, int B, int C, int Q, int QP,
+                                             float* __restrict__ dbias, float* __restrict__ dbcast, int c) {
     __shared__ float wsum[kThreads / 64];
-    const int c = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int ppw = 64 / QP, sub = lane / QP, k0 = lane % QP;
     float sb = 0.f;
@@ -562,6 +560,32 @@ __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float*
         for (int w = 0; w < kThreads / 64; ++w) s += wsum[w];
         dbias[c] = s;
     }
+}
+__global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float* __restrict__ part, int B, int C,
+                                                                    int Q, int QP, float* __restrict__ dbias,
+                                                                    float* __restrict__ dbcast) {
+    act_fin_body(part, B, C, Q, QP, dbias, dbcast, blockIdx.x);
+}
+
+// The finalizes of several activation backwards in one launch (ldm_act_finalize_many): the bias gradients of a
+// train step's convs are read only by the optimizer, so their finalize launches (one per conv, ~16 per step) can
+// wait for the end of the backward and go as one.  Block -> (job, channel) by the jobs' first blocks c0; each
+// channel's sums are act_bwd_finalize_kernel's (act_fin_body), so the same bits.
+struct FinJob {
+    const float* part;
+    float* dbias;
+    int32_t B, C, Q, QP, c0;
+};
+constexpr int kMaxFinJobs = 24;
+struct FinJobs {
+    FinJob j[kMaxFinJobs];
+    int32_t n;
+};
+__global__ __launch_bounds__(kThreads) void act_bwd_finalize_many_kernel(FinJobs jobs) {
+    int k = 0;
+    while (k + 1 < jobs.n && (int)blockIdx.x >= jobs.j[k + 1].c0) ++k;
+    const FinJob& J = jobs.j[k];
+    act_fin_body(J.part, J.B, J.C, J.Q, J.QP, J.dbias, nullptr, (int)blockIdx.x - J.c0);
 }
 static int finalize_lanes(int Q) {
     int qp = 1;
@@ -937,9 +961,12 @@ extern "C" int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, con
     return 0;
 }
 
-extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
-                                int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
-                                void* stream) {
+// defer_q != NULL (ldm_act_backward_defer): the slice partials stay in `workspace` for ldm_act_finalize_many and
+// *defer_q receives their slice count Q (0: nothing deferred, the small-plane kernel wrote dbias itself)
+static int act_backward_impl(const float* dy, const float* act_out, const float* pre_act, int32_t act_code, int32_t B,
+                             int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
+                             int32_t* defer_q, void* stream) {
+    if (defer_q) *defer_q = 0;
     const StCode sc = st_code(act_code);
     const int act = sc.act & 0xff;
     LDM_REQUIRE(dy && B > 0 && C > 0 && HW > 0, "act_backward: bad argument");
@@ -975,7 +1002,9 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
             }
         });
         LDM_CHECK_LAUNCH("act_bwd_planes_kernel");
-        if (sums) {
+        if (sums && defer_q) {
+            *defer_q = 1;
+        } else if (sums) {
             hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, 1, 1, dbias, dbcast);
             LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
         }
@@ -994,10 +1023,50 @@ extern "C" int ldm_act_backward(const float* dy, const float* act_out, const flo
         });
     });
     LDM_CHECK_LAUNCH("act_bwd_kernel");
-    if (sums) {
+    if (sums && defer_q) {
+        *defer_q = Q;
+    } else if (sums) {
         hipLaunchKernelGGL(act_bwd_finalize_kernel, dim3(C), dim3(kThreads), 0, st, part, B, C, Q,
                            finalize_lanes(Q), dbias, dbcast);
         LDM_CHECK_LAUNCH("act_bwd_finalize_kernel");
+    }
+    return 0;
+}
+
+extern "C" int ldm_act_backward(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
+                                int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* dbcast, float* workspace,
+                                void* stream) {
+    return act_backward_impl(dy, act_out, pre_act, act_code, B, C, HW, dv, dbias, dbcast, workspace, nullptr, stream);
+}
+
+extern "C" int ldm_act_backward_defer(const float* dy, const float* act_out, const float* pre_act, int32_t act_code,
+                                      int32_t B, int32_t C, int32_t HW, float* dv, float* dbias, float* workspace,
+                                      int32_t* q_out, void* stream) {
+    LDM_REQUIRE(q_out && dbias && workspace, "act_backward_defer: bad argument");
+    return act_backward_impl(dy, act_out, pre_act, act_code, B, C, HW, dv, dbias, nullptr, workspace, q_out, stream);
+}
+
+extern "C" int64_t ldm_act_partial_floats(int32_t B, int32_t C, int32_t HW) {
+    if (B <= 0 || C <= 0 || HW <= 0) return -1;
+    return (int64_t)B * C * act_slices(B, C, HW) * 2;
+}
+
+extern "C" int ldm_act_finalize_many(const ldm_act_fin_job* jobs, int32_t n, void* stream) {
+    LDM_REQUIRE(jobs && n >= 0, "act_finalize_many: bad argument");
+    hipStream_t st = (hipStream_t)stream;
+    for (int i0 = 0; i0 < n; i0 += kMaxFinJobs) {
+        FinJobs fj{};
+        int blocks = 0;
+        fj.n = n - i0 < kMaxFinJobs ? n - i0 : kMaxFinJobs;
+        for (int i = 0; i < fj.n; ++i) {
+            const ldm_act_fin_job& J = jobs[i0 + i];
+            LDM_REQUIRE(J.part && J.dbias && J.B > 0 && J.C > 0 && J.Q > 0, "act_finalize_many: bad job");
+            fj.j[i] = FinJob{J.part, J.dbias, J.B, J.C, J.Q, finalize_lanes(J.Q), blocks};
+            blocks += J.C;
+        }
+        if (blocks == 0) continue;
+        hipLaunchKernelGGL(act_bwd_finalize_many_kernel, dim3(blocks), dim3(kThreads), 0, st, fj);
+        LDM_CHECK_LAUNCH("act_bwd_finalize_many_kernel");
     }
     return 0;
 }

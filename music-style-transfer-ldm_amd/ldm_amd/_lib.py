@@ -45,6 +45,11 @@ class ConvPlan(ctypes.Structure):
         return (self.kind, self.tm, self.tn, self.wk, -self.ks if self.balance else self.ks)
 
 
+class ActFinJob(ctypes.Structure):
+    """ldm_act_fin_job: one deferred bias-gradient finalize (ldm_act_backward_defer / ldm_act_finalize_many)."""
+    _fields_ = [("part", c_fp), ("dbias", c_fp), ("B", c_int32), ("C", c_int32), ("Q", c_int32)]
+
+
 class UNetShape(ctypes.Structure):
     _fields_ = [("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32), ("nf", c_int32)]
 
@@ -169,6 +174,10 @@ SIGNATURES = {
     "ldm_conv_wgrad_workspace_floats": (c_int64, [ctypes.POINTER(ConvDesc)]),
     "ldm_conv_backward_weight_dt": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_int32, c_vp]),
     "ldm_conv_backward_weight": (c_int32, [ctypes.POINTER(ConvDesc), c_fp, c_fp, c_fp, c_int32, c_fp, c_vp]),
+    "ldm_act_backward_defer": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_vp,
+                                         c_vp]),
+    "ldm_act_partial_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_act_finalize_many": (c_int32, [c_vp, c_int32, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),
     "ldm_batchnorm_backward": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,

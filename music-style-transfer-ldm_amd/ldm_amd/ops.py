@@ -539,11 +539,71 @@ def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=Fa
     dbc = torch.empty((B, C), device=dy.device, dtype=torch.float32) if need_bcast else None
     if act == "none" and not need_bias and not need_bcast:
         return dv, None, None
-    ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
     code = L.ACT[act] | st_code(st, x16=ah, dy16=dyh, dx16=dyh and dv is not None)
+    if _BIAS_DEFER and need_bias and not need_bcast and HW > 16:
+        # the bias gradient's finalize waits for the end of the backward (bias_grads_deferred)
+        lib = L.load()
+        part = _defer_part(int(lib.ldm_act_partial_floats(B, C, HW)), dy.device)
+        q = ctypes.c_int32(0)
+        L.call("ldm_act_backward_defer", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)),
+               code, B, C, HW, _p(dv) if act != "none" else None, _p(db), ctypes.c_void_p(part),
+               ctypes.byref(q), stream_handle())
+        if q.value > 0:
+            _BIAS_DEFER[-1].append(L.ActFinJob(part, db.data_ptr(), B, C, q.value))
+        return dv, db, dbc
+    ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
     L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)), code, B,
            C, HW, _p(dv) if act != "none" else None, _p(db), _p(dbc), _p(ws), stream_handle())
     return dv, db, dbc
+
+
+_BIAS_DEFER = []     # job lists of the open bias_grads_deferred blocks
+_DEFER_ARENA = {}    # device -> [chunks, cursor]: the deferred partials' storage, reused step after step
+
+
+def _defer_part(nfloats, device):
+    """Device address of nfloats floats of the deferral arena: chunks allocated on first use and kept (a captured
+    step records their addresses; every step takes them in the same order, so the eager warm-up sizes them)."""
+    ent = _DEFER_ARENA.setdefault(str(device), {"chunks": [], "ci": 0, "off": 0})
+    need = (int(nfloats) + 63) // 64 * 64
+    while True:
+        if ent["ci"] < len(ent["chunks"]):
+            ch = ent["chunks"][ent["ci"]]
+            if ent["off"] + need <= ch.numel():
+                ptr = ch.data_ptr() + ent["off"] * 4
+                ent["off"] += need
+                return ptr
+            ent["ci"] += 1
+            ent["off"] = 0
+            continue
+        ent["chunks"].append(torch.empty(max(need, 1 << 20), device=device, dtype=torch.float32))
+
+
+class bias_grads_deferred:
+    """with bias_grads_deferred(): loss.backward() -- the convs' bias gradients (ldm_act_backward's per-channel sums)
+    are finalized at the end of the block, one launch for all of them (ldm_act_finalize_many), on the current stream
+    (which the autograd engine has synchronised with the backward's leaf streams by then).  Only where nothing reads a
+    bias gradient before the block ends: LDMTrainer's step without a gradient all-reduce (its post-accumulate hooks
+    would read it early).  Bitwise the immediate finalize."""
+
+    def __init__(self, enabled=True):
+        self.enabled = bool(enabled)
+
+    def __enter__(self):
+        if self.enabled:
+            _BIAS_DEFER.append([])
+            for ent in _DEFER_ARENA.values():
+                ent["ci"], ent["off"] = 0, 0
+        return self
+
+    def __exit__(self, *exc):
+        if not self.enabled:
+            return False
+        jobs = _BIAS_DEFER.pop()
+        if jobs and exc[0] is None:
+            arr = (L.ActFinJob * len(jobs))(*jobs)
+            L.call("ldm_act_finalize_many", ctypes.cast(arr, ctypes.c_void_p), len(jobs), stream_handle())
+        return False
 
 
 def reduce_workspace(B, C, HW, device):

@@ -227,7 +227,9 @@ class LDMTrainer:
         # the step's reconstruction (a static buffer of the graph when the step is replayed): for callers that
         # inspect the step's output, e.g. the parity tests; nothing in the step reads it
         self.last_outputs = {"reconstructed": reconstructed.detach()}
-        self.scaler.scale(total_loss).backward()
+        # the convs' bias-gradient finalizes as one launch after the backward (no all-reduce hook reads them early)
+        with ops.bias_grads_deferred(enabled=self.reducer is None and os.environ.get("LDM_AMD_DEFER_BIAS", "1") != "0"):
+            self.scaler.scale(total_loss).backward()
         if self.reducer is not None:
             self.reducer.finish()
         self.scaler.step(self.optimizer)
