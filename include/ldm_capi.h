@@ -432,9 +432,10 @@ int ldm_act_backward_defer(const float* dy, const float* act_out, const float* p
                            int32_t C, int32_t HW, float* dv, float* dbias, float* workspace, int32_t* q_out, void* stream);
 int64_t ldm_act_partial_floats(int32_t B, int32_t C, int32_t HW);
 typedef struct ldm_act_fin_job {
-    const float* part;   /* the deferred call's workspace */
-    float* dbias;        /* [C] */
-    int32_t B, C, Q;     /* Q: the call's *q_out */
+    const float* part;   /* the deferred call's partials */
+    float* dbias;        /* [C]: the sums */
+    int32_t B, C, Q;     /* Q: the call's *q_out (kind 1: *p_out) */
+    int32_t kind;        /* 0: ldm_act_backward_defer; 1: ldm_batchnorm_backward_dxsum_defer's dx sum */
 } ldm_act_fin_job;
 int ldm_act_finalize_many(const ldm_act_fin_job* jobs, int32_t n, void* stream);
 /* train-mode BatchNorm2d (+ReLU/Tanh) backward from the saved batch stats of ldm_batchnorm_train:
@@ -452,6 +453,13 @@ int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, const float* x
                                  const float* save_invstd, const float* weight, const float* bias, int32_t act,
                                  int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
                                  float* dx_sum, float* workspace, void* stream);
+/* ldm_batchnorm_backward_dxsum with the dx sum's finalize deferred to ldm_act_finalize_many (a job of kind 1 with
+ * part = dxs_part, dbias = dx_sum, Q = *p_out); dxs_part holds ldm_bn_dxsum_partial_floats(B, C, HW) floats. */
+int ldm_batchnorm_backward_dxsum_defer(const float* dy, const float* y, const float* x, const float* save_mean,
+                                       const float* save_invstd, const float* weight, const float* bias, int32_t act_code,
+                                       int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
+                                       float* dx_sum, float* dxs_part, int32_t* p_out, float* workspace, void* stream);
+int64_t ldm_bn_dxsum_partial_floats(int32_t B, int32_t C, int32_t HW);
 /* The same in two stages for SyncBatchNorm: sums[2c] = sum g, sums[2c+1] = sum g*xhat over this rank
  * (g = dy*act'(y)) and sums[2C] = this rank's B*H*W (sums holds 2C+1 doubles); dbias / dweight get the
  * local sums (parameter grads stay local, as in torch.nn.SyncBatchNorm; the DP gradient all-reduce

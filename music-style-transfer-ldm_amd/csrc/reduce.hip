@@ -574,7 +574,7 @@ __global__ __launch_bounds__(kThreads) void act_bwd_finalize_kernel(const float*
 struct FinJob {
     const float* part;
     float* dbias;
-    int32_t B, C, Q, QP, c0;
+    int32_t B, C, Q, QP, c0, kind;   // kind 0: act_fin_body; 1: chan_sum_finalize_kernel's sum (Q = its P)
 };
 constexpr int kMaxFinJobs = 24;
 struct FinJobs {
@@ -585,7 +585,14 @@ __global__ __launch_bounds__(kThreads) void act_bwd_finalize_many_kernel(FinJobs
     int k = 0;
     while (k + 1 < jobs.n && (int)blockIdx.x >= jobs.j[k + 1].c0) ++k;
     const FinJob& J = jobs.j[k];
-    act_fin_body(J.part, J.B, J.C, J.Q, J.QP, J.dbias, nullptr, (int)blockIdx.x - J.c0);
+    const int c = (int)blockIdx.x - J.c0;
+    if (J.kind == 0) {
+        act_fin_body(J.part, J.B, J.C, J.Q, J.QP, J.dbias, nullptr, c);
+    } else if (threadIdx.x == 0) {   // the slices in order, as chan_sum_finalize_kernel sums them
+        float a = 0.f;
+        for (int q = 0; q < J.Q; ++q) a += J.part[(size_t)c * J.Q + q];
+        J.dbias[c] = a;
+    }
 }
 static int finalize_lanes(int Q) {
     int qp = 1;
@@ -935,12 +942,10 @@ extern "C" int ldm_batchnorm_backward(const float* dy, const float* y, const flo
                                dx, part, dweight, dbias, stream);
 }
 
-// ldm_batchnorm_backward plus dx_sum[c] = sum of dx over (b, h, w): the bias gradient of the conv whose output is
-// the BN's input (no separate sweep over dx for it).  The slice partials go after the backward's own workspace.
-extern "C" int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, const float* x, const float* save_mean,
-                                            const float* save_invstd, const float* weight, const float* bias,
-                                            int32_t act_code, int32_t B, int32_t C, int32_t HW, float* dx,
-                                            float* dweight, float* dbias, float* dx_sum, float* workspace, void* stream) {
+static int bn_backward_dxsum_impl(const float* dy, const float* y, const float* x, const float* save_mean,
+                                  const float* save_invstd, const float* weight, const float* bias, int32_t act_code,
+                                  int32_t B, int32_t C, int32_t HW, float* dx, float* dweight, float* dbias,
+                                  float* dx_sum, float* dxs_ext, int32_t* p_out, float* workspace, void* stream) {
     LDM_REQUIRE(workspace && dx && dx_sum && B > 0 && C > 0 && HW > 0, "bn_backward_dxsum: bad argument");
     const StCode sc = st_code(act_code);
     const int act = sc.act & 0xff;
@@ -949,16 +954,47 @@ extern "C" int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, con
     const int64_t n = (int64_t)B * HW;
     const int P = bn_slices(n, C);
     double* part = reinterpret_cast<double*>(workspace);
-    float* dxs = workspace + 2 * ((int64_t)C * P * 2 + 2 * (int64_t)C + 2);
+    float* dxs = dxs_ext ? dxs_ext : workspace + 2 * ((int64_t)C * P * 2 + 2 * (int64_t)C + 2);
     int rc = bn_bwd_partial_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, part, stream);
     if (rc) return rc;
     rc = bn_bwd_apply_launch(dy, y, x, save_mean, save_invstd, weight, bias, sc, act, B, C, HW, nullptr, (double)n, dx,
                              part, dweight, dbias, stream, dxs);
     if (rc) return rc;
+    if (p_out) {   // deferred: ldm_act_finalize_many sums the slices later (job kind 1)
+        *p_out = P;
+        return 0;
+    }
     hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
                        (hipStream_t)stream, dxs, C, P, dx_sum);
     LDM_CHECK_LAUNCH("chan_sum_finalize_kernel");
     return 0;
+}
+
+// ldm_batchnorm_backward plus dx_sum[c] = sum of dx over (b, h, w): the bias gradient of the conv whose output is
+// the BN's input (no separate sweep over dx for it).  The slice partials go after the backward's own workspace.
+extern "C" int ldm_batchnorm_backward_dxsum(const float* dy, const float* y, const float* x, const float* save_mean,
+                                            const float* save_invstd, const float* weight, const float* bias,
+                                            int32_t act_code, int32_t B, int32_t C, int32_t HW, float* dx,
+                                            float* dweight, float* dbias, float* dx_sum, float* workspace, void* stream) {
+    return bn_backward_dxsum_impl(dy, y, x, save_mean, save_invstd, weight, bias, act_code, B, C, HW, dx, dweight, dbias,
+                                  dx_sum, nullptr, nullptr, workspace, stream);
+}
+
+// The same with the dx-sum's slice partials in `dxs_part` (ldm_bn_dxsum_partial_floats(B, C, HW) floats, kept until
+// the finalize) and the finalize deferred: *p_out = the slice count for an ldm_act_finalize_many job of kind 1.
+extern "C" int ldm_batchnorm_backward_dxsum_defer(const float* dy, const float* y, const float* x, const float* save_mean,
+                                                  const float* save_invstd, const float* weight, const float* bias,
+                                                  int32_t act_code, int32_t B, int32_t C, int32_t HW, float* dx,
+                                                  float* dweight, float* dbias, float* dx_sum, float* dxs_part,
+                                                  int32_t* p_out, float* workspace, void* stream) {
+    LDM_REQUIRE(dxs_part && p_out, "bn_backward_dxsum_defer: bad argument");
+    return bn_backward_dxsum_impl(dy, y, x, save_mean, save_invstd, weight, bias, act_code, B, C, HW, dx, dweight, dbias,
+                                  dx_sum, dxs_part, p_out, workspace, stream);
+}
+
+extern "C" int64_t ldm_bn_dxsum_partial_floats(int32_t B, int32_t C, int32_t HW) {
+    if (B <= 0 || C <= 0 || HW <= 0) return -1;
+    return (int64_t)C * bn_slices((int64_t)B * HW, C);
 }
 
 // defer_q != NULL (ldm_act_backward_defer): the slice partials stay in `workspace` for ldm_act_finalize_many and
@@ -1060,8 +1096,9 @@ extern "C" int ldm_act_finalize_many(const ldm_act_fin_job* jobs, int32_t n, voi
         fj.n = n - i0 < kMaxFinJobs ? n - i0 : kMaxFinJobs;
         for (int i = 0; i < fj.n; ++i) {
             const ldm_act_fin_job& J = jobs[i0 + i];
-            LDM_REQUIRE(J.part && J.dbias && J.B > 0 && J.C > 0 && J.Q > 0, "act_finalize_many: bad job");
-            fj.j[i] = FinJob{J.part, J.dbias, J.B, J.C, J.Q, finalize_lanes(J.Q), blocks};
+            LDM_REQUIRE(J.part && J.dbias && J.C > 0 && J.Q > 0 && (J.kind == 1 || (J.kind == 0 && J.B > 0)),
+                        "act_finalize_many: bad job");
+            fj.j[i] = FinJob{J.part, J.dbias, J.B, J.C, J.Q, finalize_lanes(J.Q), blocks, J.kind};
             blocks += J.C;
         }
         if (blocks == 0) continue;

@@ -47,7 +47,7 @@ class ConvPlan(ctypes.Structure):
 
 class ActFinJob(ctypes.Structure):
     """ldm_act_fin_job: one deferred bias-gradient finalize (ldm_act_backward_defer / ldm_act_finalize_many)."""
-    _fields_ = [("part", c_fp), ("dbias", c_fp), ("B", c_int32), ("C", c_int32), ("Q", c_int32)]
+    _fields_ = [("part", c_fp), ("dbias", c_fp), ("B", c_int32), ("C", c_int32), ("Q", c_int32), ("kind", c_int32)]
 
 
 class UNetShape(ctypes.Structure):
@@ -177,6 +177,9 @@ SIGNATURES = {
     "ldm_act_backward_defer": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_vp,
                                          c_vp]),
     "ldm_act_partial_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_batchnorm_backward_dxsum_defer": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
+                                                     c_int32, c_fp, c_fp, c_fp, c_fp, c_vp, c_vp, c_fp, c_vp]),
+    "ldm_bn_dxsum_partial_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "ldm_act_finalize_many": (c_int32, [c_vp, c_int32, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),

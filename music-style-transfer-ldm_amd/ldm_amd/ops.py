@@ -549,7 +549,7 @@ def act_backward(dy, act, act_out=None, pre_act=None, need_dv=True, need_bias=Fa
                code, B, C, HW, _p(dv) if act != "none" else None, _p(db), ctypes.c_void_p(part),
                ctypes.byref(q), stream_handle())
         if q.value > 0:
-            _BIAS_DEFER[-1].append(L.ActFinJob(part, db.data_ptr(), B, C, q.value))
+            _BIAS_DEFER[-1].append(L.ActFinJob(part, db.data_ptr(), B, C, q.value, 0))
         return dv, db, dbc
     ws = reduce_workspace(B, C, HW, dy.device) if (need_bias or need_bcast) else None
     L.call("ldm_act_backward", dy.data_ptr(), _p(act_out), _p(None if pre_act is None else f32c(pre_act)), code, B,
@@ -580,8 +580,9 @@ def _defer_part(nfloats, device):
 
 
 class bias_grads_deferred:
-    """with bias_grads_deferred(): loss.backward() -- the convs' bias gradients (ldm_act_backward's per-channel sums)
-    are finalized at the end of the block, one launch for all of them (ldm_act_finalize_many), on the current stream
+    """with bias_grads_deferred(): loss.backward() -- the convs' bias gradients (ldm_act_backward's per-channel sums,
+    and the BatchNorm dx sums that stand for them, batchnorm_backward(dx_sum=True)) are finalized at the end of the
+    block, one launch for all of them (ldm_act_finalize_many), on the current stream
     (which the autograd engine has synchronised with the backward's leaf streams by then).  Only where nothing reads a
     bias gradient before the block ends: LDMTrainer's step without a gradient all-reduce (its post-accumulate hooks
     would read it early).  Bitwise the immediate finalize."""
@@ -668,9 +669,18 @@ def batchnorm_backward(dy, y, x, save_mean, save_invstd, weight, act, need_dx=Tr
             # + the per-channel sum of dx (the bias gradient of the conv that produced x), from the apply pass
             # itself: attached to dx for that conv's backward (functional._conv_backward)
             dxs = torch.empty(C, device=dy.device, dtype=torch.float32)
-            L.call("ldm_batchnorm_backward_dxsum", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
-                   save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, dx.data_ptr(), _p(dw), _p(db),
-                   dxs.data_ptr(), ws.data_ptr(), stream_handle())
+            if _BIAS_DEFER:   # the sum's finalize waits for the end of the backward (bias_grads_deferred)
+                lib = L.load()
+                part = _defer_part(int(lib.ldm_bn_dxsum_partial_floats(B, C, HW)), dy.device)
+                P = ctypes.c_int32(0)
+                L.call("ldm_batchnorm_backward_dxsum_defer", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
+                       save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, dx.data_ptr(), _p(dw), _p(db),
+                       dxs.data_ptr(), ctypes.c_void_p(part), ctypes.byref(P), ws.data_ptr(), stream_handle())
+                _BIAS_DEFER[-1].append(L.ActFinJob(part, dxs.data_ptr(), B, C, P.value, 1))
+            else:
+                L.call("ldm_batchnorm_backward_dxsum", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
+                       save_invstd.data_ptr(), _p(weight), _p(bias), code, B, C, HW, dx.data_ptr(), _p(dw), _p(db),
+                       dxs.data_ptr(), ws.data_ptr(), stream_handle())
             dx._ldm_chan_sum = dxs
             return dx, dw, db
         L.call("ldm_batchnorm_backward", dy.data_ptr(), _p(y), x.data_ptr(), save_mean.data_ptr(),
