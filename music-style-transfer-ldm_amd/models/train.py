@@ -21,6 +21,7 @@ Differences from the reference, all deliberate:
 """
 import argparse
 import os
+from collections.abc import Mapping
 
 import torch
 
@@ -139,6 +140,37 @@ def train_autoencoder(config, train_loader=None, test_loader=None, device=None):
 
 
 # ------------------------------------------------------------------------------------------------
+class StepLosses(Mapping):
+    """{"compression_loss", "denoisinsg_loss", "style_loss", "total_loss"} -> float, the fp32 values .item() would
+    return, read from a pinned copy issued when the step was queued; the first access waits for that copy."""
+    KEYS = ("compression_loss", "denoisinsg_loss", "style_loss", "total_loss")
+
+    def __init__(self, vec):
+        self._host = torch.empty(vec.shape, dtype=vec.dtype, pin_memory=True)
+        self._host.copy_(vec, non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+        self._vals = None
+
+    def _values(self):
+        if self._vals is None:
+            self._event.synchronize()
+            self._vals = dict(zip(self.KEYS, self._host.tolist()))
+        return self._vals
+
+    def __getitem__(self, k):
+        return self._values()[k]
+
+    def __iter__(self):
+        return iter(self.KEYS)
+
+    def __len__(self):
+        return len(self.KEYS)
+
+    def __repr__(self):
+        return repr(self._values())
+
+
 class LDMTrainer:
     """Reference train.py:140-293."""
 
@@ -249,13 +281,12 @@ class LDMTrainer:
 
     @staticmethod
     def _losses(vec):
-        c, d, s, tot = vec.tolist()      # the fp32 values, as .item() would return them
-        return {
-            "compression_loss": c,
-            "denoisinsg_loss": d,
-            "style_loss": s,
-            "total_loss": tot,
-        }
+        """The step's four losses as the reference's dict of Python floats (train.py:203-208).  On the GPU the values
+        come back through an asynchronous copy (StepLosses): the host waits for it only when a value is read, so a
+        loop of steps that reads them later (or not at all) queues its steps on the device back to back."""
+        if vec.device.type != "cuda":
+            return dict(zip(StepLosses.KEYS, vec.tolist()))
+        return StepLosses(vec)
 
     def _graphed_step(self, content_spec, style_spec, t, noise):
         """train_step as one hipGraph replay.  The optimizer runs its capturable form (device step count,
