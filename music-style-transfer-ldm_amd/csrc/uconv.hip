@@ -813,6 +813,26 @@ constexpr KsGeo kKs2[9] = {
     {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
 };
 
+// Variant 3 ("wide", round 6): 16 x 16 tiles with one channel chunk per wave and 16 waves per block (4 per SIMD), so a
+// block keeps 16 x 9 operand loads in flight across four times the waves: enc4 with K in one block (256 tiles, no
+// partial slabs), dec4 with K over 2 blocks (128 tiles; half the slab bytes of variant 2).  Selected by bit l of
+// LDM_UCONV_KS3 (A/B timing; it takes precedence over LDM_UCONV_KS / _KS2 for that layer).
+constexpr KsGeo kKs3[9] = {
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+    {1, 1, 16, 1},   // enc4        256 tiles, K whole
+    {0, 0, 0, 0},
+    {1, 1, 16, 2},   // dec4        128 tiles x 2
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+};
+constexpr int kKs3Default = 0;
+static int ks3_mask() {
+    static const int m = [] {
+        const char* e = std::getenv("LDM_UCONV_KS3");
+        return e ? (int)std::strtol(e, nullptr, 0) : kKs3Default;
+    }();
+    return m;
+}
+
 constexpr LayerGeo kGeo[9] = {
     {0, 32, 64, 2, 1, 4, 1},     // enc1        conv3x3 s1
     {1, 64, 128, 2, 2, 1, 4},    // enc2        conv3x3 s2 (+ t_emb)
@@ -872,6 +892,7 @@ static int ks2_mask() {
 }
 // K-split form of a layer: 0 none, 1 variant 1 (kKs), 2 variant 2 (kKs2)
 static int ks_form(int layer, int dtype = LDM_DT_F32) {
+    if (layer >= 0 && layer <= 8 && kKs3[layer].wk > 0 && ((ks3_mask() >> layer) & 1)) return 3;
     if (layer < 0 || layer > 8 || !ks_on(layer, dtype)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
 }
@@ -933,7 +954,7 @@ static bool plane_taps() {
 constexpr int kDiv[9] = {1, 1, 2, 4, 8, 8, 4, 2, 1};
 static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& slab_floats, int form = 1) {
     const LayerGeo& g = kGeo[layer];
-    const KsGeo& k = form == 2 ? kKs2[layer] : kKs[layer];
+    const KsGeo& k = form == 3 ? kKs3[layer] : (form == 2 ? kKs2[layer] : kKs[layer]);
     const int Hin = H / kDiv[layer], Win = W / kDiv[layer];
     const int64_t nq = (int64_t)B * (g.mode == 1 ? (Hin / 2) * (Win / 2) : Hin * Win);
     tiles = (int64_t)(g.cout / (16 * k.tm)) * ((nq + 16 * k.tn * k.wn - 1) / (16 * k.tn * k.wn));
@@ -949,8 +970,8 @@ int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     using namespace uc;
     int64_t mt = 0, ms = 0;
     for (int l = 0; l < 9; ++l) {
-        for (int form = 1; form <= 2; ++form) {   // every K-split geometry, whatever the masks select
-            if ((form == 1 ? kKs[l].ks : kKs2[l].ks) <= 1) continue;
+        for (int form = 1; form <= 3; ++form) {   // every K-split geometry, whatever the masks select
+            if ((form == 1 ? kKs[l].ks : (form == 2 ? kKs2[l].ks : kKs3[l].ks)) <= 1) continue;
             int64_t t, sf;
             ks_tiles(l, B, H, W, t, sf, form);
             mt = std::max(mt, t);
@@ -969,7 +990,7 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     LDM_REQUIRE(B > 0 && H % 8 == 0 && W % 8 == 0, "step conv: latent H, W must be multiples of 8");
     LayerGeo g = kGeo[layer];
     if (ksv) {
-        const KsGeo& k = ksv == 2 ? kKs2[layer] : kKs[layer];
+        const KsGeo& k = ksv == 3 ? kKs3[layer] : (ksv == 2 ? kKs2[layer] : kKs[layer]);
         g.tm = k.tm, g.tn = k.tn, g.wn = k.wn, g.wk = k.wk;
     } else if (layer == 8 && dec1_thin(W)) {
         g = LayerGeo{0, 64, 32, 1, 2, 2, 2};   // 16 of the 32 rows x 64 positions (2 wave columns), K over 2 waves
@@ -1049,6 +1070,15 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
     const int ksv = s.ws ? ks_form(layer, s.dtype) : 0;   // without a workspace: the single-block form
     UArgs a;
     UC_TRY(make_args(layer, B, H, W, s, ksv, a));
+    if (ksv == 3) {
+        switch (layer) {
+            case 3: LDM_REQUIRE(s.y && a.Hin == 4 && a.Win == 16 && plane_taps(), "enc4 (variant 3): y, 4 x 16 input plane");
+                return launch<1, 256, 512, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 1>(a, s.dtype, st);
+            case 5: LDM_REQUIRE(s.y && s.skip && a.Hin == 2 && a.Win == 8 && plane_taps(), "dec4 (variant 3): y, skip, 2 x 8 plane");
+                return launch<2, 512, 256, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_SKIP | EPI_PLANE, 2>(a, s.dtype, st);
+            default: return fail(2, "step conv: no K-split variant 3 for this layer");
+        }
+    }
     if (ksv == 2) {
         const bool pl = plane_taps();
         switch (layer) {
