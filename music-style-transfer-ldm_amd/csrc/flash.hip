@@ -19,6 +19,7 @@
 // [B, E, L] channel-major or token-major [B, L, E] (TOK, the UNet engine's NHWC activations); lse / delta
 // [B, heads, L].
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -42,11 +43,12 @@ constexpr int cs_pieces() { return D * (kTok / 4) / 256; }
 // the compiler wait for it at the join, which drains the look-ahead).  VEC: n % 4 == 0, so a float4 of a row is
 // wholly inside or wholly past it.
 template <int D, bool VEC>
-__device__ __forceinline__ void load_cs(const float* __restrict__ src, int n, int t0, float4 (&v)[cs_pieces<D>()]) {
+__device__ __forceinline__ void load_cs(const float* __restrict__ src, int n, int t0, float4 (&v)[cs_pieces<D>()],
+                                        int tid = (int)threadIdx.x) {
     constexpr int NIT = cs_pieces<D>();
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
-        const int e = u * 256 + (int)threadIdx.x;
+        const int e = u * 256 + tid;
         const int c = e / (kTok / 4), t = t0 + 4 * (e % (kTok / 4));
         const float* p = src + (size_t)c * n + t;
         if constexpr (VEC) {
@@ -66,10 +68,11 @@ __device__ __forceinline__ void load_cs(const float* __restrict__ src, int n, in
     }
 }
 template <int D>
-__device__ __forceinline__ void store_cs(const float4 (&v)[cs_pieces<D>()], float* __restrict__ dst) {
+__device__ __forceinline__ void store_cs(const float4 (&v)[cs_pieces<D>()], float* __restrict__ dst,
+                                         int tid = (int)threadIdx.x) {
 #pragma unroll
     for (int u = 0; u < cs_pieces<D>(); ++u) {
-        const int e = u * 256 + (int)threadIdx.x;
+        const int e = u * 256 + tid;
         *reinterpret_cast<float4*>(dst + (e / (kTok / 4)) * kKP + 4 * (e % (kTok / 4))) = v[u];
     }
 }
@@ -129,16 +132,23 @@ __device__ __forceinline__ void load_qfrag(const float* __restrict__ base, int E
 }
 
 // ---- forward ---------------------------------------------------------------------------------------
-template <int D, bool TOK, bool LSE, bool VEC>
-__global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+// KH > 1: the block's KH groups of four waves take the same 64 queries over KH contiguous ranges of key tiles (each
+// group stages its own tiles), and the groups' (m, l, O) meet in LDS at the end (O = sum_g e^(m_g - M) O_g over the
+// same sum of l_g): KH waves per SIMD where the grid has one block per CU.  NBUF: K / V buffers per group (1: the
+// next tile is stored after a barrier that closes the current one; the D = 128, KH = 2 form needs it to fit LDS).
+template <int D, bool TOK, bool LSE, bool VEC, int KH, int NBUF>
+__global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                         float* __restrict__ out, float* __restrict__ lse, int E,
                                                         int heads, int L, int S, float scale) {
     constexpr int NJ = D / 16;
-    extern __shared__ __attribute__((aligned(16))) float sm[];   // 2 x {K [D][kKP], V [D][kKP]}
+    extern __shared__ __attribute__((aligned(16))) float smem_all[];   // KH x NBUF x {K [D][kKP], V [D][kKP]}
     const int nqt = (L + kTok - 1) / kTok;
     const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
     const int h = bh % heads, b = bh / heads;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, lg = lane >> 4;
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, col = lane & 15, lg = lane >> 4;
+    const int kg = KH > 1 ? (int)(threadIdx.x >> 8) : 0;   // key group
+    const int gtid = (int)threadIdx.x & 255;
+    float* sm = smem_all + kg * (NBUF * 2 * D * kKP);
     const int l = qt * kTok + wave * 16 + col;
     const bool lok = l < L;
     const int lc = lok ? l : L - 1;
@@ -159,20 +169,25 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
     // tile t+1 is stored into the buffer tile t-1 used (every wave left it at the barrier closing iteration t-1),
     // then tile t+2's loads are issued; one barrier per tile.  (Round 6: the single-buffered form waited out
     // a load round trip per 64-key tile, 364 us per launch at L = S = 4096.)
-    const int nt = (S + kTok - 1) / kTok;
+    const int ntall = (S + kTok - 1) / kTok;
+    const int ntg = (ntall + KH - 1) / KH;                // tiles per key group (the last group may have fewer)
+    const int tb = kg * ntg, nt = min(ntall - tb, ntg);   // this group's first tile and its count (<= 0: none)
     float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
-    load_cs<D, VEC>(kb, S, 0, rk);
-    load_cs<D, VEC>(vb, S, 0, rv);
-    store_cs<D>(rk, sm);
-    store_cs<D>(rv, sm + D * kKP);
-    if (nt > 1) {
-        load_cs<D, VEC>(kb, S, kTok, rk);
-        load_cs<D, VEC>(vb, S, kTok, rv);
+    if (nt > 0) {
+        load_cs<D, VEC>(kb, S, tb * kTok, rk, gtid);
+        load_cs<D, VEC>(vb, S, tb * kTok, rv, gtid);
+        store_cs<D>(rk, sm, gtid);
+        store_cs<D>(rv, sm + D * kKP, gtid);
+        if (nt > 1) {
+            load_cs<D, VEC>(kb, S, (tb + 1) * kTok, rk, gtid);
+            load_cs<D, VEC>(vb, S, (tb + 1) * kTok, rv, gtid);
+        }
     }
     __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-        const int s0 = t * kTok;
-        const float* Ks = sm + (t & 1) * (2 * D * kKP);   // [D][kKP]
+    for (int t = 0; t < ntg; ++t) {   // every group runs ntg iterations: the barriers are the whole block's
+      if (t < nt) {
+        const int s0 = (tb + t) * kTok;
+        const float* Ks = sm + (NBUF == 2 ? (t & 1) : 0) * (2 * D * kKP);   // [D][kKP]
         const float* Vs = Ks + D * kKP;                   // [D][kKP]
         // S^T[s][l] for the tile's 64 keys (4 tiles of 16): lane holds keys s0 + 16 st + 4 lg + r of query l; the
         // four key tiles' chains interleaved (each chain still sums jj, i in order)
@@ -239,16 +254,47 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const float* __restrict_
 #pragma unroll
             for (int ct = 0; ct < NJ; ++ct) o[ct] = mma(va[ct].w, p[st][3], o[ct]);
         }
+      }
+        if constexpr (NBUF == 1) __syncthreads();   // every wave is done with the single buffer
         if (t + 1 < nt) {
-            float* nb = sm + ((t + 1) & 1) * (2 * D * kKP);
-            store_cs<D>(rk, nb);
-            store_cs<D>(rv, nb + D * kKP);
+            float* nb = sm + (NBUF == 2 ? ((t + 1) & 1) : 0) * (2 * D * kKP);
+            store_cs<D>(rk, nb, gtid);
+            store_cs<D>(rv, nb + D * kKP, gtid);
             if (t + 2 < nt) {
-                load_cs<D, VEC>(kb, S, (t + 2) * kTok, rk);
-                load_cs<D, VEC>(vb, S, (t + 2) * kTok, rv);
+                load_cs<D, VEC>(kb, S, (tb + t + 2) * kTok, rk, gtid);
+                load_cs<D, VEC>(vb, S, (tb + t + 2) * kTok, rv, gtid);
             }
         }
         __syncthreads();
+    }
+    if constexpr (KH > 1) {
+        // the key groups' (m, l, O) meet in LDS (the K / V buffers are free after the loop's last barrier): groups
+        // 1.. publish theirs, group 0 combines them in group order
+        float* xs = smem_all + (size_t)wave * (KH - 1) * 64 * (4 * NJ + 2);
+        if (kg > 0) {
+            float* my = xs + (size_t)(kg - 1) * 64 * (4 * NJ + 2);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) my[(ct * 4 + r) * 64 + lane] = o[ct][r];
+            my[(4 * NJ) * 64 + lane] = m;
+            my[(4 * NJ + 1) * 64 + lane] = lsum;
+        }
+        __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int g = 1; g < KH; ++g) {
+            const float* ot = xs + (size_t)(g - 1) * 64 * (4 * NJ + 2);
+            const float mg = ot[(4 * NJ) * 64 + lane], lg2 = ot[(4 * NJ + 1) * 64 + lane];
+            const float M = fmaxf(m, mg);
+            const float w0 = m == -INFINITY ? 0.f : expf(m - M), w1 = mg == -INFINITY ? 0.f : expf(mg - M);
+#pragma unroll
+            for (int ct = 0; ct < NJ; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[ct][r] = o[ct][r] * w0 + ot[(ct * 4 + r) * 64 + lane] * w1;
+            lsum = lsum * w0 + lg2 * w1;
+            m = M;
+        }
     }
     if (!lok) return;
     // lane holds O[l][c] for c = 16 ct + 4 lg + r
@@ -488,21 +534,42 @@ static int opt_in_lds(K kernel, size_t bytes) {
     return 0;
 }
 
+// key groups per block (flash_fwd_kernel's KH): 2 where the grid has at most one block per CU and the keys span
+// two tiles or more (LDM_FLASH_KH = 1 / 2 forces it, A/B timing)
+static int flash_kh(int64_t blocks, int ntiles) {
+    static const int forced = [] {
+        const char* e = std::getenv("LDM_FLASH_KH");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced == 1 || forced == 2) return ntiles >= 2 ? forced : 1;
+    return blocks <= 256 && ntiles >= 2 ? 2 : 1;
+}
+
+template <int D, bool TOK, bool LSE, bool VEC, int KH>
+static int fwd_launch_k(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
+                        float scale, hipStream_t st) {
+    constexpr int NBUF = (KH == 2 && D == 128) ? 1 : 2;   // (D = 128 with two groups: one buffer each fits LDS)
+    const size_t lds = (size_t)KH * NBUF * 2 * D * kKP * sizeof(float);
+    static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE, VEC, KH, NBUF>, lds);
+    if (opted) return opted;
+    const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
+    hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, VEC, KH, NBUF>), dim3(grid), dim3(256 * KH), lds, st, q, kv, out,
+                       lse, E, heads, L, S, scale);
+    LDM_CHECK_LAUNCH("flash_fwd_kernel");
+    return 0;
+}
+
 template <int D, bool TOK, bool LSE>
 static int fwd_launch(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
                       float scale, hipStream_t st) {
-    const size_t lds = 4 * (size_t)D * kKP * sizeof(float);   // K and V, two buffers each
-    static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE, true>, lds) | opt_in_lds(flash_fwd_kernel<D, TOK, LSE, false>, lds);
-    if (opted) return opted;
-    const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
-    if (S % 4 == 0)
-        hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, true>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E, heads,
-                           L, S, scale);
-    else
-        hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, false>), dim3(grid), dim3(256), lds, st, q, kv, out, lse, E,
-                           heads, L, S, scale);
-    LDM_CHECK_LAUNCH("flash_fwd_kernel");
-    return 0;
+    const int64_t blocks = (int64_t)B * heads * ((L + kTok - 1) / kTok);
+    const int kh = flash_kh(blocks, (S + kTok - 1) / kTok);
+    if (S % 4 == 0) {
+        if (kh == 2) return fwd_launch_k<D, TOK, LSE, true, 2>(q, kv, out, lse, B, E, heads, L, S, scale, st);
+        return fwd_launch_k<D, TOK, LSE, true, 1>(q, kv, out, lse, B, E, heads, L, S, scale, st);
+    }
+    if (kh == 2) return fwd_launch_k<D, TOK, LSE, false, 2>(q, kv, out, lse, B, E, heads, L, S, scale, st);
+    return fwd_launch_k<D, TOK, LSE, false, 1>(q, kv, out, lse, B, E, heads, L, S, scale, st);
 }
 
 template <int D>

@@ -23,3 +23,20 @@ for r in 1 2; do
 done
 LDM_UCONV_KS3=0x28 timeout -k 10 120 python -u tools/step_times.py --no-loop --layers 3,5 > $OUT/layers_ks3.txt 2>&1 && cat $OUT/layers_ks3.txt
 timeout -k 10 120 python -u tools/step_times.py --no-loop --layers 3,5 > $OUT/layers_base.txt 2>&1 && cat $OUT/layers_base.txt
+# flash attention forward with two key groups per block (LDM_FLASH_KH): parity under both forms, then the stress line
+LDM_FLASH_KH=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_attention_wide.py tests/test_gpu_shape_s.py -q -x \
+    --timeout 240 --timeout-method thread > $OUT/tests_kh1.log 2>&1 || { tail -30 $OUT/tests_kh1.log; exit 1; }
+tail -1 $OUT/tests_kh1.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_attention_wide.py tests/test_gpu_shape_s.py -q -x \
+    --timeout 240 --timeout-method thread > $OUT/tests_kh.log 2>&1 || { tail -30 $OUT/tests_kh.log; exit 1; }
+tail -1 $OUT/tests_kh.log
+for kh in 1 0; do
+  LDM_FLASH_KH=$kh timeout -k 10 300 python -u bench.py --workload stress --steps 3 --warmup 1 --no-cpu-baseline > $OUT/stress_kh$kh.json 2> $OUT/stress.err \
+      || { tail -20 $OUT/stress.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/stress_kh$kh.json')); print('stress kh=$kh', d['us_per_denoise_iteration'], 'us/iter', d['roofline']['avg_launch_us'], d['roofline']['frac'])"
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof_stress -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --workload stress --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof_stress.log 2>&1 \
+    || { echo "rocprof stress failed"; tail $GRAFT_REPO_ROOT/$OUT/prof_stress.log; exit 1; }
+echo done
