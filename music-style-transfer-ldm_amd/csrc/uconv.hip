@@ -891,8 +891,12 @@ static int ks2_mask() {
     return m;
 }
 // K-split form of a layer: 0 none, 1 variant 1 (kKs), 2 variant 2 (kKs2)
-static int ks_form(int layer, int dtype = LDM_DT_F32) {
-    if (layer >= 0 && layer <= 8 && kKs3[layer].wk > 0 && ((ks3_mask() >> layer) & 1)) return 3;
+static bool plane_taps();
+// (variant 3 runs the EPI_PLANE forms only: the canonical 16 x 64 latent, whose enc4 / dec4 planes are 2 x 8)
+static int ks_form(int layer, int dtype = LDM_DT_F32, int H = 16, int W = 64) {
+    if (layer >= 0 && layer <= 8 && kKs3[layer].wk > 0 && ((ks3_mask() >> layer) & 1) && H == 16 && W == 64 &&
+        plane_taps())
+        return 3;
     if (layer < 0 || layer > 8 || !ks_on(layer, dtype)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
 }
@@ -1067,7 +1071,7 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
 
 int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st) {
     using namespace uc;
-    const int ksv = s.ws ? ks_form(layer, s.dtype) : 0;   // without a workspace: the single-block form
+    const int ksv = s.ws ? ks_form(layer, s.dtype, H, W) : 0;   // without a workspace: the single-block form
     UArgs a;
     UC_TRY(make_args(layer, B, H, W, s, ksv, a));
     if (ksv == 3) {
