@@ -815,8 +815,10 @@ constexpr KsGeo kKs2[9] = {
 
 // Variant 3 ("wide", round 6): 16 x 16 tiles with one channel chunk per wave and 16 waves per block (4 per SIMD), so a
 // block keeps 16 x 9 operand loads in flight across four times the waves: enc4 with K in one block (256 tiles, no
-// partial slabs), dec4 with K over 2 blocks (128 tiles; half the slab bytes of variant 2).  Selected by bit l of
-// LDM_UCONV_KS3 (A/B timing; it takes precedence over LDM_UCONV_KS / _KS2 for that layer).
+// partial slabs), dec4 with K over 2 blocks (128 tiles; half the slab bytes of variant 2).  Bit l of LDM_UCONV_KS3
+// (default enc4 + dec4; it takes precedence over LDM_UCONV_KS / _KS2 for that layer).  Measured in the fp32 loop
+// (B = 8, one box, gpurun_out/r6b7): none 75.28, enc4 73.47-73.68, dec4 74.28-74.37, both 72.21-72.69 us per
+// iteration; the fp16 loop 57.97 -> 56.70-57.06.
 constexpr KsGeo kKs3[9] = {
     {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
     {1, 1, 16, 1},   // enc4        256 tiles, K whole
@@ -824,7 +826,7 @@ constexpr KsGeo kKs3[9] = {
     {1, 1, 16, 2},   // dec4        128 tiles x 2
     {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
 };
-constexpr int kKs3Default = 0;
+constexpr int kKs3Default = (1 << 3) | (1 << 5);   // enc4, dec4: loop 75.28 -> 72.21-72.69 us (gpurun_out/r6b7)
 static int ks3_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS3");
@@ -968,7 +970,14 @@ static void ks_tiles(int layer, int B, int H, int W, int64_t& tiles, int64_t& sl
 
 // Split-K workspace of the step kernels at this shape: arrival counters (one int32 per tile, zero between
 // launches) sized for the layer with the most tiles, then the largest layer's partial slabs.
-int step_ks_mask() { return uc::ks_mask(); }
+// the layers on a K-split form (ldm_step_layer_forms): LDM_UCONV_KS's, with the wide variant's layers counted by its
+// own split (enc4's wide form keeps K in one block)
+int step_ks_mask() {
+    int m = uc::ks_mask();
+    for (int l = 0; l < 9; ++l)
+        if (uc::kKs3[l].wk > 0 && ((uc::ks3_mask() >> l) & 1)) m = uc::kKs3[l].ks > 1 ? (m | (1 << l)) : (m & ~(1 << l));
+    return m;
+}
 
 int64_t step_ws_floats(int B, int H, int W, int64_t* cnt_floats) {
     using namespace uc;
