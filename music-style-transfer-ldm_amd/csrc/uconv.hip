@@ -820,11 +820,15 @@ constexpr KsGeo kKs2[9] = {
 // (B = 8, one box, gpurun_out/r6b7): none 75.28, enc4 73.47-73.68, dec4 74.28-74.37, both 72.21-72.69 us per
 // iteration; the fp16 loop 57.97 -> 56.70-57.06.
 constexpr KsGeo kKs3[9] = {
-    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+    {2, 1, 2, 1, 4},   // enc1        32 x 64 tiles (4 wave columns), K (2 channel chunks) over 2 waves: 8 waves
+    {0, 0, 0, 0},
+    {2, 1, 8, 1},    // enc3        32 x 16 tiles, K over 8 waves
     {1, 1, 16, 1},   // enc4        256 tiles, K whole
     {0, 0, 0, 0},
     {1, 1, 16, 2},   // dec4        128 tiles x 2
-    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+    {1, 1, 16, 1},   // dec3        256 tiles, K over 16 waves
+    {1, 2, 8, 1},    // dec2        16 x 32 tiles, K over 8 waves
+    {0, 0, 0, 0},
 };
 constexpr int kKs3Default = (1 << 3) | (1 << 5);   // enc4, dec4: loop 75.28 -> 72.21-72.69 us (gpurun_out/r6b7)
 static int ks3_mask() {
@@ -894,10 +898,12 @@ static int ks2_mask() {
 }
 // K-split form of a layer: 0 none, 1 variant 1 (kKs), 2 variant 2 (kKs2)
 static bool plane_taps();
-// (variant 3 runs the EPI_PLANE forms only: the canonical 16 x 64 latent, whose enc4 / dec4 planes are 2 x 8)
+static bool window_taps();
+// (variant 3 runs at the canonical 16 x 64 latent only: enc4 / dec4 on its 2 x 8 planes (EPI_PLANE), the others on
+// whole rows of their column grids (EPI_WINDOW))
 static int ks_form(int layer, int dtype = LDM_DT_F32, int H = 16, int W = 64) {
     if (layer >= 0 && layer <= 8 && kKs3[layer].wk > 0 && ((ks3_mask() >> layer) & 1) && H == 16 && W == 64 &&
-        plane_taps())
+        (layer == 3 || layer == 5 ? plane_taps() : window_taps()))
         return 3;
     if (layer < 0 || layer > 8 || !ks_on(layer, dtype)) return 0;
     return (kKs2[layer].ks > 1 && ((ks2_mask() >> layer) & 1)) ? 2 : 1;
@@ -1061,7 +1067,7 @@ static int make_args(int layer, int B, int H, int W, const StepConv& s, int ksv,
     a.fd_mt = FastDiv::make(a.nMt);
     a.fd_nt = FastDiv::make(a.nNt);
     a.fd_tiles = FastDiv::make(a.nMt * a.nNt);
-    if (ksv) {
+    if (ksv && (ksv == 3 ? kKs3[layer] : (ksv == 2 ? kKs2[layer] : kKs[layer])).ks > 1) {
         int64_t cnt = 0;
         const int64_t wsf = step_ws_floats(B, H, W, &cnt);
         int64_t tiles, sf;
@@ -1084,7 +1090,16 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
     UArgs a;
     UC_TRY(make_args(layer, B, H, W, s, ksv, a));
     if (ksv == 3) {
+        const bool win = window_taps();
         switch (layer) {
+            case 0: LDM_REQUIRE(s.y && win && a.Wq % 64 == 0, "enc1 (variant 3): y, 64-column rows");
+                return launch<0, 32, 64, 2, 1, 4, 2, 9, 9, EPI_RELU | EPI_WINDOW, 1>(a, s.dtype, st);
+            case 2: LDM_REQUIRE(s.y && win && a.Wq % 16 == 0, "enc3 (variant 3): y, 16-column rows");
+                return launch<1, 128, 256, 2, 1, 1, 8, 9, 9, EPI_RELU | EPI_WINDOW, 1>(a, s.dtype, st);
+            case 6: LDM_REQUIRE(s.y && s.skip && win && a.Wq % 16 == 0, "dec3 (variant 3): y, skip, 16-column rows");
+                return launch<2, 256, 128, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_SKIP | EPI_WINDOW, 1>(a, s.dtype, st);
+            case 7: LDM_REQUIRE(s.y && s.skip && win && a.Wq % 32 == 0, "dec2 (variant 3): y, skip, 32-column rows");
+                return launch<2, 128, 64, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_SKIP | EPI_WINDOW, 1>(a, s.dtype, st);
             case 3: LDM_REQUIRE(s.y && a.Hin == 4 && a.Win == 16 && plane_taps(), "enc4 (variant 3): y, 4 x 16 input plane");
                 return launch<1, 256, 512, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 1>(a, s.dtype, st);
             case 5: LDM_REQUIRE(s.y && s.skip && a.Hin == 2 && a.Win == 8 && plane_taps(), "dec4 (variant 3): y, skip, 2 x 8 plane");
