@@ -816,9 +816,11 @@ constexpr KsGeo kKs2[9] = {
 // Variant 3 ("wide", round 6): 16 x 16 tiles with one channel chunk per wave and 16 waves per block (4 per SIMD), so a
 // block keeps 16 x 9 operand loads in flight across four times the waves: enc4 with K in one block (256 tiles, no
 // partial slabs), dec4 with K over 2 blocks (128 tiles; half the slab bytes of variant 2).  Bit l of LDM_UCONV_KS3
-// (default enc4 + dec4; it takes precedence over LDM_UCONV_KS / _KS2 for that layer).  Measured in the fp32 loop
-// (B = 8, one box, gpurun_out/r6b7): none 75.28, enc4 73.47-73.68, dec4 74.28-74.37, both 72.21-72.69 us per
-// iteration; the fp16 loop 57.97 -> 56.70-57.06.
+// (default 0xED: every layer that has one; it takes precedence over LDM_UCONV_KS / _KS2 for that layer).  Measured
+// in the fp32 loop (B = 8, one box each): none 75.28, enc4 73.47-73.68, dec4 74.28-74.37, both 72.21-72.69 us per
+// iteration (gpurun_out/r6b7); then on another box from enc4 + dec4 (72.15-72.39): + enc1 71.59-71.74, + enc3
+// 71.41-71.71, + dec3 71.44-71.56, + dec2 72.34-72.50, all six 70.12-70.18 (gpurun_out/r6b8); the fp16 loop
+// 57.97 -> 56.70-57.06 with enc4 + dec4, unchanged by the other four.
 constexpr KsGeo kKs3[9] = {
     {2, 1, 2, 1, 4},   // enc1        32 x 64 tiles (4 wave columns), K (2 channel chunks) over 2 waves: 8 waves
     {0, 0, 0, 0},
@@ -830,7 +832,7 @@ constexpr KsGeo kKs3[9] = {
     {1, 2, 8, 1},    // dec2        16 x 32 tiles, K over 8 waves
     {0, 0, 0, 0},
 };
-constexpr int kKs3Default = (1 << 3) | (1 << 5);   // enc4, dec4: loop 75.28 -> 72.21-72.69 us (gpurun_out/r6b7)
+constexpr int kKs3Default = 0xED;   // enc1, enc3, enc4, dec4, dec3, dec2 (gpurun_out/r6b7, r6b8)
 static int ks3_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS3");
