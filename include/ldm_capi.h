@@ -413,6 +413,20 @@ int64_t ldm_conv_wgrad_workspace_floats(const ldm_conv_desc* d);
  * shapes it does not cover run the fp32 kernel). */
 int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                 int32_t accumulate, float* workspace, int32_t dtype, void* stream);
+/* ldm_conv_backward_weight_dt with a tap-shared gradient's split-K reduction deferred (the train step's weight
+ * gradients are read only by the optimizer): the partials stay in `workspace` (ldm_conv_wgrad_workspace_floats,
+ * kept until the reduction) and *splits_out receives their count S (0: nothing deferred, dw written).
+ * ldm_wgrad_reduce_many then reduces every job in one launch per 24 jobs, bitwise ldm_conv_backward_weight_dt's
+ * result (MN = the gradient's element count, a multiple of 4; partial and dw 16-byte aligned). */
+int ldm_conv_backward_weight_defer(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                   int32_t accumulate, float* workspace, int32_t dtype, int32_t* splits_out,
+                                   void* stream);
+typedef struct ldm_wgrad_red_job {
+    const float* partial;   /* [S][MN] */
+    float* dw;              /* [MN] */
+    int32_t S, MN, accumulate;
+} ldm_wgrad_red_job;
+int ldm_wgrad_reduce_many(const ldm_wgrad_red_job* jobs, int32_t n, void* stream);
 /* The 16-bit storage flags (LDM_DT_X16 | LDM_DT_DY16) ldm_conv_backward_weight_dt takes for d at a 16-bit
  * operand precision (0: neither; the caller then passes fp32 tensors). */
 int32_t ldm_conv_wgrad_storage16(const ldm_conv_desc* d);

@@ -136,12 +136,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // The same sums on 16-byte pieces (round 6): a thread owns four consecutive outputs, each summed in the order
 // above, so a wave-load moves 1 KB instead of 256 B (the partials of the train step's layers are ~38 MB per
 // layer: the scalar form read them at ~4.5 TB/s).  G comes from the piece count, ~2^18 threads as before.
-__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const floatx4* __restrict__ partial, int S, int MN4,
-                                                            floatx4* __restrict__ dw, int accumulate, int G) {
+__device__ __forceinline__ void wgrad_reduce4_body(const floatx4* __restrict__ partial, int S, int MN4,
+                                                   floatx4* __restrict__ dw, int accumulate, int G, int blk) {
     __shared__ floatx4 red[256];
     const int NO = 256 / G;
     const int ol = threadIdx.x % NO, g = threadIdx.x / NO;
-    const int i = blockIdx.x * NO + ol;
+    const int i = blk * NO + ol;
     const int per = (S + G - 1) / G;
     floatx4 v = {0.f, 0.f, 0.f, 0.f};
     if (i < MN4) {
@@ -166,6 +166,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const floatx4* __res
         v = red[ol];
     }
     if (g == 0 && i < MN4) dw[i] = accumulate ? dw[i] + v : v;
+}
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const floatx4* __restrict__ partial, int S, int MN4,
+                                                            floatx4* __restrict__ dw, int accumulate, int G) {
+    wgrad_reduce4_body(partial, S, MN4, dw, accumulate, G, blockIdx.x);
+}
+
+// The split-K reductions of several weight gradients in one launch (ldm_wgrad_reduce_many): the train step's weight
+// gradients are read only by the optimizer, so their reductions can wait for the end of the backward and go as one
+// launch.  Block -> (job, block of the job) by the jobs' first blocks b0; each job's blocks run wgrad_reduce4_kernel's
+// code with its G, so the same bits.
+struct RedJob {
+    const floatx4* partial;
+    floatx4* dw;
+    int32_t S, MN4, accumulate, G, b0;
+};
+constexpr int kMaxRedJobs = 24;
+struct RedJobs {
+    RedJob j[kMaxRedJobs];
+    int32_t n;
+};
+__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(RedJobs jobs) {
+    int k = 0;
+    while (k + 1 < jobs.n && (int)blockIdx.x >= jobs.j[k + 1].b0) ++k;
+    const RedJob& J = jobs.j[k];
+    wgrad_reduce4_body(J.partial, J.S, J.MN4, J.dw, J.accumulate, J.G, (int)blockIdx.x - J.b0);
 }
 static void wgrad_reduce(const float* partial, int S, int MN, float* dw, int accumulate, hipStream_t st) {
     static const bool vec = [] {   // LDM_WGRAD_REDUCE4=0: the scalar form (A/B timing)
@@ -685,8 +710,51 @@ extern "C" int ldm_conv_backward_weight(const ldm_conv_desc* d, const float* x, 
     return ldm_conv_backward_weight_dt(d, x, dy, dw, accumulate, workspace, LDM_DT_F32, stream);
 }
 
+static int conv_backward_weight_impl(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                     int32_t accumulate, float* workspace, int32_t dtype, int32_t* defer_s, void* stream);
+
 extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
                                            int32_t accumulate, float* workspace, int32_t dtype, void* stream) {
+    return conv_backward_weight_impl(d, x, dy, dw, accumulate, workspace, dtype, nullptr, stream);
+}
+
+extern "C" int ldm_conv_backward_weight_defer(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                              int32_t accumulate, float* workspace, int32_t dtype, int32_t* splits_out,
+                                              void* stream) {
+    LDM_REQUIRE(splits_out, "wgrad_defer: bad argument");
+    return conv_backward_weight_impl(d, x, dy, dw, accumulate, workspace, dtype, splits_out, stream);
+}
+
+extern "C" int ldm_wgrad_reduce_many(const ldm_wgrad_red_job* jobs, int32_t n, void* stream) {
+    LDM_REQUIRE(jobs && n >= 0, "wgrad_reduce_many: bad argument");
+    hipStream_t st = (hipStream_t)stream;
+    for (int i0 = 0; i0 < n; i0 += kMaxRedJobs) {
+        RedJobs rj{};
+        int blocks = 0;
+        rj.n = n - i0 < kMaxRedJobs ? n - i0 : kMaxRedJobs;
+        for (int i = 0; i < rj.n; ++i) {
+            const ldm_wgrad_red_job& J = jobs[i0 + i];
+            LDM_REQUIRE(J.partial && J.dw && J.S > 0 && J.MN > 0 && J.MN % 4 == 0 &&
+                            (((uintptr_t)J.partial | (uintptr_t)J.dw) & 15) == 0,
+                        "wgrad_reduce_many: bad job");
+            const int MN4 = J.MN / 4, G = wgrad_groups(J.S, MN4), NO = 256 / G;
+            rj.j[i] = RedJob{reinterpret_cast<const floatx4*>(J.partial), reinterpret_cast<floatx4*>(J.dw), J.S, MN4,
+                             J.accumulate, G, blocks};
+            blocks += (MN4 + NO - 1) / NO;
+        }
+        if (blocks == 0) continue;
+        hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3(blocks), dim3(256), 0, st, rj);
+        LDM_CHECK_LAUNCH("wgrad_reduce_many_kernel");
+    }
+    return 0;
+}
+
+// defer_s != NULL: a tap-shared gradient split over S > 1 K ranges leaves its partials in `workspace` and *defer_s = S
+// (the caller reduces them later with ldm_wgrad_reduce_many); any other form runs as ldm_conv_backward_weight_dt and
+// *defer_s = 0
+static int conv_backward_weight_impl(const ldm_conv_desc* d, const float* x, const float* dy, float* dw,
+                                     int32_t accumulate, float* workspace, int32_t dtype, int32_t* defer_s, void* stream) {
+    if (defer_s) *defer_s = 0;
     LDM_REQUIRE(d && x && dy && dw && workspace, "wgrad: null argument");
     const int st16 = dtype & (LDM_DT_X16 | LDM_DT_DY16);
     dtype &= ~(LDM_DT_X16 | LDM_DT_DY16);
@@ -726,6 +794,10 @@ extern "C" int ldm_conv_backward_weight_dt(const ldm_conv_desc* d, const float* 
     if (rc > 0) return rc;
     LDM_REQUIRE(rc == 0 || !st16, "wgrad: 16-bit storage on a layer without the tap-shared form (ldm_conv_wgrad_storage16)");
     if (rc == 0 && S2 == 0) return 0;   // one K range, written to dw by the kernel
+    if (rc == 0 && defer_s && MN % 4 == 0 && (((uintptr_t)workspace | (uintptr_t)dw) & 15) == 0) {
+        *defer_s = S2;
+        return 0;
+    }
     if (rc == 0) {
         wgrad_reduce((const float*)workspace, S2, MN, dw, accumulate, st);
         LDM_CHECK_LAUNCH("wgrad_reduce_kernel");

@@ -50,6 +50,11 @@ class ActFinJob(ctypes.Structure):
     _fields_ = [("part", c_fp), ("dbias", c_fp), ("B", c_int32), ("C", c_int32), ("Q", c_int32), ("kind", c_int32)]
 
 
+class WgradRedJob(ctypes.Structure):
+    """ldm_wgrad_red_job: one deferred weight-gradient reduction (ldm_conv_backward_weight_defer)."""
+    _fields_ = [("partial", c_fp), ("dw", c_fp), ("S", c_int32), ("MN", c_int32), ("accumulate", c_int32)]
+
+
 class UNetShape(ctypes.Structure):
     _fields_ = [("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32), ("nf", c_int32)]
 
@@ -180,6 +185,8 @@ SIGNATURES = {
     "ldm_batchnorm_backward_dxsum_defer": (c_int32, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int32, c_int32, c_int32,
                                                      c_int32, c_fp, c_fp, c_fp, c_fp, c_vp, c_vp, c_fp, c_vp]),
     "ldm_bn_dxsum_partial_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "ldm_conv_backward_weight_defer": (c_int32, [c_vp, c_fp, c_fp, c_fp, c_int32, c_fp, c_int32, c_vp, c_vp]),
+    "ldm_wgrad_reduce_many": (c_int32, [c_vp, c_int32, c_vp]),
     "ldm_act_finalize_many": (c_int32, [c_vp, c_int32, c_vp]),
     "ldm_act_backward": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_int32, c_int32, c_int32, c_fp, c_fp, c_fp, c_fp,
                                    c_vp]),

@@ -514,9 +514,19 @@ def conv_backward_weight(x, dy, desc, dw=None, accumulate=False, dtype=0):
         shape = (desc.Cout, desc.Cin, desc.kh, desc.kw)
     if dw is None:
         dw = torch.empty(shape, device=x.device, dtype=torch.float32)
-    ws = scratch("wgrad", L.load().ldm_conv_wgrad_workspace_floats(byref(desc)), x.device)
+    nws = int(L.load().ldm_conv_wgrad_workspace_floats(byref(desc)))
+    code = dtype | (L.DT_X16 if xh else 0) | (L.DT_DY16 if dyh else 0)
+    if _BIAS_DEFER:   # the split-K reduction waits for the end of the backward (bias_grads_deferred)
+        part = _defer_part(nws, x.device)
+        S = ctypes.c_int32(0)
+        L.call("ldm_conv_backward_weight_defer", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+               int(accumulate), ctypes.c_void_p(part), code, ctypes.byref(S), stream_handle())
+        if S.value > 0:
+            _BIAS_DEFER[-1].append(L.WgradRedJob(part, dw.data_ptr(), S.value, dw.numel(), int(accumulate)))
+        return dw
+    ws = scratch("wgrad", nws, x.device)
     L.call("ldm_conv_backward_weight_dt", byref(desc), x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate),
-           ws.data_ptr(), dtype | (L.DT_X16 if xh else 0) | (L.DT_DY16 if dyh else 0), stream_handle())
+           ws.data_ptr(), code, stream_handle())
     return dw
 
 
@@ -582,7 +592,8 @@ def _defer_part(nfloats, device):
 class bias_grads_deferred:
     """with bias_grads_deferred(): loss.backward() -- the convs' bias gradients (ldm_act_backward's per-channel sums,
     and the BatchNorm dx sums that stand for them, batchnorm_backward(dx_sum=True)) are finalized at the end of the
-    block, one launch for all of them (ldm_act_finalize_many), on the current stream
+    block, one launch for all of them (ldm_act_finalize_many), and so are the weight gradients' split-K reductions
+    (conv_backward_weight: ldm_wgrad_reduce_many), on the current stream
     (which the autograd engine has synchronised with the backward's leaf streams by then).  Only where nothing reads a
     bias gradient before the block ends: LDMTrainer's step without a gradient all-reduce (its post-accumulate hooks
     would read it early).  Bitwise the immediate finalize."""
@@ -602,8 +613,14 @@ class bias_grads_deferred:
             return False
         jobs = _BIAS_DEFER.pop()
         if jobs and exc[0] is None:
-            arr = (L.ActFinJob * len(jobs))(*jobs)
-            L.call("ldm_act_finalize_many", ctypes.cast(arr, ctypes.c_void_p), len(jobs), stream_handle())
+            red = [j for j in jobs if isinstance(j, L.WgradRedJob)]
+            fin = [j for j in jobs if isinstance(j, L.ActFinJob)]
+            if red:
+                arr = (L.WgradRedJob * len(red))(*red)
+                L.call("ldm_wgrad_reduce_many", ctypes.cast(arr, ctypes.c_void_p), len(red), stream_handle())
+            if fin:
+                arr = (L.ActFinJob * len(fin))(*fin)
+                L.call("ldm_act_finalize_many", ctypes.cast(arr, ctypes.c_void_p), len(fin), stream_handle())
         return False
 
 

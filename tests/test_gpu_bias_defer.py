@@ -82,3 +82,26 @@ def test_finalize_many_equals_immediate(cuda):
     torch.cuda.synchronize()
     for i, (x, y) in enumerate(zip(imm, dfr)):
         assert torch.equal(x, y), (i, cases[i])
+
+
+@pytest.mark.parametrize("dtype", [0, 2])
+def test_wgrad_reduce_many_equals_immediate(cuda, dtype):
+    """ldm_conv_backward_weight_defer + ldm_wgrad_reduce_many (inside bias_grads_deferred) == ldm_conv_backward_weight_dt
+    bitwise, over conv / convT weight gradients that split K (the train step's classes), more jobs than one launch."""
+    from ldm_amd import ops
+    descs = [ops.make_desc(8, 64, 64, 256, 128, 3, 3, 2, 1), ops.make_desc(8, 128, 32, 128, 256, 3, 3, 2, 1),
+             ops.make_desc(8, 128, 16, 64, 64, 3, 3, 2, 1, 1, True), ops.make_desc(8, 256, 8, 32, 256, 3, 3, 1, 1),
+             ops.make_desc(8, 64, 16, 64, 32, 3, 3, 1, 1)] * 6
+    g = torch.Generator().manual_seed(9)
+    data = []
+    for d in descs:
+        x = torch.randn(d.B, d.Cin, d.Hin, d.Win, generator=g).to(cuda)
+        dy = torch.randn(d.B, d.Cout, d.Hout, d.Wout, generator=g).to(cuda)
+        data.append((x, dy))
+    with torch.no_grad():
+        imm = [ops.conv_backward_weight(x, dy, d, dtype=dtype).clone() for d, (x, dy) in zip(descs, data)]
+        with ops.bias_grads_deferred():
+            dfr = [ops.conv_backward_weight(x, dy, d, dtype=dtype) for d, (x, dy) in zip(descs, data)]
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(imm, dfr)):
+        assert torch.equal(a, b), i
