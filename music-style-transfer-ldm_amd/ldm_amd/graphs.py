@@ -44,10 +44,30 @@ def capture_mode():
 _CAPTURES = []   # per capture in progress: (origin stream, set of pool streams that joined it)
 
 
+def quiesce_collectives():
+    """Before a capture: wait until the default process group's watchdog has retired every eager collective still
+    on its work list (ProcessGroup._wait_for_pending_works; a no-op without an initialised group or for a backend
+    without it).  A capture that started while the list still held eager works could have the watchdog query their
+    events inside the capture window: round 3's abort, and in round 6 an abort in capture_end once the train step
+    stopped waiting on the host every step (its eager warm-up steps' all-reduces reached the capture sooner)."""
+    try:
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        dist.distributed_c10d._get_default_group()._wait_for_pending_works()
+    except Exception:
+        pass
+
+
 @contextlib.contextmanager
 def capture(graph, stream=None, pool=None):
     """Context manager: capture into `graph` (torch.cuda.CUDAGraph) on `stream` (capture_mode()).  Before the
-    capture ends, the origin stream waits on every branch stream that forked from it during the capture."""
+    capture ends, the origin stream waits on every branch stream that forked from it during the capture.  Before it
+    starts, the device is synchronised and the process group's pending eager collectives retired
+    (quiesce_collectives)."""
+    if not _CAPTURES:
+        torch.cuda.synchronize()
+        quiesce_collectives()
     with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode=capture_mode()):
         origin = torch.cuda.current_stream()
         rec = (origin, {})
