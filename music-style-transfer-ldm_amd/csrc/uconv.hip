@@ -830,7 +830,7 @@ constexpr KsGeo kKs3[9] = {
     {1, 1, 16, 2},   // dec4        128 tiles x 2
     {1, 1, 16, 1},   // dec3        256 tiles, K over 16 waves
     {1, 2, 8, 1},    // dec2        16 x 32 tiles, K over 8 waves
-    {0, 0, 0, 0},
+    {1, 2, 4, 1, 2}, // dec1 + DDIM 16 x 64 tiles (2 wave columns), K over 4 waves: 8 waves
 };
 constexpr int kKs3Default = 0xED;   // enc1, enc3, enc4, dec4, dec3, dec2 (gpurun_out/r6b7, r6b8)
 static int ks3_mask() {
@@ -1102,6 +1102,8 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
                 return launch<2, 256, 128, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_SKIP | EPI_WINDOW, 1>(a, s.dtype, st);
             case 7: LDM_REQUIRE(s.y && s.skip && win && a.Wq % 32 == 0, "dec2 (variant 3): y, skip, 32-column rows");
                 return launch<2, 128, 64, 1, 2, 1, 8, 9, 9, EPI_RELU | EPI_SKIP | EPI_WINDOW, 1>(a, s.dtype, st);
+            case 8: LDM_REQUIRE(s.xs && s.coef && win && a.Wq % 64 == 0, "dec1 (variant 3): sampler state, 64-column rows");
+                return launch<0, 64, 32, 1, 2, 2, 4, 9, 9, EPI_DDIM | EPI_WINDOW, 1>(a, s.dtype, st);
             case 3: LDM_REQUIRE(s.y && a.Hin == 4 && a.Win == 16 && plane_taps(), "enc4 (variant 3): y, 4 x 16 input plane");
                 return launch<1, 256, 512, 1, 1, 1, 16, 9, 9, EPI_RELU | EPI_POSB | EPI_PLANE, 1>(a, s.dtype, st);
             case 5: LDM_REQUIRE(s.y && s.skip && a.Hin == 2 && a.Win == 8 && plane_taps(), "dec4 (variant 3): y, skip, 2 x 8 plane");
