@@ -820,7 +820,8 @@ constexpr KsGeo kKs2[9] = {
 // in the fp32 loop (B = 8, one box each): none 75.28, enc4 73.47-73.68, dec4 74.28-74.37, both 72.21-72.69 us per
 // iteration (gpurun_out/r6b7); then on another box from enc4 + dec4 (72.15-72.39): + enc1 71.59-71.74, + enc3
 // 71.41-71.71, + dec3 71.44-71.56, + dec2 72.34-72.50, all six 70.12-70.18 (gpurun_out/r6b8); the fp16 loop
-// 57.97 -> 56.70-57.06 with enc4 + dec4, unchanged by the other four.
+// 57.97 -> 56.70-57.06 with enc4 + dec4, unchanged by the other four; + dec1 with its DDIM update 70.30-70.44 ->
+// 69.72-69.87, fp16 55.50-55.73 -> 55.19-55.23 (gpurun_out/r6b9).
 constexpr KsGeo kKs3[9] = {
     {2, 1, 2, 1, 4},   // enc1        32 x 64 tiles (4 wave columns), K (2 channel chunks) over 2 waves: 8 waves
     {0, 0, 0, 0},
@@ -832,7 +833,7 @@ constexpr KsGeo kKs3[9] = {
     {1, 2, 8, 1},    // dec2        16 x 32 tiles, K over 8 waves
     {1, 2, 4, 1, 2}, // dec1 + DDIM 16 x 64 tiles (2 wave columns), K over 4 waves: 8 waves
 };
-constexpr int kKs3Default = 0xED;   // enc1, enc3, enc4, dec4, dec3, dec2 (gpurun_out/r6b7, r6b8)
+constexpr int kKs3Default = 0x1ED;   // enc1, enc3, enc4, dec4, dec3, dec2, dec1 (gpurun_out/r6b7, r6b8, r6b9)
 static int ks3_mask() {
     static const int m = [] {
         const char* e = std::getenv("LDM_UCONV_KS3");
