@@ -824,7 +824,7 @@ constexpr KsGeo kKs2[9] = {
 // 69.72-69.87, fp16 55.50-55.73 -> 55.19-55.23 (gpurun_out/r6b9).
 constexpr KsGeo kKs3[9] = {
     {2, 1, 2, 1, 4},   // enc1        32 x 64 tiles (4 wave columns), K (2 channel chunks) over 2 waves: 8 waves
-    {0, 0, 0, 0},
+    {2, 1, 4, 1, 2},   // enc2        32 x 32 tiles (2 wave columns of 16), K over 4 waves: 8 waves
     {2, 1, 8, 1},    // enc3        32 x 16 tiles, K over 8 waves
     {1, 1, 16, 1},   // enc4        256 tiles, K whole
     {0, 0, 0, 0},
@@ -1097,6 +1097,8 @@ int step_conv(int layer, int B, int H, int W, const StepConv& s, hipStream_t st)
         switch (layer) {
             case 0: LDM_REQUIRE(s.y && win && a.Wq % 64 == 0, "enc1 (variant 3): y, 64-column rows");
                 return launch<0, 32, 64, 2, 1, 4, 2, 9, 9, EPI_RELU | EPI_WINDOW, 1>(a, s.dtype, st);
+            case 1: LDM_REQUIRE(s.y && s.bcast && win && a.Wq % 32 == 0, "enc2 (variant 3): y, t_emb, 32-column rows");
+                return launch<1, 64, 128, 2, 1, 2, 4, 9, 9, EPI_RELU | EPI_BCAST | EPI_WINDOW, 1>(a, s.dtype, st);
             case 2: LDM_REQUIRE(s.y && win && a.Wq % 16 == 0, "enc3 (variant 3): y, 16-column rows");
                 return launch<1, 128, 256, 2, 1, 1, 8, 9, 9, EPI_RELU | EPI_WINDOW, 1>(a, s.dtype, st);
             case 6: LDM_REQUIRE(s.y && s.skip && win && a.Wq % 16 == 0, "dec3 (variant 3): y, skip, 16-column rows");
