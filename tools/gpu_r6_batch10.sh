@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 6, batch 9: the wide form of enc2 (uconv.hip kKs3 bit 1): parity (step kernels,
+# Round 6, batch 10: the wide form of enc2 (uconv.hip kKs3 bit 1): parity (step kernels,
 # bench config, the step loop against the general loop) under LDM_UCONV_KS3=0x1EF, then the fp32 / fp16 loops against
-# the default 0x1ED, twice around.   bash tools/gpu_r6_batch9.sh <tag>
+# the default 0x1ED, twice around.   bash tools/gpu_r6_batch10.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-r6b10}; OUT=gpurun_out/$T; mkdir -p $OUT
