@@ -227,6 +227,10 @@ int32_t ldm_ca1_probs_form(void);
 /* A/B switch of the Cin = 1 stride-2 conv's packed form (two output channels per v_pk_fma_f32; bitwise the scalar
  * form's results): 1 on, 0 off; returns the previous setting.  Default: LDM_CIN1_PK. */
 int ldm_set_cin1_packed(int on);
+/* A/B switch of the Cin = 1 k3 stride-1 conv's four-column form (conv_cin1_x4_kernel, SD = 1: the UNet's first layer on
+ * the raw mel, UNet(1, 1) at shape S; models/model.py:178 Conv2d(in_channels, num_filters, 3, 1, 1)) against the one-lane-per-pixel
+ * kernel, bitwise the same results: 1 on, 0 off; returns the previous setting.  Default: LDM_CIN1_S1. */
+int ldm_set_cin1_s1(int on);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that

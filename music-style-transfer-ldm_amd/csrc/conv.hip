@@ -937,16 +937,17 @@ __device__ __forceinline__ void store4(const ConvArgs& a, size_t o, const float 
     }
 }
 
-// Cin = 1, stride 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
-// 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (6 + K) input window in registers,
-// every output channel from it, weights in LDS.
+// Cin = 1, stride SD = 2, k x k (the VAE / style encoders' first layers, and the data gradient of the decoder's
+// 64 -> 1 output layer): lane = (b, oy, 4 output columns), its K x (3 SD + K) input window in registers,
+// every output channel from it, weights in LDS.  SD = 1 (round 6): the UNet's first layer on the raw mel
+// (shape S, UNet(1, 1): 1 -> 32, k3 s1 on 128 x 512), which ran on conv_cin1_kernel (one lane per pixel).
 // PK = 1 (round 6): two output channels per packed FMA.  v_pk_fma_f32 computes each half exactly as v_fma_f32
 // does, so each output's chain fma(x, w, acc) over (ky, kx) is the scalar form's, bit for bit; the halves are
 // channels co and co + 1 (their weights one aligned 8-byte LDS read from a [tap][channel] copy), the input value
 // the same register for both (op_sel).  Round 5's packed attempt paired the FOUR OUTPUT COLUMNS instead; the
 // columns' inputs win[ky][kx + 2j] are not register pairs, and that variant failed the config-3 parity bound —
 // which fma rounding cannot explain.
-template <int K, int LP, int RO, int YS, int PK = 0>
+template <int K, int LP, int RO, int YS, int PK = 0, int SD = 2>
 __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     __shared__ float ws[64 * K * K];
     __shared__ __attribute__((aligned(8))) float wt[PK ? K * K * 64 : 1];   // PK: [ky*K + kx][co]
@@ -965,9 +966,9 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
     const int ox0 = (idx - r * W4) * 4;
     const int b = a.fd_dho.div(r);
     const int oy = r - b * a.Hout;
-    constexpr int NC = 6 + K;
+    constexpr int NC = 3 * SD + K;
     const int pad = -a.pt.dy[0][0];
-    const int iy0 = 2 * oy - pad, ix0 = 2 * ox0 - pad;
+    const int iy0 = SD * oy - pad, ix0 = SD * ox0 - pad;
     const float* xb = a.x + (size_t)b * a.Hin * a.Win;
     float win[K][NC];
 #pragma unroll
@@ -981,11 +982,14 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
             win[ky][c] = round16(ok ? xb[iy * a.Win + ix] : 0.f, LP);
         }
     }
+    // the output channels [c0, c1) of this block (gridDim.y > 1 splits them when the pixel grid alone is under
+    // a block per CU: B = 1 at shape S; the host keeps Cout / gridDim.y even)
+    const int cpb = a.Cout / (int)gridDim.y, c0 = (int)blockIdx.y * cpb, c1 = c0 + cpb;
     const size_t plane = (size_t)a.Hout * a.Wout;
-    size_t o = ((size_t)b * a.Cout * a.Hout + oy) * a.Wout + ox0;
+    size_t o = (((size_t)b * a.Cout + c0) * a.Hout + oy) * a.Wout + ox0;
     if constexpr (PK != 0) {   // (the host takes this form for an even Cout only)
         typedef float f2 __attribute__((ext_vector_type(2)));
-        for (int co = 0; co < a.Cout; co += 2, o += 2 * plane) {
+        for (int co = c0; co < c1; co += 2, o += 2 * plane) {
             f2 acc[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
@@ -994,7 +998,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
                     const f2 w2 = *reinterpret_cast<const f2*>(wt + (ky * K + kx) * 64 + co);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const float xv = win[ky][kx + 2 * j];
+                        const float xv = win[ky][kx + SD * j];
                         acc[j] = __builtin_elementwise_fma(f2{xv, xv}, w2, acc[j]);
                     }
                 }
@@ -1009,7 +1013,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
         }
         return;
     }
-    for (int co = 0; co < a.Cout; ++co, o += plane) {
+    for (int co = c0; co < c1; ++co, o += plane) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ky = 0; ky < K; ++ky)
@@ -1017,7 +1021,7 @@ __global__ __launch_bounds__(256) void conv_cin1_x4_kernel(ConvArgs a) {
             for (int kx = 0; kx < K; ++kx) {
                 const float w = ws[co * K * K + ky * K + kx];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = fmaf(win[ky][kx + 2 * j], w, acc[j]);
+                for (int j = 0; j < 4; ++j) acc[j] = fmaf(win[ky][kx + SD * j], w, acc[j]);
             }
         const ChanEpi ce = es[co];
         float v[4];
@@ -1042,6 +1046,14 @@ static int g_cin1_packed = [] {
     const char* e = std::getenv("LDM_CIN1_PK");
     return e ? std::atoi(e) : 1;
 }();
+
+// conv_cin1_x4_kernel's stride-1 form for the k3 Cin = 1 convs (LDM_CIN1_S1=0 or ldm_set_cin1_s1(0):
+// conv_cin1_kernel, for A/B timing and the bitwise test)
+static int g_cin1_s1 = [] {
+    const char* e = std::getenv("LDM_CIN1_S1");
+    return e ? std::atoi(e) : 1;
+}();
+static bool cin1_s1_on() { return g_cin1_s1 != 0; }
 
 // ConvTranspose2d(Cin -> 1, k4, s2, p1) (the decoder's output layer): lane = (b, qy, 4 input columns
 // qx0..qx0+3) -> the 2 x 8 outputs they feed (all four parities); per input channel a 3 x 6 window.
@@ -1649,19 +1661,27 @@ int conv_forward_ex(const ldm_conv_desc& d, const ldm_conv_plan& p, const float*
         a.fd_dho = FastDiv::make(d.Hout);
         a.fd_dco = FastDiv::make(d.Cout);
         const bool simple_epi = !ep.pos_bias && !ep.bcast && !ep.skip && !ep.ddim_coef && y;
-        if (simple_epi && d.Cin == 1 && !d.transposed && d.Cout <= 64 && d.kh == d.kw && (d.kh == 3 || d.kh == 4) &&
-            d.stride == 2 && d.Wout % 4 == 0 && a.pt.dy[0][0] == -d.pad && a.pt.dx[0][0] == -d.pad &&
+        if (simple_epi && d.Cin == 1 && !d.transposed && d.Cout <= 64 && d.kh == d.kw &&
+            ((d.stride == 2 && (d.kh == 3 || d.kh == 4)) || (d.stride == 1 && d.kh == 3 && cin1_s1_on())) && d.Wout % 4 == 0 && a.pt.dy[0][0] == -d.pad && a.pt.dx[0][0] == -d.pad &&
             ((uintptr_t)y & 15) == 0 && (!ep.act_out || ((uintptr_t)ep.act_out & 15) == 0)) {
             a.fd_dwo = FastDiv::make(d.Wout / 4);
             const int64_t lanes = (int64_t)d.B * d.Hout * (d.Wout / 4);
             LDM_REQUIRE(!ep.x16, "conv: the Cin = 1 kernel reads fp32 inputs only");
             const bool pk = g_cin1_packed != 0 && d.Cout % 2 == 0;
+            // under 512 pixel blocks (B = 1 at shape S: 64): split the output channels over grid.y
+            // (each split re-reads its lanes' windows; the arithmetic per output is unchanged)
+            const int64_t pblocks = (lanes + 255) / 256;
+            int csplit = 1;
+            while (pblocks * csplit < 512 && d.Cout % (csplit * 4) == 0 && d.Cout / (csplit * 2) >= 4) csplit *= 2;
             lp_dispatch(a.ep, [&](auto lp, auto ro) {
                 constexpr int LP = decltype(lp)::value, RO = decltype(ro)::value;
-                const dim3 g((unsigned)((lanes + 255) / 256));
+                const dim3 g((unsigned)pblocks, (unsigned)csplit);
                 auto go = [&](auto pkc) {
                     constexpr int PK = decltype(pkc)::value;
-                    if (LP != 0 && ep.y16) {
+                    if (d.stride == 1) {
+                        if (LP != 0 && ep.y16) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, LP, PK, 1>), g, dim3(256), 0, st, a);
+                        else hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, 0, PK, 1>), g, dim3(256), 0, st, a);
+                    } else if (LP != 0 && ep.y16) {
                         if (d.kh == 3) hipLaunchKernelGGL((conv_cin1_x4_kernel<3, LP, RO, LP, PK>), g, dim3(256), 0, st, a);
                         else hipLaunchKernelGGL((conv_cin1_x4_kernel<4, LP, RO, LP, PK>), g, dim3(256), 0, st, a);
                     } else {
@@ -1818,5 +1838,13 @@ extern "C" int ldm_conv_forward(const ldm_conv_desc* d, const ldm_conv_plan* pla
 extern "C" int ldm_set_cin1_packed(int on) {
     const int prev = ldm::g_cin1_packed;
     ldm::g_cin1_packed = on ? 1 : 0;
+    return prev;
+}
+
+// A/B switch of the Cin = 1 kernel's stride-1 form (conv_cin1_x4_kernel<3, ..., SD = 1> against conv_cin1_kernel,
+// compared bitwise in tests/test_gpu_store16.py); returns the previous setting
+extern "C" int ldm_set_cin1_s1(int on) {
+    const int prev = ldm::g_cin1_s1;
+    ldm::g_cin1_s1 = on ? 1 : 0;
     return prev;
 }

@@ -316,3 +316,41 @@ def test_conv_bias_grad_from_batchnorm_dx_sum(cuda, store16, monkeypatch):
         assert float((got - want).abs().max()) <= 1e-5 * scale, (flag, float((got - want).abs().max()), scale)
         res.append(took)
     assert res[0] > 0 and res[1] == 0
+
+
+@pytest.mark.parametrize("dt", [0, 2])
+@pytest.mark.parametrize("cout", [32, 64])
+def test_cin1_stride1_form_is_bitwise_the_pixel_kernel(cuda, cout, dt):
+    """The Cin = 1, k3, stride-1 conv (the UNet's first layer on the raw mel, UNet(1, 1) at shape S;
+    models/model.py:178 Conv2d(in_channels, num_filters, 3, 1, 1)) on conv_cin1_x4_kernel's stride-1 form (four
+    output columns per lane from one 3 x 6 window) against conv_cin1_kernel (one lane per pixel), bitwise, with the
+    packed and scalar channel walks, fp32 and bf16 operands; the fp32 form against float64 torch (1e-5); and a width
+    that is not a multiple of 4 (the pixel kernel) against float64 torch."""
+    from ldm_amd import _lib as L, ops
+    import torch.nn.functional as F
+    lib = L.load()
+    x = _rand((2, 1, 64, 256), 71).to(cuda)
+    w = _rand((cout, 1, 3, 3), 72, -0.3, 0.3).to(cuda)
+    b = _rand((cout,), 73, -0.1, 0.1).to(cuda)
+    kw = dict(stride=1, padding=1, act="relu", dtype=dt)
+    outs = []
+    prev_s1, prev_pk = lib.ldm_set_cin1_s1(0), lib.ldm_set_cin1_packed(1)
+    try:
+        for s1, pk in ((0, 1), (1, 0), (1, 1)):
+            lib.ldm_set_cin1_s1(s1)
+            lib.ldm_set_cin1_packed(pk)
+            outs.append(ops.conv_forward(x, w, b, **kw))
+            torch.cuda.synchronize()
+    finally:
+        lib.ldm_set_cin1_s1(prev_s1)
+        lib.ldm_set_cin1_packed(prev_pk)
+    for y in outs[1:]:
+        assert torch.equal(y, outs[0]), float((y.float() - outs[0].float()).abs().max())
+    if dt == 0:
+        y64 = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), stride=1, padding=1))
+        assert float((outs[-1].cpu().double() - y64).abs().max()) <= 1e-5 * float(y64.abs().max())
+        xr = _rand((2, 1, 20, 130), 74).to(cuda)   # Wout = 130: not a multiple of 4
+        yr = ops.conv_forward(xr, w, b, **kw)
+        torch.cuda.synchronize()
+        y64 = torch.relu(F.conv2d(xr.cpu().double(), w.cpu().double(), b.cpu().double(), stride=1, padding=1))
+        assert float((yr.cpu().double() - y64).abs().max()) <= 1e-5 * float(y64.abs().max())
