@@ -231,6 +231,11 @@ int ldm_set_cin1_packed(int on);
  * the raw mel, UNet(1, 1) at shape S; models/model.py:178 Conv2d(in_channels, num_filters, 3, 1, 1)) against the one-lane-per-pixel
  * kernel, bitwise the same results: 1 on, 0 off; returns the previous setting.  Default: LDM_CIN1_S1. */
 int ldm_set_cin1_s1(int on);
+/* A/B switch of the flash attention forward's key splits over blocks (flash.hip: where one block per (query tile,
+ * head) fills under a quarter of the CUs — CA1 at shape S — the key tiles split over up to 4 blocks and a combine pass
+ * merges their (O, m, l); CrossAttention, models/model.py:126-160): 1 on, 0 off; returns the previous setting.
+ * Default: LDM_FLASH_SPLIT. */
+int ldm_set_flash_split(int on);
 /* A conv (descriptor d, weight w_conv [Cout,Cmid,kh,kw], bias b_conv or NULL) applied to the output of a
  * Linear/1x1 projection (w_proj [Cmid,Cin], b_proj [Cmid]) as ONE conv: w_out [Cout,Cin,kh,kw] =
  * w_conv o w_proj and pos_bias_out [Cout,Hout,Wout] = b_conv + the projection bias through the taps that

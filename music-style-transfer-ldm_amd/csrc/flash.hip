@@ -136,10 +136,15 @@ __device__ __forceinline__ void load_qfrag(const float* __restrict__ base, int E
 // group stages its own tiles), and the groups' (m, l, O) meet in LDS at the end (O = sum_g e^(m_g - M) O_g over the
 // same sum of l_g): KH waves per SIMD where the grid has one block per CU.  NBUF: K / V buffers per group (1: the
 // next tile is stored after a barrier that closes the current one; the D = 128, KH = 2 form needs it to fit LDS).
-template <int D, bool TOK, bool LSE, bool VEC, int KH, int NBUF>
+//
+// SPL (round 6): the key tiles split over gridDim.y blocks as well (fewer (query tile, head) blocks than a quarter of
+// the CUs: CA1 at shape S, L = S = 1024, d = 128, 64 blocks).  Each block leaves its unnormalised O, m and l in the
+// workspace `part` ([split][B heads][L] rows of D + 4: O, m, l) and flash_combine_kernel merges the splits in split order.
+template <int D, bool TOK, bool LSE, bool VEC, int KH, int NBUF, bool SPL = false>
 __global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __restrict__ q, const float* __restrict__ kv,
                                                         float* __restrict__ out, float* __restrict__ lse, int E,
-                                                        int heads, int L, int S, float scale) {
+                                                        int heads, int L, int S, float scale,
+                                                        float* __restrict__ part = nullptr) {
     constexpr int NJ = D / 16;
     extern __shared__ __attribute__((aligned(16))) float smem_all[];   // KH x NBUF x {K [D][kKP], V [D][kKP]}
     const int nqt = (L + kTok - 1) / kTok;
@@ -170,8 +175,12 @@ __global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __rest
     // then tile t+2's loads are issued; one barrier per tile.  (Round 6: the single-buffered form waited out
     // a load round trip per 64-key tile, 364 us per launch at L = S = 4096.)
     const int ntall = (S + kTok - 1) / kTok;
-    const int ntg = (ntall + KH - 1) / KH;                // tiles per key group (the last group may have fewer)
-    const int tb = kg * ntg, nt = min(ntall - tb, ntg);   // this group's first tile and its count (<= 0: none)
+    // SPL: this block's contiguous range of tiles [sb, sb + nts) (the last split may have fewer, or none)
+    const int tps = SPL ? (ntall + (int)gridDim.y - 1) / (int)gridDim.y : ntall;
+    const int sb = SPL ? (int)blockIdx.y * tps : 0;
+    const int nts = SPL ? max(0, min(ntall - sb, tps)) : ntall;
+    const int ntg = (nts + KH - 1) / KH;                  // tiles per key group (the last group may have fewer)
+    const int tb = sb + kg * ntg, nt = min(sb + nts - tb, ntg);   // this group's first tile and its count (<= 0: none)
     float4 rk[cs_pieces<D>()], rv[cs_pieces<D>()];
     if (nt > 0) {
         load_cs<D, VEC>(kb, S, tb * kTok, rk, gtid);
@@ -297,6 +306,14 @@ __global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __rest
         }
     }
     if (!lok) return;
+    if constexpr (SPL) {   // unnormalised O[l][16 ct + 4 lg + r], then m and l (lane group 0)
+        const int BH = (int)gridDim.x / nqt;
+        float* pb = part + (((size_t)blockIdx.y * BH + bh) * L + l) * (D + 4);
+#pragma unroll
+        for (int ct = 0; ct < NJ; ++ct) *reinterpret_cast<floatx4*>(pb + 16 * ct + 4 * lg) = o[ct];
+        if (lg == 0) *reinterpret_cast<float2*>(pb + D) = make_float2(m, lsum);
+        return;
+    }
     // lane holds O[l][c] for c = 16 ct + 4 lg + r
     if constexpr (TOK) {
         float* ob = out + ((size_t)b * L + l) * E + (size_t)h * D + 4 * lg;
@@ -312,6 +329,89 @@ __global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __rest
             for (int r = 0; r < 4; ++r) ob[(size_t)(16 * ct + r) * L] = o[ct][r] / lsum;
     }
     if (LSE && lg == 0) lse[(size_t)bh * L + l] = m + logf(lsum);
+}
+
+// Merge of the key splits (SPL), token-major outputs: per (b, h, l) M = max m_i, w_i = e^(m_i - M) (0 for a split with no keys),
+// O = sum_i w_i O_i / sum_i w_i l_i, folded in split order (the KH groups' merge, over blocks).  Thread = 4 channels of
+// one query row: rows fastest for channel-major outputs (coalesced along L), channels fastest for token-major.
+template <int D, bool TOK, bool LSE>
+__global__ __launch_bounds__(256) void flash_combine_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                            float* __restrict__ lse, int nsp, int BH, int E, int heads,
+                                                            int L) {
+    constexpr int C4 = D / 4, P = D + 4;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)BH * L * C4) return;
+    int bh, l, c4;
+    if constexpr (TOK) {
+        c4 = (int)(i % C4);
+        const int64_t r = i / C4;
+        l = (int)(r % L), bh = (int)(r / L);
+    } else {
+        l = (int)(i % L);
+        const int64_t r = i / L;
+        c4 = (int)(r % C4), bh = (int)(r / C4);
+    }
+    const size_t split_stride = (size_t)BH * L * P;
+    const float* pr = part + ((size_t)bh * L + l) * P;
+    float M = -INFINITY;
+    for (int s = 0; s < nsp; ++s) M = fmaxf(M, pr[s * split_stride + D]);
+    floatx4 o = {0.f, 0.f, 0.f, 0.f};
+    float lsum = 0.f;
+    for (int s = 0; s < nsp; ++s) {
+        const float* ps = pr + s * split_stride;
+        const float ms = ps[D];
+        const float w = ms == -INFINITY ? 0.f : expf(ms - M);
+        o = o + w * *reinterpret_cast<const floatx4*>(ps + 4 * c4);
+        lsum = lsum + w * ps[D + 1];
+    }
+    const int h = bh % heads, b = bh / heads, c = 4 * c4;
+    if constexpr (TOK) {
+        *reinterpret_cast<float4*>(out + ((size_t)b * L + l) * E + (size_t)h * D + c) =
+            make_float4(o[0] / lsum, o[1] / lsum, o[2] / lsum, o[3] / lsum);
+    } else {
+        float* ob = out + ((size_t)b * E + (size_t)h * D + c) * L + l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ob[(size_t)r * L] = o[r] / lsum;
+    }
+    if (LSE && c4 == 0) lse[(size_t)bh * L + l] = M + logf(lsum);
+}
+
+// The channel-major form: a block merges 16 query rows x D channels (threads along the channels of a row: the
+// partial rows read whole), parks O / l in LDS and writes it along L (out [B, E, L]).  Same arithmetic per output.
+template <int D, bool LSE>
+__global__ __launch_bounds__(256) void flash_combine_cm_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                               float* __restrict__ lse, int nsp, int BH, int E,
+                                                               int heads, int L) {
+    constexpr int C4 = D / 4, P = D + 4, RB = 16;   // (64 rows: 64 blocks at CA1's shape S, 21 us; 16: 256 blocks)
+    __shared__ float tile[D][RB + 1];
+    const int bh = (int)blockIdx.y, l0 = (int)blockIdx.x * RB;
+    const size_t split_stride = (size_t)BH * L * P;
+    for (int it = (int)threadIdx.x; it < RB * C4; it += 256) {
+        const int lr = it / C4, c4 = it % C4, l = l0 + lr;
+        if (l >= L) continue;
+        const float* pr = part + ((size_t)bh * L + l) * P;
+        float M = -INFINITY;
+        for (int s = 0; s < nsp; ++s) M = fmaxf(M, pr[s * split_stride + D]);
+        floatx4 o = {0.f, 0.f, 0.f, 0.f};
+        float lsum = 0.f;
+        for (int s = 0; s < nsp; ++s) {
+            const float* ps = pr + s * split_stride;
+            const float ms = ps[D];
+            const float w = ms == -INFINITY ? 0.f : expf(ms - M);
+            o = o + w * *reinterpret_cast<const floatx4*>(ps + 4 * c4);
+            lsum = lsum + w * ps[D + 1];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tile[4 * c4 + r][lr] = o[r] / lsum;
+        if (LSE && c4 == 0) lse[(size_t)bh * L + l] = M + logf(lsum);
+    }
+    __syncthreads();
+    const int h = bh % heads, b = bh / heads;
+    float* ob = out + ((size_t)b * E + (size_t)h * D) * L;
+    for (int it = (int)threadIdx.x; it < D * RB; it += 256) {
+        const int c = it / RB, lr = it % RB, l = l0 + lr;
+        if (l < L) ob[(size_t)c * L + l] = tile[c][lr];
+    }
 }
 
 // ---- backward ----------------------------------------------------------------------------------------
@@ -545,16 +645,73 @@ static int flash_kh(int64_t blocks, int ntiles) {
     return blocks <= 256 && ntiles >= 2 ? 2 : 1;
 }
 
+// key splits over blocks (flash_fwd_kernel's SPL): doubled while the grid stays within 256 blocks and every split
+// keeps 4 key tiles or more; g_flash_split = 0 (LDM_FLASH_SPLIT=0, ldm_set_flash_split(0)) keeps one block per
+// (query tile, head)
+static int g_flash_split = [] {
+    const char* e = std::getenv("LDM_FLASH_SPLIT");
+    return e ? std::atoi(e) : 1;
+}();
+// (LDM_FLASH_SPLIT = 8, A/B timing: up to 8 splits within 512 blocks, 2 tiles per split)
+static int flash_splits(int64_t blocks, int ntiles) {
+    if (!g_flash_split) return 1;
+    const bool wide = g_flash_split == 8;
+    const int maxsp = wide ? 8 : 4, maxb = wide ? 512 : 256, mint = wide ? 2 : 4;
+    int nsp = 1;
+    while (nsp < maxsp && blocks * 2 * nsp <= maxb && ntiles / (2 * nsp) >= mint) nsp *= 2;
+    return nsp;
+}
+
+// The splits' workspace: one device buffer per device, grown (never freed: a captured graph may still hold the
+// old one) outside stream capture only; nullptr when a capture would need it to grow (the caller runs unsplit).
+static float* split_workspace(size_t floats, hipStream_t st) {
+    static float* buf[64];
+    static size_t cap[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (cap[dev] >= floats) return buf[dev];
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    float* p = nullptr;
+    if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    buf[dev] = p;
+    cap[dev] = floats;
+    return p;
+}
+
 template <int D, bool TOK, bool LSE, bool VEC, int KH>
 static int fwd_launch_k(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
-                        float scale, hipStream_t st) {
+                        float scale, int nsp, hipStream_t st) {
     constexpr int NBUF = (KH == 2 && D == 128) ? 1 : 2;   // (D = 128 with two groups: one buffer each fits LDS)
     const size_t lds = (size_t)KH * NBUF * 2 * D * kKP * sizeof(float);
+    const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
+    float* part = nullptr;
+    if (nsp > 1) part = split_workspace((size_t)nsp * B * heads * L * (D + 4), st);
+    if (part) {
+        static int opted_s = opt_in_lds(flash_fwd_kernel<D, TOK, false, VEC, KH, NBUF, true>, lds);
+        if (opted_s) return opted_s;
+        hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, false, VEC, KH, NBUF, true>), dim3(grid, (unsigned)nsp), dim3(256 * KH),
+                           lds, st, q, kv, out, nullptr, E, heads, L, S, scale, part);
+        LDM_CHECK_LAUNCH("flash_fwd_kernel (key splits)");
+        if constexpr (TOK) {
+            const int64_t n = (int64_t)B * heads * L * (D / 4);
+            hipLaunchKernelGGL((flash_combine_kernel<D, TOK, LSE>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                               part, out, lse, nsp, B * heads, E, heads, L);
+            LDM_CHECK_LAUNCH("flash_combine_kernel");
+        } else {
+            hipLaunchKernelGGL((flash_combine_cm_kernel<D, LSE>), dim3((unsigned)((L + 15) / 16), (unsigned)(B * heads)),
+                               dim3(256), 0, st, part, out, lse, nsp, B * heads, E, heads, L);
+            LDM_CHECK_LAUNCH("flash_combine_cm_kernel");
+        }
+        return 0;
+    }
     static int opted = opt_in_lds(flash_fwd_kernel<D, TOK, LSE, VEC, KH, NBUF>, lds);
     if (opted) return opted;
-    const unsigned grid = (unsigned)B * heads * ((L + kTok - 1) / kTok);
     hipLaunchKernelGGL((flash_fwd_kernel<D, TOK, LSE, VEC, KH, NBUF>), dim3(grid), dim3(256 * KH), lds, st, q, kv, out,
-                       lse, E, heads, L, S, scale);
+                       lse, E, heads, L, S, scale, nullptr);
     LDM_CHECK_LAUNCH("flash_fwd_kernel");
     return 0;
 }
@@ -563,13 +720,15 @@ template <int D, bool TOK, bool LSE>
 static int fwd_launch(const float* q, const float* kv, float* out, float* lse, int B, int E, int heads, int L, int S,
                       float scale, hipStream_t st) {
     const int64_t blocks = (int64_t)B * heads * ((L + kTok - 1) / kTok);
-    const int kh = flash_kh(blocks, (S + kTok - 1) / kTok);
+    const int ntiles = (S + kTok - 1) / kTok;
+    const int nsp = flash_splits(blocks, ntiles);
+    const int kh = flash_kh(blocks * nsp, (ntiles + nsp - 1) / nsp);
     if (S % 4 == 0) {
-        if (kh == 2) return fwd_launch_k<D, TOK, LSE, true, 2>(q, kv, out, lse, B, E, heads, L, S, scale, st);
-        return fwd_launch_k<D, TOK, LSE, true, 1>(q, kv, out, lse, B, E, heads, L, S, scale, st);
+        if (kh == 2) return fwd_launch_k<D, TOK, LSE, true, 2>(q, kv, out, lse, B, E, heads, L, S, scale, nsp, st);
+        return fwd_launch_k<D, TOK, LSE, true, 1>(q, kv, out, lse, B, E, heads, L, S, scale, nsp, st);
     }
-    if (kh == 2) return fwd_launch_k<D, TOK, LSE, false, 2>(q, kv, out, lse, B, E, heads, L, S, scale, st);
-    return fwd_launch_k<D, TOK, LSE, false, 1>(q, kv, out, lse, B, E, heads, L, S, scale, st);
+    if (kh == 2) return fwd_launch_k<D, TOK, LSE, false, 2>(q, kv, out, lse, B, E, heads, L, S, scale, nsp, st);
+    return fwd_launch_k<D, TOK, LSE, false, 1>(q, kv, out, lse, B, E, heads, L, S, scale, nsp, st);
 }
 
 template <int D>
@@ -627,6 +786,14 @@ int attention_flash(const float* q, const float* kv, float* out, float* lse, int
 }  // namespace ldm
 
 using namespace ldm;
+
+// A/B switch of the flash forward's key splits over blocks (bitwise-stable per setting; tests compare the two within
+// fp32 rounding); returns the previous setting
+extern "C" int ldm_set_flash_split(int on) {
+    const int prev = fa::g_flash_split;
+    fa::g_flash_split = on ? (on == 8 ? 8 : 1) : 0;
+    return prev;
+}
 
 extern "C" int ldm_attention_forward_lse(const float* q, const float* kv, float* out, float* lse, int32_t B, int32_t E,
                                          int32_t heads, int32_t L, int32_t S, float scale, void* stream) {

@@ -157,6 +157,7 @@ SIGNATURES = {
     "ldm_ca1_probs_form": (c_int32, []),
     "ldm_set_cin1_packed": (c_int32, [c_int32]),
     "ldm_set_cin1_s1": (c_int32, [c_int32]),
+    "ldm_set_flash_split": (c_int32, [c_int32]),
     "ldm_q_sample": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_predict_start": (c_int32, [c_fp, c_fp, c_fp, c_int32, c_vp, c_fp, c_int32, c_int64, c_vp]),
     "ldm_sched_backward": (c_int32, [c_int32, c_fp, c_fp, c_int32, c_vp, c_fp, c_fp, c_int32, c_int64, c_vp]),

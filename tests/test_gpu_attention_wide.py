@@ -47,7 +47,10 @@ def _ref_attn(q, kv, heads):
 
 CASES = {"ca2_w128": (2, 256, 128, 128), "ca1_ragged": (2, 512, 40, 200), "ca2_ragged": (1, 256, 100, 77),
          "ca2_long": (1, 256, 1024, 1024), "ca1_256": (1, 512, 256, 256), "s_gt_64_l_small": (3, 256, 16, 130),
-         "one_key_tile": (2, 256, 70, 40)}   # S <= 64: the double-buffered K/V loop's single-tile path
+         "one_key_tile": (2, 256, 70, 40),   # S <= 64: the double-buffered K/V loop's single-tile path
+         # key splits over blocks (flash_combine_kernel): CA1 at shape S (d = 128, 4 splits), ragged S with 13
+         # tiles over 2 splits (S % 4 == 0), and S % 4 != 0 over 4 splits
+         "ca1_shape_s": (1, 512, 1024, 1024), "split_13_tiles": (1, 256, 200, 800), "split_ragged": (1, 512, 130, 1001)}
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
@@ -65,6 +68,41 @@ def test_flash_forward(cuda, case):
     assert rel_err(npy(out), ref.numpy()) < TOL
     assert torch.equal(out, out2)
     assert rel_err(npy(lse), lse_ref.numpy()) < 1e-5
+
+
+SPLIT = ("ca2_long", "ca1_shape_s", "split_13_tiles", "split_ragged")
+
+
+@pytest.mark.parametrize("case", SPLIT)
+def test_flash_key_splits_match_one_block(cuda, case):
+    """The forward with its key tiles split over blocks and merged by flash_combine_kernel against the one-block-per-
+    (query tile, head) form (ldm_set_flash_split): O and lse within fp32 rounding of each other (the merge re-groups
+    the sums: 1e-5 relative), both within the float64 bound (channel-major, the per-layer path's layout)."""
+    from ldm_amd import _lib as L, ops
+    B, E, Lq, S = CASES[case]
+    g = torch.Generator().manual_seed(Lq * 5 + S)
+    q = torch.randn(B, E, Lq, generator=g).to(cuda)
+    kv = torch.randn(B, 2 * E, S, generator=g).to(cuda)
+    lib = L.load()
+    res = {}
+    prev = lib.ldm_set_flash_split(1)
+    try:
+        for sp in (0, 1, 8):   # 8: the A/B form with up to 8 splits
+            lib.ldm_set_flash_split(sp)
+            o, lse = ops.attention_forward_lse(q, kv, 4)
+            o2 = ops.attention_core(q, kv, 4)
+            torch.cuda.synchronize()
+            assert torch.equal(o, o2)
+            res[sp] = (o, lse)
+    finally:
+        lib.ldm_set_flash_split(prev)
+    ref, lse_ref = _ref_attn(q.cpu().double(), kv.cpu().double(), 4)
+    for sp in (0, 1, 8):
+        assert rel_err(npy(res[sp][0]), ref.numpy()) < TOL
+        assert rel_err(npy(res[sp][1]), lse_ref.numpy()) < 1e-5
+    for sp in (1, 8):
+        assert rel_err(npy(res[sp][0]), npy(res[0][0])) < 1e-5
+        assert rel_err(npy(res[sp][1]), npy(res[0][1])) < 1e-6
 
 
 BWD = {"ca2_w128": (2, 256, 128, 128), "ca1_ragged": (1, 512, 96, 200), "ca2_ragged": (2, 256, 70, 33)}
