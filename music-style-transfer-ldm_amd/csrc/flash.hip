@@ -331,26 +331,19 @@ __global__ __launch_bounds__(256 * KH) void flash_fwd_kernel(const float* __rest
     if (LSE && lg == 0) lse[(size_t)bh * L + l] = m + logf(lsum);
 }
 
-// Merge of the key splits (SPL), token-major outputs: per (b, h, l) M = max m_i, w_i = e^(m_i - M) (0 for a split with no keys),
-// O = sum_i w_i O_i / sum_i w_i l_i, folded in split order (the KH groups' merge, over blocks).  Thread = 4 channels of
-// one query row: rows fastest for channel-major outputs (coalesced along L), channels fastest for token-major.
-template <int D, bool TOK, bool LSE>
+// Merge of the key splits (SPL), token-major outputs: per (b, h, l) M = max m_i, w_i = e^(m_i - M) (0 for a split with
+// no keys), O = sum_i w_i O_i / sum_i w_i l_i, folded in split order (the KH groups' merge, over blocks).  Thread = 4
+// channels of one query row, channels fastest (reads and writes both along the row).
+template <int D, bool LSE>
 __global__ __launch_bounds__(256) void flash_combine_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                             float* __restrict__ lse, int nsp, int BH, int E, int heads,
                                                             int L) {
     constexpr int C4 = D / 4, P = D + 4;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)BH * L * C4) return;
-    int bh, l, c4;
-    if constexpr (TOK) {
-        c4 = (int)(i % C4);
-        const int64_t r = i / C4;
-        l = (int)(r % L), bh = (int)(r / L);
-    } else {
-        l = (int)(i % L);
-        const int64_t r = i / L;
-        c4 = (int)(r % C4), bh = (int)(r / C4);
-    }
+    const int c4 = (int)(i % C4);
+    const int64_t r = i / C4;
+    const int l = (int)(r % L), bh = (int)(r / L);
     const size_t split_stride = (size_t)BH * L * P;
     const float* pr = part + ((size_t)bh * L + l) * P;
     float M = -INFINITY;
@@ -365,14 +358,8 @@ __global__ __launch_bounds__(256) void flash_combine_kernel(const float* __restr
         lsum = lsum + w * ps[D + 1];
     }
     const int h = bh % heads, b = bh / heads, c = 4 * c4;
-    if constexpr (TOK) {
-        *reinterpret_cast<float4*>(out + ((size_t)b * L + l) * E + (size_t)h * D + c) =
-            make_float4(o[0] / lsum, o[1] / lsum, o[2] / lsum, o[3] / lsum);
-    } else {
-        float* ob = out + ((size_t)b * E + (size_t)h * D + c) * L + l;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ob[(size_t)r * L] = o[r] / lsum;
-    }
+    *reinterpret_cast<float4*>(out + ((size_t)b * L + l) * E + (size_t)h * D + c) =
+        make_float4(o[0] / lsum, o[1] / lsum, o[2] / lsum, o[3] / lsum);
     if (LSE && c4 == 0) lse[(size_t)bh * L + l] = M + logf(lsum);
 }
 
@@ -662,24 +649,39 @@ static int flash_splits(int64_t blocks, int ntiles) {
     return nsp;
 }
 
-// The splits' workspace: one device buffer per device, grown (never freed: a captured graph may still hold the
-// old one) outside stream capture only; nullptr when a capture would need it to grow (the caller runs unsplit).
+// The splits' workspace: per device one buffer of kLanes lanes, each stream that launches a split forward owning a
+// lane (assigned on first use, inside a capture too: no allocation needed), so launches on two streams (concurrent
+// sub-batch chains, a captured graph beside its eager warm-up) never share partials, and launches on one stream are
+// ordered.  The buffer grows (never freed: a captured graph may still hold the old one) outside stream capture only;
+// nullptr — the caller then runs unsplit — when a capture would need it to grow or the lanes are all taken.
 static float* split_workspace(size_t floats, hipStream_t st) {
-    static float* buf[64];
-    static size_t cap[64];
+    constexpr int kLanes = 8, kDev = 16;
+    static float* buf[kDev];
+    static size_t cap[kDev];   // floats per lane
+    static hipStream_t lane_st[kDev][kLanes];
+    static int lanes[kDev];
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    if (cap[dev] >= floats) return buf[dev];
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    float* p = nullptr;
-    if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDev) return nullptr;
+    int lane = -1;
+    for (int i = 0; i < lanes[dev]; ++i)
+        if (lane_st[dev][i] == st) lane = i;
+    if (lane < 0) {
+        if (lanes[dev] == kLanes) return nullptr;
+        lane = lanes[dev]++;
+        lane_st[dev][lane] = st;
     }
-    buf[dev] = p;
-    cap[dev] = floats;
-    return p;
+    if (cap[dev] < floats) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        float* p = nullptr;
+        if (hipMalloc(&p, floats * kLanes * sizeof(float)) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        buf[dev] = p;
+        cap[dev] = floats;
+    }
+    return buf[dev] + (size_t)lane * cap[dev];
 }
 
 template <int D, bool TOK, bool LSE, bool VEC, int KH>
@@ -698,7 +700,7 @@ static int fwd_launch_k(const float* q, const float* kv, float* out, float* lse,
         LDM_CHECK_LAUNCH("flash_fwd_kernel (key splits)");
         if constexpr (TOK) {
             const int64_t n = (int64_t)B * heads * L * (D / 4);
-            hipLaunchKernelGGL((flash_combine_kernel<D, TOK, LSE>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+            hipLaunchKernelGGL((flash_combine_kernel<D, LSE>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                                part, out, lse, nsp, B * heads, E, heads, L);
             LDM_CHECK_LAUNCH("flash_combine_kernel");
         } else {

@@ -163,6 +163,36 @@ def test_ddim_wide_latent(g3, cuda):
     assert rel_err(npy(x), g3["w128_ddim5_x"]) < TOL
 
 
+def test_unet_engine_key_splits_token_major(cuda):
+    """The fused engine's token-major flash attention with its key tiles split over blocks (flash_combine_kernel): the
+    UNet on a [1,32,16,512] latent (CA2 over 512 tokens: 32 blocks, 2 splits) through the engine (no grad) against the
+    per-layer autograd path (channel-major attention, merged by flash_combine_cm_kernel) and against the engine with
+    the splits off (ldm_set_flash_split(0)); 1e-5 relative to each other (fp32 regroupings only)."""
+    from ldm_amd import _lib as L
+    u = _unet(102, 32).to(cuda)
+    z = torch.from_numpy(recipe.normal((1, 32, 16, 512), 780)).to(cuda)
+    s5 = torch.from_numpy(recipe.uniform01((1, 256, 4, 128), 781)).to(cuda)
+    s6 = torch.from_numpy(recipe.uniform01((1, 512, 2, 64), 782)).to(cuda)
+    t = torch.tensor([321], device=cuda)
+    emb = {"s5": s5, "s6": s6}
+    lib = L.load()
+    prev = lib.ldm_set_flash_split(1)
+    try:
+        with torch.no_grad():
+            y_eng = u(z, t, emb)
+        with torch.enable_grad():
+            y_layer = u(z, t, emb).detach()
+        lib.ldm_set_flash_split(0)
+        with torch.no_grad():
+            y_one = u(z, t, emb)
+        torch.cuda.synchronize()
+    finally:
+        lib.ldm_set_flash_split(prev)
+    assert torch.isfinite(y_eng).all()
+    assert rel_err(npy(y_eng), npy(y_one)) < 1e-5
+    assert rel_err(npy(y_eng), npy(y_layer)) < 1e-5
+
+
 @pytest.mark.parametrize("grad", [False, True])
 def test_unet_shape_s_reduced(g3, cuda, grad):
     """UNet(1, 1, 64) directly on a [1,1,64,256] mel (SURVEY §0.4 shape S, reduced 2x per side)."""
